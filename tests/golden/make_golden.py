@@ -1,0 +1,227 @@
+"""Generate golden vectors by running the REFERENCE implementation.
+
+Run in the build container only (the reference is not present on GPU boxes):
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+It imports the reference's own modules from /root/reference
+(enflow.nn.egcl.EGCL, enflow.nn.argmax.ArgMax, enflow.flow.dynamics.LFIntegrator,
+enflow.flow.loss.Alchemical_NLL, enflow.utils.helpers) and runs them in
+float64 on synthetic molecules.  ``enflow.data.base`` cannot be imported (its
+import chain needs rdkit, which is absent), so ``RefData`` below restates the
+batch container's edge / pbc / iteration behaviour (enflow/data/base.py:9-144)
+around the reference's own ``get_periodic_images_within`` and ``apply_pbc``.
+
+All inputs are float32-representable (weights come from torch's float32
+nn.Linear init; positions etc. are rounded through float32) so the fp32 HIP
+path sees bit-identical inputs.  Inputs are stored as float32, reference
+outputs as float64, in one .npz per case.
+"""
+import os
+import sys
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+sys.path.insert(0, "/root/reference")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from enflow.nn.egcl import EGCL  # noqa: E402  (reference)
+from enflow.nn.argmax import ArgMax  # noqa: E402  (reference)
+from enflow.flow.dynamics import LFIntegrator  # noqa: E402  (reference)
+from enflow.flow.loss import Alchemical_NLL  # noqa: E402  (reference)
+from enflow.utils import helpers  # noqa: E402  (reference)
+
+from enflow_amd.data.synthetic import make_molecules, default_dt, default_kBT  # noqa: E402
+
+
+class RefEdges:
+    """Restates enflow/data/base.py:9-19 (Edges)."""
+
+    def __init__(self, edge_index, box, coord):
+        self.box = box
+        self.row, self.col = edge_index
+        self.coord = coord
+
+    @property
+    def coord_diff(self):
+        d = self.coord[self.row] - self.coord[self.col]
+        return helpers.apply_pbc(d, self.box * 0.5)
+
+
+class RefData:
+    """Restates the parts of enflow/data/base.py:21-144 (Data) the flow uses."""
+
+    def __init__(self, h, g, pos, vel, box, r_cut, N):
+        self.h, self.g, self.pos, self.vel = h, g, pos, vel
+        self.box, self.r_cut, self.N = box, r_cut, N
+
+    def _mol(self, i):
+        s = int(self.N[:i].sum())
+        e = s + int(self.N[i])
+        return RefData(self.h[s:e], self.g[s:e], self.pos[s:e], self.vel[s:e],
+                       self.box[s:e], self.r_cut[i], self.N[i])
+
+    def __iter__(self):
+        return (self._mol(i) for i in range(len(self.N)))
+
+    @property
+    def num_atoms(self):
+        return int(self.N.sum())
+
+    @property
+    def num_mols(self):
+        return len(self.N)
+
+    def pbc(self):
+        self.pos = helpers.apply_pbc(self.pos, self.box)
+
+    @property
+    def edges(self):
+        edge_index = torch.empty((2, 0), dtype=torch.long)
+        boxes = []
+        n_cnt = 0
+        for mol in self:
+            box = mol.box[0]
+            imgs, id_mapping = helpers.get_periodic_images_within(mol.pos, box, mol.r_cut)
+            r_sq = mol.r_cut * mol.r_cut
+            d2 = (imgs.unsqueeze(1) - mol.pos).pow(2).sum(dim=2)
+            ids = (d2 < r_sq).nonzero()
+            e = id_mapping[ids] + n_cnt
+            e = e[torch.nonzero(e[:, 0] - e[:, 1])].squeeze(1)
+            boxes.append(box.repeat(e.shape[0], 1))
+            edge_index = torch.cat((edge_index, e.T.long()), dim=1)
+            n_cnt += int(mol.N)
+        return RefEdges(edge_index, torch.cat(boxes), self.pos)
+
+
+def f32(x):
+    return np.asarray(x, dtype=np.float32).astype(np.float64)
+
+
+def to_t(x):
+    return torch.tensor(x, dtype=torch.float64)
+
+
+def batch_inputs(num_mols, n_atoms, nf, seed, box_ang=None, r_cut_ang=3.0, one_hot=True):
+    b = make_molecules(num_mols, n_atoms, nf=nf, seed=seed, box_ang=box_ang, r_cut_ang=r_cut_ang)
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        b[k] = f32(b[k])
+    if not one_hot:
+        rng = np.random.default_rng(seed + 17)
+        b["h"] = f32(rng.normal(size=b["h"].shape))
+    return b
+
+
+def ref_data(b):
+    n = torch.tensor(np.diff(b["mol_ptr"]))
+    return RefData(to_t(b["h"]), to_t(b["g"]), to_t(b["pos"]), to_t(b["vel"]),
+                   to_t(b["box"]), to_t(b["r_cut"]), n)
+
+
+def params_of(module, prefix):
+    return {f"{prefix}{k}": v.detach().numpy().astype(np.float32)
+            for k, v in module.state_dict().items()}
+
+
+def save(name, inputs, outputs):
+    out = {}
+    for k, v in inputs.items():
+        v = np.asarray(v)
+        out["in_" + k] = v.astype(np.float32) if (v.dtype.kind == "f" and v.ndim > 0) else v
+    for k, v in outputs.items():
+        out["out_" + k] = np.asarray(v, dtype=np.float64) if np.asarray(v).dtype.kind == "f" else np.asarray(v)
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(f"wrote {path} ({os.path.getsize(path) // 1024} KiB)")
+
+
+def case_edges():
+    """Neighbour lists: default (extent) boxes, a large box, a small box."""
+    for tag, kw in (("extent", {}), ("box20", {"box_ang": 20.0}), ("box5", {"box_ang": 5.0})):
+        b = batch_inputs(6, [22, 9, 15, 3, 30, 22], 5, seed=11, **kw)
+        d = ref_data(b)
+        e = d.edges
+        save(f"edges_{tag}", b, {"row": e.row.numpy(), "col": e.col.numpy(),
+                                 "coord_diff": e.coord_diff.numpy()})
+
+
+def case_egcl(hid, seed):
+    torch.manual_seed(seed)
+    nf = 5
+    net = EGCL(nf, nf, hid).double()
+    b = batch_inputs(4, [22, 9, 15, 3], nf, seed=seed, one_hot=False)
+    d = ref_data(b)
+    q, f, g = net(d.h, d.edges)
+    inp = dict(b)
+    inp.update(params_of(net, "p0."))
+    save(f"egcl_h{hid}", inp, {"Q": q.detach().numpy(), "F": f.detach().numpy(),
+                               "G": g.detach().numpy()})
+
+
+def case_argmax(hid, seed):
+    torch.manual_seed(seed)
+    nf = 5
+    am = ArgMax(nf, hid).double()
+    b = batch_inputs(3, [22, 9, 15], nf, seed=seed)
+    h = to_t(b["h"])
+    torch.manual_seed(seed + 1)
+    z, log_q = am(h)
+    torch.manual_seed(seed + 1)
+    eps = torch.randn(h.size())
+    inp = {"h": b["h"], "mol_ptr": b["mol_ptr"], "eps": eps.numpy()}
+    inp.update(params_of(am, "dq."))
+    rev = am.reverse(z.detach())
+    save(f"argmax_h{hid}", inp, {"z": z.detach().numpy(), "log_q": float(log_q),
+                                 "reverse": rev.numpy()})
+
+
+def case_flow(hid, n_layers, sizes, seed, name):
+    torch.manual_seed(seed)
+    nf = 5
+    dt = default_dt()
+    nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+    model = LFIntegrator(nets, ArgMax(nf, hid), dt=dt)   # BaseFlow casts to float64
+    b = batch_inputs(len(sizes), sizes, nf, seed=seed)
+    d = ref_data(b)
+    torch.manual_seed(seed + 1)
+    eps = torch.randn(d.h.size())
+    torch.manual_seed(seed + 1)
+    with torch.no_grad():
+        out, ldj = model(d)
+    kBT = default_kBT()
+    nll = Alchemical_NLL(kBT=kBT, softening=0.1)
+    with torch.no_grad():
+        loss = nll(out, ldj)
+    fwd = {"h": out.h.numpy().copy(), "g": out.g.numpy().copy(), "pos": out.pos.numpy().copy(),
+           "vel": out.vel.numpy().copy(), "ldj": float(ldj), "nll": float(loss)}
+    # generate direction: reverse of the forward output (main.py:263-278)
+    with torch.no_grad():
+        back = model.reverse(out)
+    rev = {"rev_h": back.h.numpy(), "rev_g": back.g.numpy(), "rev_pos": back.pos.numpy(),
+           "rev_vel": back.vel.numpy()}
+    inp = dict(b)
+    inp["eps"] = eps.numpy()
+    inp["dt"] = np.array(dt)
+    inp["kBT"] = np.array(kBT)
+    inp["softening"] = np.array(0.1)
+    inp["n_layers"] = np.array(n_layers)
+    inp["hid"] = np.array(hid)
+    for i, net in enumerate(model.networks):
+        inp.update(params_of(net, f"p{i}."))
+    inp.update(params_of(model.dequantize, "dq."))
+    fwd.update(rev)
+    save(name, inp, fwd)
+
+
+if __name__ == "__main__":
+    case_edges()
+    case_egcl(32, 3)
+    case_egcl(128, 4)
+    case_argmax(32, 5)
+    case_flow(32, 3, [22, 9, 15, 3], 7, "lf_h32_L3")
+    case_flow(64, 2, [22, 22, 30], 8, "lf_h64_L2")
+    case_flow(128, 2, [22, 22], 9, "lf_h128_L2")
