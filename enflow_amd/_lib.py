@@ -1,0 +1,97 @@
+"""ctypes binding of the C ABI in include/enflow_hip.h (libenflow_hip.so).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).
+There is deliberately no fallback: if the shared object is missing or cannot
+be loaded every operator raises.
+"""
+import ctypes
+import os
+
+import torch
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libenflow_hip.so")
+
+ERR_TOO_MANY_ATOMS = 1
+ERR_FEW_IMAGES = 2
+ERR_TOO_MANY_FEATURES = 4
+DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
+
+_i, _i64, _f, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/enflow_hip.h one to one
+SIGNATURES = {
+    "enflow_abi_version": (_i, []),
+    "enflow_max_atoms": (_i, []),
+    "enflow_max_node_nf": (_i, []),
+    "enflow_supports_hidden": (_i, [_i]),
+    "enflow_egcl_packed_size": (_i64, [_i, _i]),
+    "enflow_argmax_packed_size": (_i64, [_i, _i]),
+    "enflow_pack_egcl_f32": (_i, [_p, _i, _i, _p, _p]),
+    "enflow_pack_argmax_f32": (_i, [_p, _i, _i, _p, _p]),
+    "enflow_lf_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p]),
+    "enflow_lf_reverse_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                   _i, _f, _f, _p, _p, _p, _p]),
+    "enflow_one_hot_f32": (_i, [_p, _i, _i, _p, _p]),
+    "enflow_egcl_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f,
+                                     _p, _p, _p, _p, _p]),
+    "enflow_argmax_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "enflow_neighbour_pairs_f32": (_i, [_i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
+    "enflow_alchemical_nll_f32": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f, _f, _f,
+                                       _p, _p, _p]),
+}
+
+_lib = None
+
+
+class HipPathError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise if it is unavailable."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HipPathError(
+                f"{LIB_PATH} is missing: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def check(rc, what):
+    if rc != 0:
+        raise HipPathError(f"{what} failed with code {rc}")
+
+
+def require_gpu(t):
+    if not (isinstance(t, torch.Tensor) and t.is_cuda):
+        raise HipPathError("the enflow_amd HIP path needs tensors on a ROCm GPU "
+                           "(there is no CPU fallback)")
+
+
+def raise_on_err(err_flag):
+    """Read the device error word (synchronises) and raise like the reference."""
+    e = int(err_flag.item())
+    if e & ERR_FEW_IMAGES:
+        raise IndexError("fewer periodic images than atoms in a molecule: the reference "
+                         "indexes id_mapping out of range here (enflow/data/base.py:137)")
+    if e & ERR_TOO_MANY_ATOMS:
+        raise HipPathError(f"molecule larger than {lib().enflow_max_atoms()} atoms")
+    if e & ERR_TOO_MANY_FEATURES:
+        raise HipPathError(f"node_nf larger than {lib().enflow_max_node_nf()}")

@@ -1,0 +1,1215 @@
+// enflow_flow.hip -- MI355X (gfx950, CDNA4) kernels for the enflow coupling flow.
+//
+// One workgroup (4 waves, 256 threads) owns one molecule for the WHOLE flow:
+// its coordinates, features, neighbour pairs and per-atom aggregates live in
+// LDS across all layers, so HBM sees each molecule once in and once out and the
+// only other global traffic is the (L2-resident) packed weights.
+//
+// Per layer (reference: enflow/flow/dynamics.py:10-37, enflow/nn/egcl.py:76-92,
+// enflow/data/base.py:122-144):
+//   1. periodic neighbour list -> unique (row, col, multiplicity) pairs in LDS
+//      (27-bit image mask per atom, wave ballots for the image->atom mapping,
+//      an N x N multiplicity matrix, block scan to compact);
+//   2. per 32-pair tile, one wave runs the three chained per-edge GEMMs
+//      (pair features -> edge_nn.0 -> edge_nn.2 -> coord_nn.0) on
+//      v_mfma_f32_32x32x2_f32 in "weights = A, activations = B" orientation: an
+//      accumulator tile is directly the next GEMM's B operand (lane = pair,
+//      registers = features), so the chain never leaves registers; the
+//      weight fragments are pre-packed (enflow_pack_egcl_f32) in exactly the
+//      permuted k order the accumulator layout produces;
+//   3. deterministic segment sums of the edge messages and forces into per-atom
+//      LDS rows (each row written by the one wave holding its first pair, plus
+//      one ordered fix-up per wave boundary);
+//   4. node MLP (node_nn.0 on MFMA, node_nn.2 and vel_scaling_nn on VALU);
+//   5. leapfrog update + pbc, log|detJ| accumulation.
+//
+// All arithmetic is float32; MFMA f32 is an exact fmaf chain.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#include "enflow_hip.h"
+
+#define ENFLOW_ABI 1
+#define WAVES 4
+#define BLOCK 256
+#define NFMAX 8
+#define NFP 9  // LDS row stride of h / g / G (odd -> conflict-free across atoms)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// layouts
+// ---------------------------------------------------------------------------
+// Row of the 32x32 f32 MFMA accumulator held by register r in lane half hh
+// (C/D map col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).
+__host__ __device__ constexpr int rho(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
+
+__host__ __device__ inline int node_ksteps(int H, int nf) { return (H + nf + 1) / 2; }
+
+struct EgclLayout {
+  int we1f, we2f, wc1f, wn1f, be1, be2, bc1, wc2, bn1, wn2, bn2, wv1t, bv1, wv2, bv2, total;
+};
+
+// Packed EGCL layer (floats).  *f sections are MFMA A-fragments.
+__host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
+  EgclLayout L;
+  int o = 0;
+  L.we1f = o; o += (H / 32) * (NFMAX + 1) * 64;      // [t][s<=NFMAX][lane]
+  L.we2f = o; o += H * H;                            // [tp][t][rg][lane][4]
+  L.wc1f = o; o += H * H;                            // [tp][t][rg][lane][4]
+  L.wn1f = o; o += (H / 32) * node_ksteps(H, nf) * 64; // [tp][s][lane]
+  L.be1 = o; o += H;
+  L.be2 = o; o += H;
+  L.bc1 = o; o += H;
+  L.wc2 = o; o += H;
+  L.bn1 = o; o += H;
+  L.wn2 = o; o += nf * H;                            // [q][k] (torch layout)
+  L.bn2 = o; o += NFMAX;
+  L.wv1t = o; o += nf * H;                           // [q][k]
+  L.bv1 = o; o += H;
+  L.wv2 = o; o += H;
+  L.bv2 = o; o += 4;
+  o = (o + 63) & ~63;
+  L.total = o;
+  return L;
+}
+
+struct RawEgcl {  // offsets into the raw (torch) concatenation
+  int We1, be1, We2, be2, Wn1, bn1, Wn2, bn2, Wc1, bc1, wc2, Wv1, bv1, Wv2, bv2, total;
+};
+__host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
+  RawEgcl R;
+  int o = 0;
+  R.We1 = o; o += H * (2 * nf + 1);
+  R.be1 = o; o += H;
+  R.We2 = o; o += H * H;
+  R.be2 = o; o += H;
+  R.Wn1 = o; o += H * (H + nf);
+  R.bn1 = o; o += H;
+  R.Wn2 = o; o += nf * H;
+  R.bn2 = o; o += nf;
+  R.Wc1 = o; o += H * H;
+  R.bc1 = o; o += H;
+  R.wc2 = o; o += H;
+  R.Wv1 = o; o += H * nf;
+  R.bv1 = o; o += H;
+  R.Wv2 = o; o += H;
+  R.bv2 = o; o += 1;
+  R.total = o;
+  return R;
+}
+
+struct AmLayout { int wa1t, ba1, wa2, ba2, total; };
+__host__ __device__ inline AmLayout argmax_layout(int H, int nf) {
+  AmLayout L;
+  int o = 0;
+  L.wa1t = o; o += nf * H;   // [q][k]
+  L.ba1 = o; o += H;
+  L.wa2 = o; o += 2 * nf * H; // [o][k] (torch layout)
+  L.ba2 = o; o += 2 * NFMAX;
+  o = (o + 63) & ~63;
+  L.total = o;
+  return L;
+}
+
+// ---------------------------------------------------------------------------
+// packing kernels
+// ---------------------------------------------------------------------------
+__global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
+  const EgclLayout L = egcl_layout(H, nf);
+  const RawEgcl R = raw_egcl(H, nf);
+  const int NT = H / 32;
+  const int K1 = 2 * nf + 1;
+  const int KSN = node_ksteps(H, nf);
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < L.total; idx += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (idx < L.we2f) {                      // we1f[t][slot][lane]
+      // slots 0..3: h_i feature pairs (2s, 2s+1); 4..7: h_j pairs; 8: radial (lane half 0)
+      int e = idx - L.we1f;
+      int lane = e & 63, slot = (e >> 6) % (NFMAX + 1), t = (e >> 6) / (NFMAX + 1);
+      int hh = lane >> 5;
+      int q = -1;
+      if (slot < NFMAX / 2) { int f = 2 * slot + hh; if (f < nf) q = f; }
+      else if (slot < NFMAX) { int f = 2 * (slot - NFMAX / 2) + hh; if (f < nf) q = nf + f; }
+      else if (hh == 0) q = 2 * nf;
+      if (q >= 0) v = raw[R.We1 + (32 * t + (lane & 31)) * K1 + q];
+    } else if (idx < L.wn1f) {               // we2f / wc1f chain fragments
+      const bool c1 = idx >= L.wc1f;
+      int e = idx - (c1 ? L.wc1f : L.we2f);
+      int u = e & 3, lane = (e >> 2) & 63, rg = (e >> 8) & 3;
+      int rest = e >> 10;                     // tp * NT + t
+      int t = rest % NT, tp = rest / NT;
+      int r = 4 * rg + u;
+      int row = 32 * tp + (lane & 31), col = 32 * t + rho(r, lane >> 5);
+      v = raw[(c1 ? R.Wc1 : R.We2) + row * H + col];
+    } else if (idx < L.be1) {                // wn1f[tp][s][lane]
+      int e = idx - L.wn1f;
+      int lane = e & 63, s = (e >> 6) % KSN, tp = (e >> 6) / KSN;
+      int q = 2 * s + (lane >> 5);
+      if (q < H + nf) v = raw[R.Wn1 + (32 * tp + (lane & 31)) * (H + nf) + q];
+    } else if (idx < L.be2) v = raw[R.be1 + idx - L.be1];
+    else if (idx < L.bc1) v = raw[R.be2 + idx - L.be2];
+    else if (idx < L.wc2) v = raw[R.bc1 + idx - L.bc1];
+    else if (idx < L.bn1) v = raw[R.wc2 + idx - L.wc2];
+    else if (idx < L.wn2) v = raw[R.bn1 + idx - L.bn1];
+    else if (idx < L.bn2) v = raw[R.Wn2 + idx - L.wn2];
+    else if (idx < L.wv1t) { int e = idx - L.bn2; if (e < nf) v = raw[R.bn2 + e]; }
+    else if (idx < L.bv1) { int e = idx - L.wv1t; int q = e / H, k = e % H; v = raw[R.Wv1 + k * nf + q]; }
+    else if (idx < L.wv2) v = raw[R.bv1 + idx - L.bv1];
+    else if (idx < L.bv2) v = raw[R.Wv2 + idx - L.wv2];
+    else if (idx == L.bv2) v = raw[R.bv2];
+    out[idx] = v;
+  }
+}
+
+__global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
+  const AmLayout L = argmax_layout(H, nf);
+  const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < L.total; idx += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (idx < L.ba1) { int e = idx - L.wa1t; int q = e / H, k = e % H; v = raw[rW1 + k * nf + q]; }
+    else if (idx < L.wa2) v = raw[rb1 + idx - L.ba1];
+    else if (idx < L.ba2) v = raw[rW2 + idx - L.wa2];
+    else { int e = idx - L.ba2; if (e < 2 * nf) v = raw[rb2 + e]; }
+    out[idx] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+
+__device__ __forceinline__ rsrc_t weights_rsrc(const float* p, int nfloats) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
+}
+// voffset: per-lane bytes (VGPR), soffset: uniform bytes (SGPR, usually a constant)
+__device__ __forceinline__ float bload(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ f32x4 bload4(rsrc_t r, int voff, int soff) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x * __frcp_rn(1.0f + __expf(-x)); }
+
+__device__ __forceinline__ float pbc1(float x, float b) { return x - rintf(x / b) * b; }
+
+__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+__device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - log1pf(expf(-fabsf(x))); }
+
+// A wave's own LDS traffic is FIFO; this keeps the compiler from moving LDS
+// accesses across the point and drains outstanding ones.
+__device__ __forceinline__ void wave_lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    int t = __shfl_up(v, off, 64);
+    if (lane >= off) v += t;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+
+// Chained GEMM  acc[tp] += W_packed[tp][t][r] * X[t][r]  over all (t, r):
+// X is an accumulator-layout register tile (lane = pair, registers = features
+// in rho order), W the fragment-packed [H][H] weight.  Fragments for step
+// k+1 are issued before the MFMAs of step k (one 16-MFMA step = 1024 cycles
+// covers an L2 hit); sched_barrier keeps hipcc from hoisting all 64 loads.
+template <int NT>
+__device__ __forceinline__ void chain_gemm(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
+                                           int lane) {
+  f32x4 cur[NT], nxt[NT];
+  const int vo = lane * 16;
+#pragma unroll
+  for (int tp = 0; tp < NT; ++tp) cur[tp] = bload4(W, vo, (off_floats + (tp * NT) * 4 * 256) * 4);
+#pragma unroll
+  for (int step = 0; step < NT * 4; ++step) {
+    const int t = step >> 2, rg = step & 3;
+    if (step + 1 < NT * 4) {
+      const int t2 = (step + 1) >> 2, rg2 = (step + 1) & 3;
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) nxt[tp] = bload4(W, vo, (off_floats + ((tp * NT + t2) * 4 + rg2) * 256) * 4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma32(cur[tp][u], X[t][4 * rg + u], acc[tp]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (step + 1 < NT * 4) {
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) cur[tp] = nxt[tp];
+    }
+  }
+}
+
+// X[t][r] = silu(X[t][r] + bias[32 t + rho(r, hh)]); bias read from LDS as float4
+template <int NT>
+__device__ __forceinline__ void bias_silu(f32x16 (&X)[NT], const float* __restrict__ bias, int hh) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) X[t][4 * g4 + u] = silu_f(X[t][4 * g4 + u] + b[u]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// shared memory
+// ---------------------------------------------------------------------------
+template <int H, int NMAX>
+struct Smem {
+  static constexpr int AST = H + 5;   // agg row: H message sums, 3 force sums, pad (odd stride)
+  static constexpr int SST = 33;      // stage row stride
+  static constexpr int ACT = H + 1;   // node activation row stride
+  static constexpr int MAXP = NMAX * (NMAX - 1);
+  float pos[NMAX * 3], vel[NMAX * 3], boxa[NMAX * 3];
+  float h[NMAX * NFP], g[NMAX * NFP], G[NMAX * NFP];
+  float Q[NMAX];
+  alignas(16) float bias[4 * H];      // be1, be2, bc1, wc2 of the current layer
+  float agg[NMAX * AST];
+  float head[WAVES][H + 4];
+  uint32_t pairs[MAXP];
+  uint32_t mask27[NMAX];
+  int idmap[NMAX];
+  int cntrow[NMAX];
+  int headrow[WAVES];
+  int ishead[WAVES];
+  int scan[WAVES];
+  int npairs;
+  int err;
+  float red[WAVES];
+  union {
+    float stage[WAVES][32 * SST];
+    int C[NMAX * NMAX];
+    float act[NMAX * ACT];
+  } u;
+};
+
+struct MolRef {
+  int a0, n;
+  float rc;
+  float bx, by, bz;   // the molecule's edge box = box of its first atom (base.py:130)
+};
+
+// ---------------------------------------------------------------------------
+// neighbour list: Data.edges (enflow/data/base.py:122-144) for one molecule
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float shift_of(int idx, float b) { return idx == 0 ? -b : (idx == 1 ? b : 0.f); }
+
+template <int H, int NMAX>
+__device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M) {
+  const int tid = threadIdx.x;
+  const int n = M.n;
+  const float rx = M.bx + M.rc, ry = M.by + M.rc, rz = M.bz + M.rc;   // helpers.py:20
+  // (a) image masks: bit s <=> image s of atom a lies in the ellipsoid (helpers.py:17-22)
+  for (int a = tid; a < n; a += BLOCK) {
+    const float px = sm.pos[a * 3 + 0], py = sm.pos[a * 3 + 1], pz = sm.pos[a * 3 + 2];
+    uint32_t m = 0;
+    for (int s = 0; s < 27; ++s) {
+      const float ix = px + shift_of(s % 3, M.bx), iy = py + shift_of((s / 3) % 3, M.by),
+                  iz = pz + shift_of(s / 9, M.bz);
+      const float sx = ix / rx, sy = iy / ry, sz = iz / rz;
+      if (sx * sx + sy * sy + sz * sz <= 1.0f) m |= 1u << s;
+    }
+    sm.mask27[a] = m;
+  }
+  for (int e = tid; e < n * n; e += BLOCK) sm.u.C[e] = 0;
+  for (int a = tid; a < n; a += BLOCK) sm.idmap[a] = -1;
+  __syncthreads();
+  // (b) id_mapping[q] for q < n: the q-th surviving image in (image, atom) order (helpers.py:25-27)
+  if (tid < 64) {
+    const int lane = tid;
+    const uint32_t mk = lane < n ? sm.mask27[lane] : 0u;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int prefix = 0;
+    for (int s = 0; s < 27; ++s) {
+      const bool bit = (mk >> s) & 1u;
+      const uint64_t bal = __ballot(bit);
+      if (bit) {
+        const int posF = prefix + __popcll(bal & lt);
+        if (posF < n) sm.idmap[posF] = lane;
+      }
+      prefix += __popcll(bal);
+    }
+    if (lane == 0 && prefix < n) sm.err |= ENFLOW_ERR_FEW_IMAGES;
+  }
+  __syncthreads();
+  // (c) multiplicity matrix: C[i][id_mapping[q]] += #images of i within r_cut of atom q
+  //     (base.py:133-139: both hit columns mapped through id_mapping, self pairs dropped)
+  const float r_sq = M.rc * M.rc;
+  for (int e = tid; e < n * n; e += BLOCK) {
+    const int i = e / n, q = e - i * n;
+    const int jl = sm.idmap[q];
+    if (jl == i || jl < 0) continue;   // jl < 0 only with ENFLOW_ERR_FEW_IMAGES
+    const uint32_t mk = sm.mask27[i];
+    const float px = sm.pos[i * 3 + 0], py = sm.pos[i * 3 + 1], pz = sm.pos[i * 3 + 2];
+    const float qx = sm.pos[q * 3 + 0], qy = sm.pos[q * 3 + 1], qz = sm.pos[q * 3 + 2];
+    int cnt = 0;
+    uint32_t bits = mk;
+    while (bits) {
+      const int s = __builtin_ctz(bits);
+      bits &= bits - 1;
+      const float ix = px + shift_of(s % 3, M.bx), iy = py + shift_of((s / 3) % 3, M.by),
+                  iz = pz + shift_of(s / 9, M.bz);
+      const float dx = ix - qx, dy = iy - qy, dz = iz - qz;
+      if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
+    }
+    if (cnt) atomicAdd(&sm.u.C[i * n + jl], cnt);
+  }
+  __syncthreads();
+  // (d) compact to (row, col, mult) sorted by (row, col); row edge counts
+  const int NN = n * n;
+  const int per = (NN + BLOCK - 1) / BLOCK;
+  const int e0 = tid * per, e1 = min(NN, e0 + per);
+  int local = 0;
+  for (int e = e0; e < e1; ++e) local += sm.u.C[e] > 0;
+  const int incl = wave_incl_scan(local);
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 63) sm.scan[w] = incl;
+  __syncthreads();
+  int base = incl - local;
+  for (int k = 0; k < w; ++k) base += sm.scan[k];
+  for (int e = e0; e < e1; ++e) {
+    const int c = sm.u.C[e];
+    if (c > 0) {
+      const int i = e / n, jl = e - i * n;
+      sm.pairs[base++] = (uint32_t)i | ((uint32_t)jl << 8) | ((uint32_t)c << 16);
+    }
+  }
+  for (int i = tid; i < n; i += BLOCK) {
+    int s = 0;
+    for (int jl = 0; jl < n; ++jl) s += sm.u.C[i * n + jl];
+    sm.cntrow[i] = s;
+  }
+  if (tid == BLOCK - 1) {
+    int tot = 0;
+    for (int k = 0; k < WAVES; ++k) tot += sm.scan[k];
+    sm.npairs = tot;
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// EGCL edge part: per-pair MLP chain on MFMA + deterministic segment sums
+// ---------------------------------------------------------------------------
+template <int H, int NMAX>
+__device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
+                           const MolRef& M, int nf) {
+  constexpr int NT = H / 32;
+  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int SST = Smem<H, NMAX>::SST;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const int n = M.n;
+  const int P = sm.npairs;
+  const int T = (P + 31) >> 5;
+  const int tpw = (T + WAVES - 1) / WAVES;
+
+  // zero aggregates / heads, stage biases, find each wave's head row
+  for (int e = tid; e < n * AST; e += BLOCK) sm.agg[e] = 0.f;
+  for (int e = tid; e < WAVES * (H + 4); e += BLOCK) (&sm.head[0][0])[e] = 0.f;
+  for (int k = tid; k < H; k += BLOCK) {
+    sm.bias[k] = Lp[L.be1 + k];
+    sm.bias[H + k] = Lp[L.be2 + k];
+    sm.bias[2 * H + k] = Lp[L.bc1 + k];
+    sm.bias[3 * H + k] = Lp[L.wc2 + k];
+  }
+  if (tid < WAVES) {
+    const int t0 = tid * tpw;
+    int hr = -1, ih = 0;
+    if (t0 < T) {
+      const int p0 = t0 * 32;
+      hr = (int)(sm.pairs[p0] & 0xffu);
+      ih = (p0 > 0) && ((int)(sm.pairs[p0 - 1] & 0xffu) == hr);
+    }
+    sm.headrow[tid] = hr;
+    sm.ishead[tid] = ih;
+  }
+  __syncthreads();
+
+  const int t0 = w * tpw, t1 = min(T, t0 + tpw);
+  const int headrow = sm.headrow[w];
+  const bool ishead = sm.ishead[w] != 0;
+  float* __restrict__ stg = sm.u.stage[w];
+  const int nh = (nf + 1) >> 1;
+  const rsrc_t W = weights_rsrc(Lp, L.total);
+  const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
+
+  for (int tile = t0; tile < t1; ++tile) {
+    const int p = tile * 32 + j;
+    const bool valid = p < P;
+    const uint32_t pr = valid ? sm.pairs[p] : 0u;
+    const int i = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
+    const float c = (float)(pr >> 16);
+    // Edges.coord_diff with the reference's half-box image (base.py:15-19)
+    const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
+    const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
+    const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], hbz);
+    const float radial = dx * dx + dy * dy + dz * dz;                 // egcl.py:79
+
+    // ---- GEMM0: X0^T = edge_nn.0.weight . [h_i, h_j, radial]^T  (egcl.py:57-58)
+    //      k-steps: nh pairs of h_i features, nh pairs of h_j features, radial
+    f32x16 x0[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
+    for (int s = 0; s < nh; ++s) {
+      const float b = sm.h[i * NFP + 2 * s + hh];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
+    }
+    for (int s = 0; s < nh; ++s) {
+      const float b = sm.h[jl * NFP + 2 * s + hh];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + NFMAX / 2 + s) * 64) * 4), b, x0[t]);
+    }
+    {
+      const float b = hh == 0 ? radial : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + NFMAX) * 64) * 4), b, x0[t]);
+    }
+    bias_silu<NT>(x0, sm.bias, hh);
+
+    // ---- GEMM1: E^T = edge_nn.2 (egcl.py:20-24)
+    f32x16 e[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) e[t] = (f32x16)0.f;
+    chain_gemm<NT>(W, L.we2f, x0, e, lane);
+    bias_silu<NT>(e, sm.bias + H, hh);
+
+    // ---- segment_sum of the messages by row (egcl.py:64-65), weighted by multiplicity
+    const int cnt = min(32, P - tile * 32);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) stg[rho(r, hh) * SST + j] = c * e[t][r];
+      wave_lds_sync();
+      float sum = 0.f;
+      int cur = __builtin_amdgcn_readlane(i, 0);
+      for (int qq = 0; qq < cnt; ++qq) {
+        const int row = __builtin_amdgcn_readlane(i, qq);
+        if (row != cur) {
+          if (hh == 0) {
+            float* dst = (ishead && cur == headrow) ? &sm.head[w][32 * t + j] : &sm.agg[cur * AST + 32 * t + j];
+            *dst += sum;
+          }
+          sum = 0.f;
+          cur = row;
+        }
+        sum += stg[j * SST + qq];
+      }
+      if (hh == 0) {
+        float* dst = (ishead && cur == headrow) ? &sm.head[w][32 * t + j] : &sm.agg[cur * AST + 32 * t + j];
+        *dst += sum;
+      }
+      wave_lds_sync();
+    }
+
+    // ---- GEMM2: coord_nn.0, then coord_nn.2 as a per-pair dot (egcl.py:35-42, 70)
+    f32x16 hc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) hc[t] = (f32x16)0.f;
+    chain_gemm<NT>(W, L.wc1f, e, hc, lane);
+    float part = 0.f;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 2 * H + 32 * t + 8 * g4 + 4 * hh);
+        const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(hc[t][4 * g4 + u] + b[u]);
+      }
+    const float phi = part + __shfl_xor(part, 32, 64);
+    // trans = clamp(coord_diff * phi, -100, 100) (egcl.py:71-72)
+    if (hh == 0) {
+      stg[0 * SST + j] = c * fminf(fmaxf(dx * phi, -100.f), 100.f);
+      stg[1 * SST + j] = c * fminf(fmaxf(dy * phi, -100.f), 100.f);
+      stg[2 * SST + j] = c * fminf(fmaxf(dz * phi, -100.f), 100.f);
+    }
+    wave_lds_sync();
+    {
+      const int fq = j < 3 ? j : 0;
+      float sum = 0.f;
+      int cur = __builtin_amdgcn_readlane(i, 0);
+      for (int qq = 0; qq < cnt; ++qq) {
+        const int row = __builtin_amdgcn_readlane(i, qq);
+        if (row != cur) {
+          if (lane < 3) {
+            float* dst = (ishead && cur == headrow) ? &sm.head[w][H + lane] : &sm.agg[cur * AST + H + lane];
+            *dst += sum;
+          }
+          sum = 0.f;
+          cur = row;
+        }
+        sum += stg[fq * SST + qq];
+      }
+      if (lane < 3) {
+        float* dst = (ishead && cur == headrow) ? &sm.head[w][H + lane] : &sm.agg[cur * AST + H + lane];
+        *dst += sum;
+      }
+    }
+    wave_lds_sync();
+  }
+  __syncthreads();
+  // ordered fix-up of rows that continue across a wave boundary
+  for (int f = tid; f < H + 3; f += BLOCK) {
+    for (int ww = 0; ww < WAVES; ++ww)
+      if (sm.ishead[ww]) sm.agg[sm.headrow[ww] * AST + f] += sm.head[ww][f];
+  }
+  __syncthreads();
+}
+
+// Q = vel_scaling_nn(h)  (egcl.py:51-54, 90)
+template <int H, int NMAX>
+__device__ __forceinline__ void node_q(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L, int n, int nf) {
+  constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
+  constexpr int ACT = Smem<H, NMAX>::ACT;
+  const int tid = threadIdx.x;
+  {
+    const int k = tid % H, grp = tid / H;
+    if (grp < NG) {
+      const float b = Lp[L.bv1 + k], w2 = Lp[L.wv2 + k];
+      for (int a = grp; a < n; a += NG) {
+        float v = b;
+        for (int q = 0; q < nf; ++q) v += Lp[L.wv1t + q * H + k] * sm.h[a * NFP + q];
+        sm.u.act[a * ACT + k] = w2 * silu_f(v);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid < n) {
+    float s = 0.f;
+    for (int k = 0; k < H; ++k) s += sm.u.act[tid * ACT + k];
+    sm.Q[tid] = s + Lp[L.bv2];
+  }
+  __syncthreads();
+}
+
+// G = node_nn([h, agg])  (egcl.py:26-30, 62-67); node_nn.0 on MFMA, node_nn.2 on VALU
+template <int H, int NMAX>
+__device__ __forceinline__ void node_g(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L, int n, int nf) {
+  constexpr int NT = H / 32;
+  constexpr int NA = NMAX / 32;
+  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int ACT = Smem<H, NMAX>::ACT;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const int ks = node_ksteps(H, nf);
+  const rsrc_t W = weights_rsrc(Lp, L.total);
+  for (int item = w; item < NT * NA; item += WAVES) {
+    const int tp = item % NT, at = item / NT;
+    const int a = at * 32 + j;
+    const bool va = a < n;
+    const int ac = va ? a : 0;
+    f32x16 acc = (f32x16)0.f;
+    for (int s = 0; s < ks; ++s) {
+      const int q = 2 * s + hh;
+      float b = 0.f;
+      if (q < nf) b = sm.h[ac * NFP + q];
+      else if (q < nf + H) b = sm.agg[ac * AST + (q - nf)];
+      acc = mfma32(bload(W, lane * 4, (L.wn1f + (tp * ks + s) * 64) * 4), va ? b : 0.f, acc);
+    }
+    if (va) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = 32 * tp + rho(r, hh);
+        sm.u.act[a * ACT + f] = silu_f(acc[r] + Lp[L.bn1 + f]);
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    float s = Lp[L.bn2 + q];
+    const float* wr = Lp + L.wn2 + q * H;
+    for (int k = 0; k < H; ++k) s += wr[k] * sm.u.act[a * ACT + k];
+    sm.G[a * NFP + q] = s;
+  }
+  __syncthreads();
+}
+
+// ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
+// returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
+template <int H, int NMAX>
+__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX>& sm, const float* __restrict__ Dp, const float* __restrict__ noise,
+                                int a0, int n, int nf) {
+  constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
+  constexpr int ACT = Smem<H, NMAX>::ACT;
+  const AmLayout L = argmax_layout(H, nf);
+  const int tid = threadIdx.x;
+  {
+    const int k = tid % H, grp = tid / H;
+    if (grp < NG) {
+      const float b = Dp[L.ba1 + k];
+      for (int a = grp; a < n; a += NG) {
+        float v = b;
+        for (int q = 0; q < nf; ++q) v += Dp[L.wa1t + q * H + k] * sm.h[a * NFP + q];
+        sm.u.act[a * ACT + k] = silu_f(v);
+      }
+    }
+  }
+  __syncthreads();
+  // net[a][o], o < 2 nf, staged in G (log_scale) / g-free scratch
+  float* net = &sm.agg[0];   // agg is free before the first layer: [a][2*NFMAX]
+  for (int e = tid; e < n * 2 * nf; e += BLOCK) {
+    const int a = e / (2 * nf), o = e - a * 2 * nf;
+    float s = Dp[L.ba2 + o];
+    const float* wr = Dp + L.wa2 + o * H;
+    for (int k = 0; k < H; ++k) s += wr[k] * sm.u.act[a * ACT + k];
+    net[a * 2 * NFMAX + o] = s;
+  }
+  __syncthreads();
+  float lq = 0.f;
+  if (tid < n) {
+    const int a = tid;
+    float u[NFMAX], hv[NFMAX];
+    float T = 0.f;
+#pragma unroll
+    for (int q = 0; q < NFMAX; ++q) {
+      if (q < nf) {
+        const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
+        u[q] = tr + noise[(size_t)(a0 + a) * nf + q] * expf(ls);
+        hv[q] = sm.h[a * NFP + q];
+        T += hv[q] * u[q];
+        lq += -0.5f * u[q] * u[q] - ls;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NFMAX; ++q) {
+      if (q < nf) {
+        const float z = hv[q] * u[q] + (1.f - hv[q]) * (T - softplus_f(T - u[q]));
+        lq -= (1.f - hv[q]) * logsigmoid_f(T - u[q]);
+        sm.h[a * NFP + q] = z;
+      }
+    }
+  }
+  __syncthreads();
+  return lq;
+}
+
+// deterministic block sum (thread values -> one float, fixed order)
+template <int H, int NMAX>
+__device__ __forceinline__ float block_sum(Smem<H, NMAX>& sm, float v) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sm.red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int k = 0; k < WAVES; ++k) s += sm.red[k];
+  return s;
+}
+
+struct FlowArgs {
+  const int32_t* mol_ptr;
+  const float* r_cut;
+  const float* box;
+  float* h;
+  float* g;
+  float* pos;
+  float* vel;
+  const float* layers;
+  int n_layers;
+  int nf;
+  int dequant_kind;
+  const float* dequant;
+  const float* noise;
+  float dequant_scale;
+  float dt;
+  float cw;
+  float* ldj_mol;
+  int32_t* argmax_idx;
+  int32_t* max_idx;
+  int32_t* err;
+};
+
+enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
+
+template <int H, int NMAX>
+__device__ __forceinline__ bool load_molecule(Smem<H, NMAX>& sm, const FlowArgs& A, MolRef& M, int what) {
+  const int m = blockIdx.x;
+  const int tid = threadIdx.x;
+  M.a0 = A.mol_ptr[m];
+  M.n = A.mol_ptr[m + 1] - M.a0;
+  M.rc = 0.f;
+  M.bx = M.by = M.bz = 0.f;
+  if (M.n > NMAX || A.nf > NFMAX) {
+    if (tid == 0) atomicOr(A.err, M.n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
+    return false;
+  }
+  const int n = M.n, nf = A.nf;
+  if (what & LOAD_POS) {
+    M.rc = A.r_cut[m];
+    for (int e = tid; e < n * 3; e += BLOCK) {
+      sm.pos[e] = A.pos[(size_t)M.a0 * 3 + e];
+      sm.boxa[e] = A.box[(size_t)M.a0 * 3 + e];
+    }
+  }
+  if (what & LOAD_VELG)
+    for (int e = tid; e < n * 3; e += BLOCK) sm.vel[e] = A.vel[(size_t)M.a0 * 3 + e];
+  for (int e = tid; e < n * NFP; e += BLOCK) {   // rows zero-padded past nf
+    const int a = e / NFP, q = e - a * NFP;
+    const size_t src = (size_t)(M.a0 + a) * nf + q;
+    if (what & LOAD_H) sm.h[e] = q < nf ? A.h[src] : 0.f;
+    if (what & LOAD_VELG) sm.g[e] = q < nf ? A.g[src] : 0.f;
+  }
+  if (tid == 0) sm.err = 0;
+  __syncthreads();
+  if ((what & LOAD_POS) && n > 0) {
+    M.bx = sm.boxa[0];
+    M.by = sm.boxa[1];
+    M.bz = sm.boxa[2];
+  }
+  return true;
+}
+
+// ---------------------------------------------------------------------------
+// the fused flow kernel (forward or reverse)
+// ---------------------------------------------------------------------------
+template <int H, int NMAX, bool REV>
+__global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
+  __shared__ Smem<H, NMAX> sm;
+  MolRef M;
+  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) return;
+  const int tid = threadIdx.x;
+  const int n = M.n, nf = A.nf;
+  const EgclLayout L = egcl_layout(H, nf);
+  constexpr int AST = Smem<H, NMAX>::AST;
+  float ldj = 0.f;
+
+  if (!REV) {
+    if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
+      ldj += argmax_dequant(sm, A.dequant, A.noise, M.a0, n, nf);
+    } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+      for (int e = tid; e < n * nf; e += BLOCK) {
+        const int a = e / nf, q = e - a * nf;
+        sm.h[a * NFP + q] += A.dequant_scale * A.noise[(size_t)M.a0 * nf + e];
+      }
+      __syncthreads();
+    }
+  }
+
+  for (int it = 0; it < A.n_layers; ++it) {
+    // Opaque per-layer copies: stop hipcc from hoisting every nf / molecule
+    // derived predicate and address out of the layer loop (SGPR/VGPR spills).
+    int nf = A.nf, n = M.n;
+    asm volatile("" : "+s"(nf), "+s"(n));
+    MolRef Ml = M;
+    Ml.n = n;
+    const EgclLayout L = egcl_layout(H, nf);
+    const int l = REV ? A.n_layers - 1 - it : it;
+    const float* Lp = A.layers + (size_t)l * L.total;
+    if (REV) {   // dynamics.py:28-30
+      for (int a = tid; a < n; a += BLOCK) {
+        for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] -= sm.g[a * NFP + q] * A.dt;
+        for (int d = 0; d < 3; ++d)
+          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, sm.boxa[a * 3 + d]);
+      }
+      __syncthreads();
+    }
+    build_pairs(sm, Ml);
+    node_q(sm, Lp, L, n, nf);
+    edge_tiles(sm, Lp, L, Ml, nf);
+    node_g(sm, Lp, L, n, nf);
+    for (int a = tid; a < n; a += BLOCK) {
+      const float q = sm.Q[a];
+      const float eq = expf(q);
+      const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);   // helpers.py:63-70
+      if (!REV) {  // dynamics.py:15-22
+        for (int d = 0; d < 3; ++d) {
+          const float F = sm.agg[a * AST + H + d] * inv * A.cw;
+          const float v = eq * sm.vel[a * 3 + d] + F * A.dt;
+          sm.vel[a * 3 + d] = v;
+          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, sm.boxa[a * 3 + d]);
+        }
+        for (int qf = 0; qf < nf; ++qf) {
+          const float gn = sm.g[a * NFP + qf] + sm.G[a * NFP + qf] * A.dt;
+          sm.g[a * NFP + qf] = gn;
+          sm.h[a * NFP + qf] += gn * A.dt;
+        }
+        ldj += q;
+      } else {     // dynamics.py:32-35
+        for (int qf = 0; qf < nf; ++qf) sm.g[a * NFP + qf] -= sm.G[a * NFP + qf] * A.dt;
+        for (int d = 0; d < 3; ++d) {
+          const float F = sm.agg[a * AST + H + d] * inv * A.cw;
+          sm.vel[a * 3 + d] = (sm.vel[a * 3 + d] - F * A.dt) / eq;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  if (REV) {   // dequantize.reverse (argmax.py:27-28 / floor.py:13)
+    for (int a = tid; a < n; a += BLOCK) {
+      if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
+        int best = 0;
+        float bv = sm.h[a * NFP];
+        for (int q = 1; q < nf; ++q)
+          if (sm.h[a * NFP + q] > bv) { bv = sm.h[a * NFP + q]; best = q; }
+        A.argmax_idx[M.a0 + a] = best;
+        atomicMax(A.max_idx, best);
+      } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+        for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] = floorf(sm.h[a * NFP + q]);
+      }
+    }
+  }
+  // write back
+  for (int e = tid; e < n * 3; e += BLOCK) {
+    A.pos[(size_t)M.a0 * 3 + e] = sm.pos[e];
+    A.vel[(size_t)M.a0 * 3 + e] = sm.vel[e];
+  }
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    A.h[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
+    A.g[(size_t)M.a0 * nf + e] = sm.g[a * NFP + q];
+  }
+  if (!REV) {
+    const float s = block_sum(sm, ldj);
+    if (tid == 0) A.ldj_mol[blockIdx.x] = s;
+  }
+  if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
+}
+
+// one EGCL.forward: Q, F, G to global
+template <int H, int NMAX>
+__global__ void __launch_bounds__(BLOCK, 2) egcl_forward_kernel(FlowArgs A, float* Qo, float* Fo, float* Go) {
+  __shared__ Smem<H, NMAX> sm;
+  MolRef M;
+  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H)) return;
+  const int tid = threadIdx.x;
+  const int n = M.n, nf = A.nf;
+  const EgclLayout L = egcl_layout(H, nf);
+  constexpr int AST = Smem<H, NMAX>::AST;
+  build_pairs(sm, M);
+  node_q(sm, A.layers, L, n, nf);
+  edge_tiles(sm, A.layers, L, M, nf);
+  node_g(sm, A.layers, L, n, nf);
+  for (int a = tid; a < n; a += BLOCK) {
+    Qo[M.a0 + a] = sm.Q[a];
+    const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);
+    for (int d = 0; d < 3; ++d) Fo[(size_t)(M.a0 + a) * 3 + d] = sm.agg[a * AST + H + d] * inv * A.cw;
+    for (int q = 0; q < nf; ++q) Go[(size_t)(M.a0 + a) * nf + q] = sm.G[a * NFP + q];
+  }
+  if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
+}
+
+// ArgMax.forward only
+template <int H, int NMAX>
+__global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float* z, float* lq_mol) {
+  __shared__ Smem<H, NMAX> sm;
+  MolRef M;
+  if (!load_molecule(sm, A, M, LOAD_H)) return;
+  const int tid = threadIdx.x;
+  const int n = M.n, nf = A.nf;
+  const float lq = argmax_dequant(sm, A.dequant, A.noise, M.a0, n, nf);
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    z[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
+  }
+  const float s = block_sum(sm, lq);
+  if (tid == 0) lq_mol[blockIdx.x] = s;
+}
+
+// neighbour pairs only
+template <int NMAX>
+__global__ void __launch_bounds__(BLOCK) neighbour_pairs_kernel(FlowArgs A, int max_pairs, uint32_t* pairs, int32_t* count) {
+  __shared__ Smem<32, NMAX> sm;
+  MolRef M;
+  if (!load_molecule(sm, A, M, LOAD_POS)) return;
+  build_pairs(sm, M);
+  const int P = sm.npairs;
+  for (int p = threadIdx.x; p < P && p < max_pairs; p += BLOCK) pairs[(size_t)blockIdx.x * max_pairs + p] = sm.pairs[p];
+  if (threadIdx.x == 0) {
+    count[blockIdx.x] = P;
+    if (sm.err) atomicOr(A.err, sm.err);
+  }
+}
+
+// Alchemical_NLL per-molecule sums (loss.py:11-19, 21-24)
+template <int NMAX>
+__global__ void __launch_bounds__(BLOCK) nll_mol_kernel(const int32_t* mol_ptr, int nf, const float* h, const float* g,
+                                                      const float* pos, const float* vel, float softening, float* out) {
+  __shared__ float spos[NMAX * 3];
+  __shared__ float red[4][WAVES];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
+  for (int e = tid; e < n * 3; e += BLOCK) spos[e] = pos[(size_t)a0 * 3 + e];
+  __syncthreads();
+  float lj = 0.f, v2 = 0.f, h2 = 0.f, g2 = 0.f;
+  for (int e = tid; e < n * n; e += BLOCK) {
+    const int i = e / n, k = e - i * n;
+    if (k <= i) continue;
+    const float dx = spos[i * 3] - spos[k * 3], dy = spos[i * 3 + 1] - spos[k * 3 + 1], dz = spos[i * 3 + 2] - spos[k * 3 + 2];
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    if (d2 != 0.f) {
+      const float r2 = d2 + softening;
+      const float r6 = r2 * r2 * r2;
+      lj += 4.f * (1.f / (r6 * r6) - 1.f / r6);
+    }
+  }
+  for (int e = tid; e < n * 3; e += BLOCK) { const float v = vel[(size_t)a0 * 3 + e]; v2 += v * v; }
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const float a = h[(size_t)a0 * nf + e], b = g[(size_t)a0 * nf + e];
+    h2 += a * a;
+    g2 += b * b;
+  }
+  lj = wave_sum(lj); v2 = wave_sum(v2); h2 = wave_sum(h2); g2 = wave_sum(g2);
+  const int lane = tid & 63, w = tid >> 6;
+  if (lane == 0) { red[0][w] = lj; red[1][w] = v2; red[2][w] = h2; red[3][w] = g2; }
+  __syncthreads();
+  if (tid < 4) {
+    float s = 0.f;
+    for (int k = 0; k < WAVES; ++k) s += red[tid][k];
+    out[(size_t)m * 4 + tid] = s;
+  }
+}
+
+// batch scalars: fixed-order double reduction over molecules
+__global__ void __launch_bounds__(BLOCK) reduce_ldj_kernel(const float* ldj_mol, int num_mols, double cst, float* out) {
+  __shared__ double red[BLOCK];
+  double s = 0.0;
+  for (int m = threadIdx.x; m < num_mols; m += BLOCK) s += (double)ldj_mol[m];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = BLOCK / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = (float)(red[0] + cst);
+}
+
+__global__ void __launch_bounds__(BLOCK) reduce_nll_kernel(const float* nll_mol, int num_mols, int num_atoms,
+                                                         const float* ldj_total, float kBT, float partition_func,
+                                                         float* loss) {
+  __shared__ double red[4][BLOCK];
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int m = threadIdx.x; m < num_mols; m += BLOCK)
+    for (int k = 0; k < 4; ++k) s[k] += (double)nll_mol[(size_t)m * 4 + k];
+  for (int k = 0; k < 4; ++k) red[k][threadIdx.x] = s[k];
+  __syncthreads();
+  for (int off = BLOCK / 2; off > 0; off >>= 1) {
+    if (threadIdx.x < off)
+      for (int k = 0; k < 4; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double L2PI = 1.8378770664093453;   // log(2 pi)
+    const double Hn = red[0][0] + 0.5 * red[1][0];
+    const double logZ = -(double)num_atoms * (log((double)partition_func) - 1.5 * log(2.0 * M_PI / (double)kBT));
+    const double lgh = -0.5 * (red[2][0] + L2PI), lgg = -0.5 * (red[3][0] + L2PI);
+    const double log_px = -Hn / (double)kBT + logZ + (double)ldj_total[0] + lgh + lgg;
+    loss[0] = (float)(-log_px / (double)num_mols);
+  }
+}
+
+__global__ void one_hot_kernel(const int32_t* idx, int num_atoms, int width, float* out) {
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < num_atoms * width; e += gridDim.x * blockDim.x) {
+    const int a = e / width, k = e - a * width;
+    out[e] = idx[a] == k ? 1.f : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int hid_ok(int H) { return H == 32 || H == 64 || H == 128; }
+static const double kLog2Pi = 1.8378770664093453;
+
+#define DISPATCH_HN(H, NMAXSEL, CALL)                        \
+  do {                                                        \
+    if (NMAXSEL <= 32) {                                      \
+      if (H == 32) { CALL(32, 32); }                          \
+      else if (H == 64) { CALL(64, 32); }                     \
+      else { CALL(128, 32); }                                 \
+    } else {                                                  \
+      if (H == 32) { CALL(32, 64); }                          \
+      else if (H == 64) { CALL(64, 64); }                     \
+      else { CALL(128, 64); }                                 \
+    }                                                         \
+  } while (0)
+
+extern "C" {
+
+int enflow_abi_version(void) { return ENFLOW_ABI; }
+int enflow_max_atoms(void) { return 64; }
+int enflow_max_node_nf(void) { return NFMAX; }
+int enflow_supports_hidden(int hidden_nf) { return hid_ok(hidden_nf); }
+
+int64_t enflow_egcl_packed_size(int hidden_nf, int node_nf) {
+  if (!hid_ok(hidden_nf) || node_nf < 1 || node_nf > NFMAX) return -1;
+  return egcl_layout(hidden_nf, node_nf).total;
+}
+int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf) {
+  if (!hid_ok(hidden_nf) || node_nf < 1 || node_nf > NFMAX) return -1;
+  return argmax_layout(hidden_nf, node_nf).total;
+}
+
+int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {
+  if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
+  const int total = egcl_layout(H, nf).total;
+  hipLaunchKernelGGL(pack_egcl_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_pack_argmax_f32(const float* raw, int H, int nf, float* packed, void* stream) {
+  if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
+  const int total = argmax_layout(H, nf).total;
+  hipLaunchKernelGGL(pack_argmax_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+static int check_common(int num_mols, int max_mol_atoms, int nf, int H) {
+  if (num_mols < 0 || max_mol_atoms < 0) return -1;
+  if (max_mol_atoms > 64) return -3;
+  if (nf < 1 || nf > NFMAX) return -4;
+  if (!hid_ok(H)) return -5;
+  return 0;
+}
+
+int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                          const int32_t* mol_ptr, const float* r_cut, const float* box,
+                          float* h, float* g, float* pos, float* vel,
+                          const float* layers, int n_layers,
+                          int dequant_kind, const float* dequant, const float* noise,
+                          float dequant_scale, float dt, float cw,
+                          float* ldj_mol, float* ldj_total, int32_t* err_flag, void* stream) {
+  int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (rc) return rc;
+  if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
+      (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
+  (void)num_atoms;
+  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
+             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag};
+  if (num_mols > 0) {
+#define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
+    DISPATCH_HN(H, max_mol_atoms, CALL);
+#undef CALL
+  }
+  const double cst = dequant_kind == ENFLOW_DEQUANT_ARGMAX ? -0.5 * kLog2Pi : 0.0;
+  hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                          const int32_t* mol_ptr, const float* r_cut, const float* box,
+                          float* h, float* g, float* pos, float* vel,
+                          const float* layers, int n_layers,
+                          int dequant_kind, float dt, float cw,
+                          int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, void* stream) {
+  int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (rc) return rc;
+  if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
+  (void)num_atoms;
+  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
+             0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag};
+  if (num_mols > 0) {
+#define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
+    DISPATCH_HN(H, max_mol_atoms, CALL);
+#undef CALL
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_one_hot_f32(const int32_t* idx, int num_atoms, int width, float* out, void* stream) {
+  if (num_atoms < 0 || width < 0) return -1;
+  const long long tot = (long long)num_atoms * width;
+  if (tot == 0) return 0;
+  const int blocks = (int)((tot + 255) / 256 < 65536 ? (tot + 255) / 256 : 65536);
+  hipLaunchKernelGGL(one_hot_kernel, dim3(blocks), dim3(256), 0, S(stream), idx, num_atoms, width, out);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_egcl_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                            const int32_t* mol_ptr, const float* r_cut, const float* box,
+                            const float* h, const float* pos, const float* layer,
+                            float cw, float* Q, float* F, float* G, int32_t* err_flag, void* stream) {
+  int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (rc) return rc;
+  (void)num_atoms;
+  FlowArgs A{mol_ptr, r_cut, box, const_cast<float*>(h), nullptr, const_cast<float*>(pos), nullptr, layer, 1, nf,
+             0, nullptr, nullptr, 0.f, 0.f, cw, nullptr, nullptr, nullptr, err_flag};
+  if (num_mols > 0) {
+#define CALL(HH, NN) hipLaunchKernelGGL((egcl_forward_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, Q, F, G)
+    DISPATCH_HN(H, max_mol_atoms, CALL);
+#undef CALL
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_argmax_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                              const int32_t* mol_ptr, const float* h, const float* dequant,
+                              const float* noise, float* z, float* log_q_mol, float* log_q, void* stream) {
+  int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (rc) return rc;
+  (void)num_atoms;
+  FlowArgs A{mol_ptr, nullptr, nullptr, const_cast<float*>(h), nullptr, nullptr, nullptr, nullptr, 0, nf,
+             ENFLOW_DEQUANT_ARGMAX, dequant, noise, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr};
+  if (num_mols > 0) {
+#define CALL(HH, NN) hipLaunchKernelGGL((argmax_forward_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, z, log_q_mol)
+    DISPATCH_HN(H, max_mol_atoms, CALL);
+#undef CALL
+  }
+  hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), log_q_mol, num_mols, -0.5 * kLog2Pi, log_q);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_neighbour_pairs_f32(int num_mols, int num_atoms, int max_mol_atoms, const int32_t* mol_ptr,
+                               const float* r_cut, const float* box, const float* pos,
+                               int max_pairs, uint32_t* pairs, int32_t* pair_count,
+                               int32_t* err_flag, void* stream) {
+  if (num_mols < 0 || max_mol_atoms > 64 || max_pairs < 0) return -1;
+  (void)num_atoms;
+  FlowArgs A{mol_ptr, r_cut, box, nullptr, nullptr, const_cast<float*>(pos), nullptr, nullptr, 0, 1,
+             0, nullptr, nullptr, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, err_flag};
+  if (num_mols > 0) {
+    if (max_mol_atoms <= 32)
+      hipLaunchKernelGGL((neighbour_pairs_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
+    else
+      hipLaunchKernelGGL((neighbour_pairs_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf,
+                              const int32_t* mol_ptr, const float* h, const float* g,
+                              const float* pos, const float* vel, const float* ldj_total,
+                              float kBT, float softening, float partition_func,
+                              float* nll_mol, float* loss, void* stream) {
+  if (num_mols < 0 || max_mol_atoms > 64 || nf < 1) return -1;
+  if (num_mols > 0) {
+    if (max_mol_atoms <= 32)
+      hipLaunchKernelGGL((nll_mol_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+    else
+      hipLaunchKernelGGL((nll_mol_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+  }
+  hipLaunchKernelGGL(reduce_nll_kernel, dim3(1), dim3(BLOCK), 0, S(stream), nll_mol, num_mols, num_atoms, ldj_total,
+                     kBT, partition_func, loss);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

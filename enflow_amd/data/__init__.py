@@ -1,0 +1,1 @@
+from .base import Data, Edges, DataLoader  # noqa: F401

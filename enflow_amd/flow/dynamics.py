@@ -1,0 +1,157 @@
+"""Leapfrog coupling flow (mirrors enflow/flow/dynamics.py:4-37).
+
+``LFIntegrator.forward(data) -> (data, ldj)`` and ``reverse(data) -> data``
+run the whole flow -- dequantisation, every layer's periodic neighbour list,
+EGCL and leapfrog update, and the log|detJ| sum -- as ONE HIP kernel launch
+(enflow_lf_forward_f32 / enflow_lf_reverse_f32): one workgroup per molecule,
+molecule state resident in LDS across layers.  Like the reference, ``data`` is
+updated (its tensors rebound) and returned.
+
+VVIntegrator (dynamics.py:39-86) is not provided: in the reference it cannot
+run (it reads ``self.n_iter``, which BaseFlow never sets, and treats the
+dequantiser's (z, ldj) tuple as a tensor), see DESIGN.md.
+"""
+import warnings
+
+import torch
+
+from .. import _lib
+from ..nn.argmax import ArgMax
+from ..nn.egcl import EGCL
+from ..nn.floor import Floor
+from .base import BaseFlow
+
+
+class LFIntegrator(BaseFlow):
+    def make_networks(self, network):
+        return [network for _ in range(self.n_iter)]
+
+    # ------------------------------------------------------------------
+    def _geometry(self):
+        nets = list(self.networks)
+        if not nets:
+            return None, None, 1.0
+        if not all(isinstance(n, EGCL) for n in nets):
+            raise NotImplementedError("LFIntegrator on the HIP path needs enflow_amd.nn.EGCL networks")
+        h0, f0 = nets[0].hidden_nf, nets[0].input_nf
+        for n in nets:
+            n._check_supported()
+            if (n.hidden_nf, n.input_nf) != (h0, f0) or n.coords_weight != nets[0].coords_weight:
+                raise NotImplementedError("all EGCL layers must share hidden_nf, node_nf and coords_weight")
+        return h0, f0, float(nets[0].coords_weight)
+
+    def _dequant_kind(self):
+        d = self.dequantize
+        if isinstance(d, ArgMax):
+            return _lib.DEQUANT_ARGMAX
+        if isinstance(d, Floor):
+            return _lib.DEQUANT_FLOOR
+        if d is None:
+            return _lib.DEQUANT_NONE
+        raise NotImplementedError(f"unsupported dequantiser {type(d).__name__}")
+
+    def packed_layers(self, device):
+        """All layers packed back to back (cached; re-packed on any parameter change)."""
+        params = [p for n in self.networks for _, p in n.named_parameters()]
+        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        if getattr(self, "_layers_key", None) == key:
+            return self._layers_buf
+        hid, nf, _ = self._geometry()
+        L = _lib.lib()
+        stride = L.enflow_egcl_packed_size(hid, nf)
+        buf = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)
+        for i, n in enumerate(self.networks):
+            n.pack_into(buf[i * stride:(i + 1) * stride])
+        self._layers_buf, self._layers_key = buf, key
+        return buf
+
+    def _warn_grad(self):
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            warnings.warn("enflow_amd LFIntegrator: HIP backward is not implemented yet; outputs "
+                          "are detached", RuntimeWarning, stacklevel=3)
+
+    # ------------------------------------------------------------------
+    def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
+                        ldj_mol, ldj_total, err):
+        """In-place fused forward on preallocated fp32 device buffers (no
+        host sync, no allocation): the entry point the benchmark times."""
+        hid, nf, cw = self._geometry()
+        kind = self._dequant_kind()
+        dev = h.device
+        dq = self.dequantize.packed(dev) if kind == _lib.DEQUANT_ARGMAX else None
+        scale = float(getattr(self.dequantize, "dequant_scale", 1.0)) if kind == _lib.DEQUANT_FLOOR else 0.0
+        L = _lib.lib()
+        _lib.check(L.enflow_lf_forward_f32(
+            mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
+            _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
+            _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
+            _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
+            _lib.ptr(err), _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
+
+    def _state(self, data):
+        _lib.require_gpu(data.pos)
+        dev = data.pos.device
+        f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous().clone()  # noqa: E731
+        rc = torch.as_tensor(data.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous()
+        return dict(h=f(data.h), g=f(data.g), pos=f(data.pos), vel=f(data.vel),
+                    box=data.box.detach().to(device=dev, dtype=torch.float32).contiguous(), r_cut=rc,
+                    mol_ptr=data.mol_ptr, max_n=data.max_mol_atoms, dev=dev)
+
+    def forward(self, data, noise=None, check_errors=True):
+        """dynamics.py:10-24.  ``noise`` optionally supplies the dequantiser's
+        draw (N(0,1) for ArgMax, U[0,1) for Floor), shape h.shape."""
+        self._warn_grad()
+        s = self._state(data)
+        dev = s["dev"]
+        kind = self._dequant_kind()
+        if noise is None:
+            if kind == _lib.DEQUANT_ARGMAX:
+                noise = torch.randn(s["h"].shape, device=dev, dtype=torch.float32)
+            elif kind == _lib.DEQUANT_FLOOR:
+                noise = torch.rand(s["h"].shape, device=dev, dtype=torch.float32)
+        else:
+            noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+        M = s["mol_ptr"].numel() - 1
+        ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
+        ldj = torch.empty(1, dtype=torch.float32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
+                             s["max_n"], noise, ldj_mol, ldj, err)
+        if check_errors:
+            _lib.raise_on_err(err)
+        dt = data.h.dtype
+        data.h, data.g = s["h"].to(dt), s["g"].to(dt)
+        data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
+        return data, ldj.reshape(()).to(dt)
+
+    def reverse(self, data, check_errors=True):
+        """dynamics.py:26-37 (ends with dequantize.reverse)."""
+        self._warn_grad()
+        s = self._state(data)
+        dev = s["dev"]
+        hid, nf, cw = self._geometry()
+        kind = self._dequant_kind()
+        n = s["h"].shape[0]
+        idx = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        mx = torch.zeros(1, dtype=torch.int32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        L = _lib.lib()
+        _lib.check(L.enflow_lf_reverse_f32(
+            s["mol_ptr"].numel() - 1, n, s["max_n"], nf, hid, _lib.ptr(s["mol_ptr"]), _lib.ptr(s["r_cut"]),
+            _lib.ptr(s["box"]), _lib.ptr(s["h"]), _lib.ptr(s["g"]), _lib.ptr(s["pos"]), _lib.ptr(s["vel"]),
+            _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, float(self.dt), cw,
+            _lib.ptr(idx), _lib.ptr(mx), _lib.ptr(err), _lib.stream_ptr(dev)), "enflow_lf_reverse_f32")
+        if check_errors:
+            _lib.raise_on_err(err)
+        dt = data.h.dtype
+        if kind == _lib.DEQUANT_ARGMAX:
+            width = int(mx.item()) + 1
+            oh = torch.empty((n, width), dtype=torch.float32, device=dev)
+            _lib.check(L.enflow_one_hot_f32(_lib.ptr(idx), n, width, _lib.ptr(oh), _lib.stream_ptr(dev)),
+                       "enflow_one_hot_f32")
+            data.h = oh.to(dt)
+        else:
+            data.h = s["h"].to(dt)
+        data.g = s["g"].to(dt)
+        data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
+        return data

@@ -1,0 +1,70 @@
+"""ArgMax dequantiser (mirrors enflow/nn/argmax.py:5-28).
+
+forward(h) -> (z, log_q) runs enflow_argmax_forward_f32 with a device-side
+N(0, 1) draw (the reference's torch.randn(h.size()), argmax.py:16);
+reverse(z) is the one-hot of the first maximum with the reference's width
+(max index + 1).
+"""
+import torch
+from torch import nn
+
+from .. import _lib
+from ..utils.helpers import one_hot, mol_ptr_from_counts
+
+
+class ArgMax(nn.Module):
+    def __init__(self, node_nf, hidden_nf, act_fn=nn.SiLU()):
+        super().__init__()
+        self.node_nf, self.hidden_nf = node_nf, hidden_nf
+        self.network = nn.Sequential(nn.Linear(node_nf, hidden_nf), act_fn,
+                                     nn.Linear(hidden_nf, node_nf * 2))
+        self._packed = None
+        self._packed_key = None
+
+    def packed(self, device):
+        params = [p for _, p in self.named_parameters()]
+        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        L = _lib.lib()
+        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in params])
+        out = torch.empty(L.enflow_argmax_packed_size(self.hidden_nf, self.node_nf),
+                          dtype=torch.float32, device=device)
+        _lib.check(L.enflow_pack_argmax_f32(_lib.ptr(raw), self.hidden_nf, self.node_nf, _lib.ptr(out),
+                                            _lib.stream_ptr(device)), "enflow_pack_argmax_f32")
+        self._packed, self._packed_key = out, key
+        return out
+
+    def forward(self, h, noise=None, N=None):
+        """``N``: atoms per molecule (defaults to one molecule holding every
+        atom; log_q is a batch scalar either way).  ``noise``: optional N(0,1)
+        draw of shape h.shape."""
+        _lib.require_gpu(h)
+        L = _lib.lib()
+        dev = h.device
+        n = h.shape[0]
+        if N is None:
+            N = torch.tensor([n])
+        N = torch.as_tensor(N).reshape(-1)
+        # the kernel owns one molecule per workgroup (<= 64 atoms): split a
+        # single big "molecule" into chunks -- log_q is a plain sum over atoms
+        if int(N.max()) > 64:
+            chunks = []
+            for c in N.tolist():
+                chunks += [64] * (c // 64) + ([c % 64] if c % 64 else [])
+            N = torch.tensor(chunks)
+        ptr = mol_ptr_from_counts(N, device=dev)
+        hf = h.detach().to(torch.float32).contiguous()
+        eps = (torch.randn(h.shape, device=dev, dtype=torch.float32) if noise is None
+               else noise.to(device=dev, dtype=torch.float32).contiguous())
+        z = torch.empty_like(hf)
+        lq_mol = torch.empty(N.numel(), dtype=torch.float32, device=dev)
+        lq = torch.empty(1, dtype=torch.float32, device=dev)
+        _lib.check(L.enflow_argmax_forward_f32(N.numel(), n, int(N.max()), self.node_nf, self.hidden_nf,
+                                               _lib.ptr(ptr), _lib.ptr(hf), _lib.ptr(self.packed(dev)),
+                                               _lib.ptr(eps), _lib.ptr(z), _lib.ptr(lq_mol), _lib.ptr(lq),
+                                               _lib.stream_ptr(dev)), "enflow_argmax_forward_f32")
+        return z.to(h.dtype), lq.reshape(()).to(h.dtype)
+
+    def reverse(self, z):
+        return one_hot(torch.argmax(z, dim=-1), dtype=z.dtype)

@@ -1,0 +1,123 @@
+"""EGCL message-passing block (mirrors enflow/nn/egcl.py:6-92).
+
+Same constructor, same sub-module and parameter names (edge_nn, node_nn,
+coord_nn, vel_scaling_nn) and the same initialisation order, so a reference
+state_dict loads unchanged and a given torch seed yields the same weights.
+``forward(h, edges)`` returns (Q [n, 1], F [n, 3], G [n, nf]) computed by
+enflow_egcl_forward_f32: neighbour list, per-edge MLP chain on MFMA and the
+segment reductions all run in one HIP kernel per molecule.
+"""
+import warnings
+
+import torch
+from torch import nn
+
+from .. import _lib
+from ..data.base import Edges
+
+
+class EGCL(nn.Module):
+    def __init__(self, input_nf, output_nf, hidden_nf, act_fn=nn.SiLU(), coords_weight=1.0,
+                 attention=False, clamp=False, norm_diff=False, tanh=False):
+        super().__init__()
+        input_edge = input_nf * 2
+        self.input_nf, self.output_nf, self.hidden_nf = input_nf, output_nf, hidden_nf
+        self.coords_weight = coords_weight
+        self.attention = attention
+        self.norm_diff = norm_diff
+        self.tanh = tanh
+        self.act_fn = act_fn
+        edge_coords_nf = 1
+        # construction order = reference order (egcl.py:12-55): same RNG stream
+        self.edge_nn = nn.Sequential(nn.Linear(input_edge + edge_coords_nf, hidden_nf), act_fn,
+                                     nn.Linear(hidden_nf, hidden_nf), act_fn)
+        self.node_nn = nn.Sequential(nn.Linear(hidden_nf + input_nf, hidden_nf), act_fn,
+                                     nn.Linear(hidden_nf, output_nf))
+        layer = nn.Linear(hidden_nf, 1, bias=False)
+        torch.nn.init.xavier_uniform_(layer.weight, gain=0.001)
+        self.clamp = clamp
+        coord_nn = [nn.Linear(hidden_nf, hidden_nf), act_fn, layer]
+        if self.tanh:
+            coord_nn.append(nn.Tanh())
+            self.coords_range = nn.Parameter(torch.ones(1)) * 3
+        self.coord_nn = nn.Sequential(*coord_nn)
+        if self.attention:
+            self.att_nn = nn.Sequential(nn.Linear(hidden_nf, 1), nn.Sigmoid())
+        self.vel_scaling_nn = nn.Sequential(nn.Linear(input_nf, hidden_nf), act_fn,
+                                            nn.Linear(hidden_nf, 1))
+        self._packed = None
+        self._packed_key = None
+
+    # ------------------------------------------------------------------
+    def hip_supported(self):
+        """The HIP kernels implement the reference defaults used by main.py."""
+        L = _lib.lib()
+        return (not self.attention and not self.norm_diff and not self.tanh
+                and isinstance(self.act_fn, nn.SiLU) and self.input_nf == self.output_nf
+                and 1 <= self.input_nf <= L.enflow_max_node_nf()
+                and bool(L.enflow_supports_hidden(self.hidden_nf)))
+
+    def _check_supported(self):
+        if not self.hip_supported():
+            raise NotImplementedError(
+                "enflow_amd EGCL kernels implement attention=False, norm_diff=False, tanh=False, "
+                "SiLU, input_nf == output_nf <= 8 and hidden_nf in {32, 64, 128}")
+
+    def raw_parameters(self):
+        """Parameters in named_parameters() order, as the C ABI expects."""
+        return [p for _, p in self.named_parameters()]
+
+    def packed(self, device):
+        """MFMA-fragment packed fp32 weights on `device` (cached, re-packed when
+        any parameter changes)."""
+        params = self.raw_parameters()
+        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        L = _lib.lib()
+        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in params])
+        size = L.enflow_egcl_packed_size(self.hidden_nf, self.input_nf)
+        out = torch.empty(size, dtype=torch.float32, device=device)
+        _lib.check(L.enflow_pack_egcl_f32(_lib.ptr(raw), self.hidden_nf, self.input_nf, _lib.ptr(out),
+                                          _lib.stream_ptr(device)), "enflow_pack_egcl_f32")
+        self._packed, self._packed_key = out, key
+        return out
+
+    def pack_into(self, dst):
+        """Pack into a slice of a caller-owned buffer (used by the fused flow)."""
+        L = _lib.lib()
+        device = dst.device
+        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
+                         for p in self.raw_parameters()])
+        _lib.check(L.enflow_pack_egcl_f32(_lib.ptr(raw), self.hidden_nf, self.input_nf, _lib.ptr(dst),
+                                          _lib.stream_ptr(device)), "enflow_pack_egcl_f32")
+
+    # ------------------------------------------------------------------
+    def forward(self, h, edges):
+        if not isinstance(edges, Edges):
+            raise TypeError("EGCL.forward expects the Edges handle returned by Data.edges")
+        self._check_supported()
+        _lib.require_gpu(h)
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            warnings.warn("enflow_amd EGCL: HIP backward is not implemented yet; outputs are "
+                          "detached", RuntimeWarning, stacklevel=2)
+        L = _lib.lib()
+        dev = h.device
+        n = h.shape[0]
+        nf = self.input_nf
+        hf = h.detach().to(torch.float32).contiguous()
+        pos = edges.pos.detach().to(torch.float32).contiguous()
+        box = edges.box.detach().to(torch.float32).contiguous()
+        rc = torch.as_tensor(edges.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous()
+        Q = torch.empty(n, dtype=torch.float32, device=dev)
+        F = torch.empty((n, 3), dtype=torch.float32, device=dev)
+        G = torch.empty((n, nf), dtype=torch.float32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(L.enflow_egcl_forward_f32(edges.num_mols, n, edges.max_mol_atoms, nf, self.hidden_nf,
+                                             _lib.ptr(edges.mol_ptr), _lib.ptr(rc), _lib.ptr(box),
+                                             _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),
+                                             float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F),
+                                             _lib.ptr(G), _lib.ptr(err), _lib.stream_ptr(dev)),
+                   "enflow_egcl_forward_f32")
+        _lib.raise_on_err(err)
+        return (Q.reshape(n, 1).to(h.dtype), F.to(h.dtype), G.to(h.dtype))

@@ -1,0 +1,44 @@
+"""Small tensor helpers mirroring enflow/utils/helpers.py.
+
+These are the element-wise / bookkeeping helpers of the reference's public
+API.  The hot path (edges, EGCL, flow, loss) never calls them: it runs inside
+the HIP kernels of libenflow_hip.so.
+"""
+import math
+
+import torch
+
+
+def log_gaussian(z):
+    """enflow/utils/helpers.py:4-5 (one log(2 pi) for the whole tensor)."""
+    return -0.5 * ((z ** 2).sum() + math.log(2 * math.pi))
+
+
+def apply_pbc(pos, box):
+    """enflow/utils/helpers.py:7-8."""
+    return pos - (pos / box).round() * box
+
+
+def get_box_len(pos):
+    """enflow/utils/helpers.py:10-13."""
+    return (pos.max(dim=0)[0] - pos.min(dim=0)[0]).round()
+
+
+def one_hot(index, num_classes=None, dtype=None):
+    """enflow/utils/helpers.py:43-52 (width = max + 1 when num_classes is None)."""
+    if index.dim() != 1:
+        raise ValueError("'index' tensor needs to be one-dimensional")
+    if num_classes is None:
+        num_classes = int(index.max()) + 1
+    out = torch.zeros((index.size(0), num_classes), dtype=dtype, device=index.device)
+    return out.scatter_(1, index.unsqueeze(1), 1)
+
+
+def mol_ptr_from_counts(N, device=None):
+    """CSR atom offsets (int32, [M+1]) from per-molecule atom counts Data.N."""
+    N = torch.as_tensor(N)
+    if N.ndim == 0:
+        N = N.reshape(1)
+    ptr = torch.zeros(N.numel() + 1, dtype=torch.int32, device=device if device is not None else N.device)
+    ptr[1:] = torch.cumsum(N.to(ptr.device), 0).to(torch.int32)
+    return ptr

@@ -1,0 +1,167 @@
+/*
+ * enflow_hip.h -- C ABI of the MI355X (gfx950) coupling-flow hot path.
+ *
+ * The reference (bharath-raghavan/enflow) is pure Python/PyTorch; it has no
+ * FFI.  Each entry point below replaces one operator of the reference's
+ * nn.Module surface (cited per function) and is bound from Python with ctypes
+ * by enflow_amd/_lib.py (see INTEGRATION.md for the binding a maintainer of the
+ * reference would add).
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer (hipMalloc / torch CUDA storage) unless
+ *     documented otherwise; sizes are element counts;
+ *   - a batch is the concatenation of molecules (the reference's Data layout,
+ *     enflow/data/base.py:21-50): mol_ptr[num_mols + 1] (int32) holds the
+ *     atom offsets, per-atom arrays are row-major [num_atoms][k];
+ *   - stream is a hipStream_t passed as void* (NULL = default stream);
+ *   - return value 0 = launched, < 0 = argument error (nothing launched);
+ *     data-dependent faults the reference would raise on (e.g. fewer periodic
+ *     images than atoms) are reported through err_flag (device int32, OR-ed
+ *     ENFLOW_ERR_* bits) which the host reads after the stream syncs.
+ *   - max_mol_atoms is the largest molecule in the batch (host-known from
+ *     Data.N); it selects the kernel instantiation (<= 32 or <= 64 atoms);
+ *   - all arithmetic is float32 (the reference computes in float64; parity is
+ *     1e-5 relative).
+ */
+#ifndef ENFLOW_HIP_H
+#define ENFLOW_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ENFLOW_ERR_TOO_MANY_ATOMS   1  /* molecule larger than the kernel's NMAX */
+#define ENFLOW_ERR_FEW_IMAGES       2  /* reference would IndexError (base.py:137) */
+#define ENFLOW_ERR_TOO_MANY_FEATURES 4
+
+#define ENFLOW_DEQUANT_NONE   0
+#define ENFLOW_DEQUANT_ARGMAX 1  /* enflow/nn/argmax.py */
+#define ENFLOW_DEQUANT_FLOOR  2  /* enflow/nn/floor.py  */
+
+/* ABI version of this header; bump on any signature change. */
+int enflow_abi_version(void);
+
+/* Largest molecule (atoms) / node_nf the compiled kernels accept. */
+int enflow_max_atoms(void);
+int enflow_max_node_nf(void);
+/* 1 if hidden_nf is one of the compiled widths (32, 64, 128). */
+int enflow_supports_hidden(int hidden_nf);
+
+/* Floats needed to hold one packed EGCL layer / one packed ArgMax network. */
+int64_t enflow_egcl_packed_size(int hidden_nf, int node_nf);
+int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf);
+
+/*
+ * Pack one EGCL layer's parameters (torch nn.Linear layouts, concatenated in
+ * named_parameters() order of enflow/nn/egcl.py:12-55 with the default flags:
+ *   edge_nn.0.weight [H][2nf+1], edge_nn.0.bias [H], edge_nn.2.weight [H][H],
+ *   edge_nn.2.bias [H], node_nn.0.weight [H][H+nf], node_nn.0.bias [H],
+ *   node_nn.2.weight [nf][H], node_nn.2.bias [nf], coord_nn.0.weight [H][H],
+ *   coord_nn.0.bias [H], coord_nn.2.weight [1][H], vel_scaling_nn.0.weight
+ *   [H][nf], vel_scaling_nn.0.bias [H], vel_scaling_nn.2.weight [1][H],
+ *   vel_scaling_nn.2.bias [1])
+ * into the MFMA-fragment layout the flow kernels read.
+ */
+int enflow_pack_egcl_f32(const float* raw, int hidden_nf, int node_nf,
+                         float* packed, void* stream);
+
+/* Pack ArgMax.network (enflow/nn/argmax.py:6-10): network.0.weight [H][nf],
+ * network.0.bias [H], network.2.weight [2nf][H], network.2.bias [2nf]. */
+int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,
+                           float* packed, void* stream);
+
+/*
+ * LFIntegrator.forward (enflow/flow/dynamics.py:10-24), all layers fused:
+ * dequantisation, then per layer the periodic neighbour list
+ * (Data.edges, enflow/data/base.py:122-144), EGCL.forward
+ * (enflow/nn/egcl.py:76-92) and the leapfrog update, accumulating log|detJ|.
+ *   layers      : n_layers packed EGCL layers, back to back
+ *                 (stride enflow_egcl_packed_size)
+ *   dequant     : packed ArgMax (kind ARGMAX), ignored otherwise
+ *   noise       : [num_atoms][nf]; N(0,1) draws for ARGMAX
+ *                 (torch.randn in argmax.py:16), U[0,1) for FLOOR
+ *   dequant_scale: Floor.dequant_scale
+ *   h, g [num_atoms][nf], pos, vel [num_atoms][3] : updated in place
+ *   box [num_atoms][3], r_cut [num_mols]
+ *   ldj_mol [num_mols] : per-molecule log|detJ| contributions (out)
+ *   ldj_total [1]      : batch log|detJ| exactly as the reference's scalar (out)
+ */
+int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                          const int32_t* mol_ptr, const float* r_cut, const float* box,
+                          float* h, float* g, float* pos, float* vel,
+                          const float* layers, int n_layers,
+                          int dequant_kind, const float* dequant, const float* noise,
+                          float dequant_scale, float dt, float coords_weight,
+                          float* ldj_mol, float* ldj_total, int32_t* err_flag,
+                          void* stream);
+
+/*
+ * LFIntegrator.reverse (enflow/flow/dynamics.py:26-37), all layers fused.
+ * h, g, pos, vel updated in place.  With ARGMAX the final ArgMax.reverse
+ * (argmax.py:27-28) is split: argmax_idx [num_atoms] (out) receives the index
+ * of the first maximum and max_idx [1] (out) its batch maximum, and
+ * enflow_one_hot_f32 then writes the one-hot rows (width max_idx + 1, as
+ * helpers.one_hot without num_classes).  With FLOOR h is floored in place.
+ */
+int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                          const int32_t* mol_ptr, const float* r_cut, const float* box,
+                          float* h, float* g, float* pos, float* vel,
+                          const float* layers, int n_layers,
+                          int dequant_kind, float dt, float coords_weight,
+                          int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
+                          void* stream);
+
+/* helpers.one_hot (enflow/utils/helpers.py:43-52): out[num_atoms][width]. */
+int enflow_one_hot_f32(const int32_t* idx, int num_atoms, int width, float* out,
+                       void* stream);
+
+/*
+ * One EGCL.forward (enflow/nn/egcl.py:76-92) on Data.edges built from pos
+ * (enflow/data/base.py:122-144): Q [num_atoms], F [num_atoms][3],
+ * G [num_atoms][nf] (out).
+ */
+int enflow_egcl_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                            const int32_t* mol_ptr, const float* r_cut, const float* box,
+                            const float* h, const float* pos, const float* layer,
+                            float coords_weight, float* Q, float* F, float* G,
+                            int32_t* err_flag, void* stream);
+
+/*
+ * ArgMax.forward (enflow/nn/argmax.py:13-25): z [num_atoms][nf] (out) and
+ * log_q [1] (out) with noise = the N(0,1) draw.
+ */
+int enflow_argmax_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                              const int32_t* mol_ptr, const float* h, const float* dequant,
+                              const float* noise, float* z, float* log_q_mol,
+                              float* log_q, void* stream);
+
+/*
+ * Data.edges (enflow/data/base.py:122-144) as unique pairs with multiplicity:
+ * pair_count[num_mols] (out) and, per molecule m, up to max_pairs entries at
+ * pairs[m * max_pairs + p] = row | col << 8 | mult << 16 (molecule-local atom
+ * indices, sorted by (row, col)); mult is how many times the reference's edge
+ * list holds (row, col).
+ */
+int enflow_neighbour_pairs_f32(int num_mols, int num_atoms, int max_mol_atoms, const int32_t* mol_ptr,
+                               const float* r_cut, const float* box, const float* pos,
+                               int max_pairs, uint32_t* pairs, int32_t* pair_count,
+                               int32_t* err_flag, void* stream);
+
+/*
+ * Alchemical_NLL.__call__ (enflow/flow/loss.py:21-24) on a flow output:
+ * nll_mol [num_mols][4] (out) = {LJ energy, sum vel^2, sum h^2, sum g^2}
+ * per molecule, loss [1] (out) the reference's scalar.
+ */
+int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf,
+                              const int32_t* mol_ptr, const float* h, const float* g,
+                              const float* pos, const float* vel, const float* ldj_total,
+                              float kBT, float softening, float partition_func,
+                              float* nll_mol, float* loss, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ENFLOW_HIP_H */

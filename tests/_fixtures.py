@@ -45,3 +45,32 @@ def rel_err(a, b):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def flow_from_fixture(inp, device="cuda"):
+    """enflow_amd LFIntegrator + Data carrying exactly the fixture's weights/inputs."""
+    import torch
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+
+    hid, nf, nl = int(inp["hid"]), inp["h"].shape[1], int(inp["n_layers"])
+    nets = []
+    for i in range(nl):
+        net = EGCL(nf, nf, hid)
+        net.load_state_dict({k: torch.tensor(inp[f"p{i}.{k}"]) for k in EGCL_KEYS})
+        nets.append(net)
+    am = ArgMax(nf, hid)
+    am.load_state_dict({k: torch.tensor(inp[f"dq.{k}"]) for k in ARGMAX_KEYS})
+    model = LFIntegrator(nets, am, dt=float(inp["dt"])).to(device)
+    return model, data_from_fixture(inp, device)
+
+
+def data_from_fixture(inp, device="cuda"):
+    import torch
+    from enflow_amd.data import Data
+
+    t = lambda k: torch.tensor(inp[k], dtype=torch.float32, device=device)  # noqa: E731
+    N = torch.tensor(np.diff(inp["mol_ptr"]), dtype=torch.long)
+    return Data(h=t("h"), g=t("g"), pos=t("pos"), vel=t("vel"), N=N, r_cut=t("r_cut"), box=t("box"),
+                device=device)

@@ -1,0 +1,233 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's golden
+vectors and the CPU oracle.  Tolerance (BASELINE.json north_star): float32
+results within 1e-5 relative of the float64 reference, measured normwise per
+tensor as max|a - b| / max|b|.  Integer / index results must be exact."""
+import collections
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import enflow_oracle as O
+from _fixtures import (load, layer_params, dequant_params, state, n_layers, rel_err,
+                       flow_from_fixture, data_from_fixture, EGCL_KEYS, ARGMAX_KEYS)
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+# ---------------------------------------------------------------------------
+# neighbour list (integer work: exact)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("tag", ["extent", "box20", "box5"])
+def test_neighbour_pairs_exact(tag):
+    inp, out = load(f"edges_{tag}")
+    d = data_from_fixture(inp, DEV)
+    e = d.edges
+    got = collections.Counter(zip(e.row.cpu().tolist(), e.col.cpu().tolist()))
+    ref = collections.Counter(zip(out["row"].tolist(), out["col"].tolist()))
+    assert got == ref
+    # coord_diff per (row, col), half-box image included
+    cd = e.coord_diff.cpu().numpy()
+    rows, cols = e.row.cpu().numpy(), e.col.cpu().numpy()
+    ref_cd = {}
+    for r, c, v in zip(out["row"], out["col"], out["coord_diff"]):
+        ref_cd[(int(r), int(c))] = v
+    want = np.stack([ref_cd[(int(r), int(c))] for r, c in zip(rows, cols)])
+    assert np.max(np.abs(cd - want)) < 1e-6
+
+
+# ---------------------------------------------------------------------------
+# single EGCL call
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("hid", [32, 128])
+def test_egcl_matches_reference(hid):
+    from enflow_amd.nn import EGCL
+    inp, out = load(f"egcl_h{hid}")
+    net = EGCL(5, 5, hid)
+    net.load_state_dict({k: torch.tensor(inp["p0." + k]) for k in EGCL_KEYS})
+    net = net.to(DEV)
+    d = data_from_fixture(inp, DEV)
+    with torch.no_grad():
+        q, f, g = net(d.h, d.edges)
+    assert rel_err(q.cpu().numpy(), out["Q"]) < TOL
+    assert rel_err(f.cpu().numpy(), out["F"]) < TOL
+    assert rel_err(g.cpu().numpy(), out["G"]) < TOL
+
+
+def test_argmax_matches_reference():
+    from enflow_amd.nn import ArgMax
+    inp, out = load("argmax_h32")
+    am = ArgMax(5, 32)
+    am.load_state_dict({k: torch.tensor(inp["dq." + k]) for k in ARGMAX_KEYS})
+    am = am.to(DEV)
+    h = torch.tensor(inp["h"], device=DEV)
+    z, lq = am(h, noise=torch.tensor(inp["eps"], device=DEV), N=np.diff(inp["mol_ptr"]))
+    assert rel_err(z.cpu().numpy(), out["z"]) < TOL
+    assert abs(float(lq) - float(out["log_q"])) <= TOL * abs(float(out["log_q"]))
+    np.testing.assert_array_equal(am.reverse(z).cpu().numpy(), out["reverse"])
+
+
+# ---------------------------------------------------------------------------
+# fused flow
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
+def test_lf_forward_matches_reference(name):
+    from enflow_amd.flow import Alchemical_NLL
+    inp, out = load(name)
+    model, d = flow_from_fixture(inp, DEV)
+    with torch.no_grad():
+        o, ldj = model(d, noise=torch.tensor(inp["eps"], device=DEV))
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), out[k]) < TOL, k
+    assert abs(float(ldj) - float(out["ldj"])) <= TOL * abs(float(out["ldj"]))
+    nll = Alchemical_NLL(kBT=float(inp["kBT"]), softening=float(inp["softening"]))(o, ldj)
+    assert abs(float(nll) - float(out["nll"])) <= TOL * abs(float(out["nll"]))
+
+
+@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
+def test_lf_reverse_matches_reference(name):
+    """generate direction: reverse of the reference's forward output."""
+    inp, out = load(name)
+    model, _ = flow_from_fixture(inp, DEV)
+    d = data_from_fixture(inp, DEV)
+    for k in ("h", "g", "pos", "vel"):
+        setattr(d, k, torch.tensor(out[k], dtype=torch.float32, device=DEV))
+    with torch.no_grad():
+        back = model.reverse(d)
+    np.testing.assert_array_equal(back.h.cpu().numpy(), out["rev_h"])
+    for k in ("g", "pos", "vel"):
+        assert rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) < 1e-4, k
+
+
+def _oracle_flow(model, batch, noise):
+    """Oracle run with the module's own fp32 weights (as float64)."""
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    dq = {k: v.detach().cpu().double().numpy() for k, v in model.dequantize.state_dict().items()}
+    return O.lf_forward(layers, dq, batch, noise.cpu().double().numpy(), model.dt)
+
+
+def _make_model(hid, nf, n_layers, seed, dt):
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    torch.manual_seed(seed)
+    return LFIntegrator([EGCL(nf, nf, hid) for _ in range(n_layers)], ArgMax(nf, hid), dt=dt).to(DEV)
+
+
+def _f32(b):
+    out = dict(b)
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        out[k] = b[k].astype(np.float32).astype(np.float64)
+    return out
+
+
+@pytest.mark.parametrize("sizes", [[1, 2, 22, 5], [64, 40, 33, 7], [22] * 12])
+def test_ragged_and_edge_sizes_vs_oracle(sizes):
+    """1- and 2-atom molecules, the 64-atom instantiation, uniform batches."""
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(len(sizes), sizes, nf=5, seed=sum(sizes)))
+    model = _make_model(64, 5, 3, 5, default_dt())
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV)
+    with torch.no_grad():
+        o, ldj = model(d, noise=noise)
+    ref, ref_ldj = _oracle_flow(model, b, noise)
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
+
+
+def test_floor_dequant_vs_oracle():
+    from enflow_amd.nn import EGCL, Floor
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(4, 22, nf=4, seed=3))
+    torch.manual_seed(1)
+    model = LFIntegrator([EGCL(4, 4, 32) for _ in range(2)], Floor(), dt=default_dt()).to(DEV)
+    d = Data.from_arrays(b, device=DEV)
+    u = torch.rand(d.h.shape, device=DEV)
+    with torch.no_grad():
+        o, ldj = model(d, noise=u)
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    ref, ref_ldj = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
+    with torch.no_grad():
+        back = model.reverse(o)
+    # floor(h + u) after an fp32 round trip: an element whose pre-floor value
+    # lands a hair under an integer legitimately floors down
+    assert (back.h.cpu().numpy() == np.floor(b["h"])).mean() > 0.99
+
+
+def test_too_large_molecule_raises():
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules
+    from enflow_amd import _lib
+    model = _make_model(32, 5, 1, 0, 0.01)
+    d = Data.from_arrays(make_molecules(1, 65, seed=0), device=DEV)
+    with pytest.raises(_lib.HipPathError):
+        with torch.no_grad():
+            model(d)
+
+
+# ---------------------------------------------------------------------------
+# benchmark-size configuration: size-independent properties + sampled oracle
+# ---------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def bench_run():
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(1024, 22, nf=5, seed=123))
+    model = _make_model(128, 5, 8, 7, default_dt())
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(9))
+    with torch.no_grad():
+        o1, l1 = model(d.clone(), noise=noise)
+        o2, l2 = model(d.clone(), noise=noise)
+    return b, model, d, noise, (o1, l1), (o2, l2)
+
+
+def test_bench_config_deterministic(bench_run):
+    _, _, _, _, (o1, l1), (o2, l2) = bench_run
+    for k in ("h", "g", "pos", "vel"):
+        assert torch.equal(getattr(o1, k), getattr(o2, k)), k
+    assert torch.equal(l1, l2)
+
+
+def test_bench_config_sampled_molecules_vs_oracle(bench_run):
+    """Molecules are independent: check a sample of the 1024 against the oracle."""
+    b, model, _, noise, (o1, _), _ = bench_run
+    ptr = b["mol_ptr"]
+    for m in (0, 1, 511, 1023):
+        a0, a1 = ptr[m], ptr[m + 1]
+        sub = {k: b[k][a0:a1] for k in ("h", "g", "pos", "vel", "box")}
+        sub["r_cut"] = b["r_cut"][m:m + 1]
+        sub["mol_ptr"] = np.array([0, a1 - a0])
+        ref, _ = _oracle_flow(model, sub, noise[a0:a1])
+        for k in ("h", "g", "pos", "vel"):
+            assert rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k]) < TOL, (m, k)
+
+
+def test_bench_config_roundtrip(bench_run):
+    """reverse(forward(x)) recovers the one-hot h exactly and pos/vel/g closely."""
+    b, model, d, _, (o1, _), _ = bench_run
+    with torch.no_grad():
+        back = model.reverse(o1.clone())
+    got = back.h.cpu().numpy()
+    assert got.shape[1] == int(np.argmax(b["h"], 1).max()) + 1     # reference one_hot width
+    np.testing.assert_array_equal(np.argmax(got, 1), np.argmax(b["h"], 1))
+    for k in ("g", "vel"):
+        assert rel_err(getattr(back, k).cpu().numpy(), b[k]) < 1e-3, k
+    # positions come back wrapped into the box (forward applies pbc each layer)
+    dpos = O.apply_pbc(back.pos.cpu().numpy() - b["pos"], b["box"])
+    assert np.max(np.abs(dpos)) < 1e-3 * np.max(np.abs(b["pos"]))

@@ -1,0 +1,106 @@
+"""CPU-only checks of the host side: the C ABI library loads and exports
+every symbol include/enflow_hip.h declares; argument validation works
+without launching anything; host helpers behave like the reference."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from enflow_amd import _lib
+from enflow_amd.data.synthetic import make_molecules
+from enflow_amd.utils.helpers import mol_ptr_from_counts, one_hot, apply_pbc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "enflow_hip.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(enflow_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    syms = header_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(L, s), s
+        assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+
+
+def test_abi_queries():
+    L = _lib.lib()
+    assert L.enflow_abi_version() == 1
+    assert L.enflow_max_atoms() == 64
+    assert L.enflow_max_node_nf() == 8
+    for h in (32, 64, 128):
+        assert L.enflow_supports_hidden(h) == 1
+        assert L.enflow_egcl_packed_size(h, 5) > 2 * h * h
+        assert L.enflow_egcl_packed_size(h, 5) % 64 == 0
+    assert L.enflow_supports_hidden(96) == 0
+    assert L.enflow_egcl_packed_size(96, 5) == -1
+    assert L.enflow_egcl_packed_size(128, 9) == -1
+
+
+def test_argument_errors_launch_nothing():
+    L = _lib.lib()
+    # too-large molecule, bad hidden width, bad nf: rejected before any launch
+    args = [1, 100, 100, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 4
+    assert L.enflow_lf_forward_f32(*args) == -3
+    args[2], args[4] = 20, 96
+    assert L.enflow_lf_forward_f32(*args) == -5
+    args[3], args[4] = 9, 128
+    assert L.enflow_lf_forward_f32(*args) == -4
+
+
+def test_synthetic_batch_layout():
+    b = make_molecules(5, [22, 3, 9, 22, 1], nf=5, seed=1)
+    assert b["mol_ptr"].tolist() == [0, 22, 25, 34, 56, 57]
+    assert b["h"].shape == (57, 5) and np.all(b["h"].sum(1) == 1)
+    # box of the first molecule reused for all (BaseDataset caches self.box)
+    assert np.all(b["box"] == b["box"][0])
+    for m in range(5):
+        x = b["pos"][b["mol_ptr"][m]:b["mol_ptr"][m + 1]]
+        assert np.allclose(x.mean(0), 0, atol=1e-12)
+
+
+def test_mol_ptr_and_helpers():
+    ptr = mol_ptr_from_counts(torch.tensor([3, 0, 2]))
+    assert ptr.tolist() == [0, 3, 3, 5] and ptr.dtype == torch.int32
+    oh = one_hot(torch.tensor([0, 2, 1]))
+    assert oh.shape == (3, 3)
+    oh = one_hot(torch.tensor([0, 1, 1]))
+    assert oh.shape == (3, 2)          # reference width = max + 1
+    x = torch.tensor([[0.6, -0.6, 1.5]])
+    assert torch.allclose(apply_pbc(x, torch.tensor([[1.0, 1.0, 1.0]])), torch.tensor([[-0.4, 0.4, -0.5]]))
+
+
+def test_hip_path_refuses_cpu_tensors():
+    from enflow_amd.nn import EGCL
+    from enflow_amd.data import Data
+    net = EGCL(5, 5, 32)
+    d = Data.from_arrays(make_molecules(1, 22, seed=0), device="cpu")
+    with pytest.raises(_lib.HipPathError):
+        net(d.h, d.edges)
+
+
+def test_module_surface_matches_reference_names():
+    """state_dict keys equal the reference's so its checkpoints load as-is."""
+    from enflow_amd.nn import EGCL, ArgMax
+    from _fixtures import EGCL_KEYS, ARGMAX_KEYS
+    assert tuple(EGCL(5, 5, 32).state_dict().keys()) == EGCL_KEYS
+    assert tuple(ArgMax(5, 32).state_dict().keys()) == ARGMAX_KEYS
+
+
+def test_same_seed_same_init_as_reference():
+    """Construction order mirrors egcl.py, so a seed gives the reference's weights."""
+    from _fixtures import load, EGCL_KEYS
+    from enflow_amd.nn import EGCL
+    inp, _ = load("egcl_h32")
+    torch.manual_seed(3)                       # make_golden.case_egcl(32, 3)
+    net = EGCL(5, 5, 32)
+    for k in EGCL_KEYS:
+        np.testing.assert_array_equal(net.state_dict()[k].numpy(), inp["p0." + k])
