@@ -1,0 +1,223 @@
+"""Benchmark: enflow LFIntegrator forward + log|detJ| on MI355X.
+
+Workload (BASELINE.json configs[1]): per GPU a batch of 1024 synthetic
+22-atom molecules, 8 EGCL coupling layers, hidden_nf 128, node_nf 5,
+float32, ArgMax dequantisation, periodic neighbour lists rebuilt every layer.
+One step = one fused forward over the batch (ArgMax noise drawn on device,
+inputs copied into the work buffers, ONE flow kernel + one reduce kernel),
+inputs already resident in HBM.
+
+Multi-GPU: one process per GPU (torch.distributed.run), molecules sharded
+across ranks (weak scaling: 1024 per GPU), no collective in the data path;
+barrier + synchronize around the timed region and the MAX time over ranks.
+
+Also reported (rank 0): the roofline of the flow kernel (algorithmic FLOPs
+from the kernel's own pair counters / its event-timed duration vs the f32
+MFMA peak) and the CPU oracle timed on a bounded sample (cpu_baseline).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "molecule-transforms/sec (fwd+log|detJ|), batch 1024×22 atoms, 1/2/4/8 GPU"
+PEAK_F32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
+MOLS_PER_GPU, ATOMS, LAYERS, HID, NF = 1024, 22, 8, 128, 5
+
+
+def flops_per_launch(pairs, atoms, layers, hid, nf):
+    """Algorithmic FLOPs of one forward launch.  Per unique neighbour pair:
+    edge_nn.0 (2nf+1 -> H), edge_nn.2 (H -> H), coord_nn.0 (H -> H),
+    coord_nn.2 (H -> 1); per atom and layer: vel_scaling_nn, node_nn; per
+    atom once: ArgMax.network.  Multiply-add = 2 FLOPs; activations excluded."""
+    per_pair = 2 * hid * (2 * nf + 1) + 4 * hid * hid + 2 * hid
+    per_atom_layer = (2 * hid * nf + 2 * hid) + (2 * hid * (hid + nf) + 2 * hid * nf)
+    per_atom_dq = 2 * hid * nf + 2 * hid * 2 * nf
+    return pairs * per_pair + atoms * layers * per_atom_layer + atoms * per_atom_dq
+
+
+def build_workload(rank, device):
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.utils.helpers import mol_ptr_from_counts
+    b = make_molecules(MOLS_PER_GPU, ATOMS, nf=NF, seed=1000 + rank)
+    torch.manual_seed(0)                    # same (random-init) weights on every rank
+    model = LFIntegrator([EGCL(NF, NF, HID) for _ in range(LAYERS)], ArgMax(NF, HID),
+                         dt=default_dt()).to(device)
+    f = lambda k: torch.tensor(b[k], dtype=torch.float32, device=device).contiguous()  # noqa: E731
+    inp = {k: f(k) for k in ("h", "g", "pos", "vel", "box", "r_cut")}
+    inp["mol_ptr"] = mol_ptr_from_counts(torch.tensor(np.diff(b["mol_ptr"])), device=device)
+    return b, model, inp
+
+
+def cpu_baseline(sample_mols=1536):
+    """The CPU oracle (numpy float64 port of the reference path) on a bounded
+    sample of the same workload, scaled to molecule-transforms/s."""
+    from oracle import enflow_oracle as O
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    from enflow_amd.nn import EGCL, ArgMax
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        threads = 1
+    torch.manual_seed(0)
+    nets = [EGCL(NF, NF, HID) for _ in range(LAYERS)]
+    am = ArgMax(NF, HID)
+    layers = [{k: v.double().numpy() for k, v in n.state_dict().items()} for n in nets]
+    dq = {k: v.double().numpy() for k, v in am.state_dict().items()}
+    b = make_molecules(sample_mols, ATOMS, nf=NF, seed=4242)
+    eps = np.random.default_rng(0).normal(size=b["h"].shape)
+    t0 = time.perf_counter()
+    O.lf_forward(layers, dq, b, eps, default_dt())
+    dt = time.perf_counter() - t0
+    return {"value": sample_mols / dt, "unit": "molecule-transforms/s", "cores": int(threads),
+            "kind": "port",
+            "sample": f"{sample_mols} molecules x {ATOMS} atoms, {LAYERS} layers, hidden {HID}, "
+                      f"numpy float64 oracle (oracle/enflow_oracle.py), {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per flow-kernel launch from the committed rocprofv3 PMC
+    summary (profiles/*pmc_traffic.json, written by profiles/collect_pmc.py),
+    if it was collected for this workload."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")), reverse=True):
+        try:
+            with open(path) as fh:
+                d = json.load(fh)
+            if d.get("workload") == workload_name():
+                return d.get("hbm_bytes_per_launch")
+        except Exception:
+            continue
+    return None
+
+
+def workload_name():
+    return f"lf_forward_{MOLS_PER_GPU}x{ATOMS}_L{LAYERS}_H{HID}_nf{NF}_f32"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=1536)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    b, model, inp = build_workload(rank, device)
+    n_atoms = inp["h"].shape[0]
+    work = {k: torch.empty_like(inp[k]) for k in ("h", "g", "pos", "vel")}
+    noise = torch.empty_like(inp["h"])
+    ldj_mol = torch.empty(MOLS_PER_GPU, dtype=torch.float32, device=device)
+    ldj = torch.empty(1, dtype=torch.float32, device=device)
+    err = torch.zeros(1, dtype=torch.int32, device=device)
+    stats = torch.zeros(2, dtype=torch.int64, device=device)
+    model.packed_layers(device)
+    model.dequantize.packed(device)
+    gen = torch.Generator(device).manual_seed(rank)
+
+    def step(st=None):
+        for k in work:
+            work[k].copy_(inp[k])
+        torch.randn(noise.shape, generator=gen, out=noise)
+        model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                              inp["mol_ptr"], ATOMS, noise, ldj_mol, ldj, err, st)
+
+    # one counted run: pair statistics for the roofline's algorithmic FLOPs
+    step(stats)
+    torch.cuda.synchronize()
+    pairs, edges = (int(x) for x in stats.tolist())
+    if int(err.item()) != 0:
+        raise RuntimeError(f"flow kernel error flag {int(err.item())}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # kernel-only timing with HIP events on the launch stream (torch's current stream)
+    stream = torch.cuda.current_stream(device)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for e0, e1 in evs:
+        for k in work:
+            work[k].copy_(inp[k])
+        torch.randn(noise.shape, generator=gen, out=noise)
+        e0.record(stream)
+        model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                              inp["mol_ptr"], ATOMS, noise, ldj_mol, ldj, err)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+    if rank == 0:
+        total_mols = MOLS_PER_GPU * world * args.steps
+        flops = flops_per_launch(pairs, n_atoms, LAYERS, HID, NF)
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        line = {
+            "metric": METRIC,
+            "value": total_mols / elapsed,
+            "unit": "molecule-transforms/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (random-walk 22-atom molecules, random-init weights)",
+            "config": {"workload": workload_name(), "molecules_per_gpu": MOLS_PER_GPU,
+                       "atoms_per_molecule": ATOMS, "coupling_layers": LAYERS, "hidden_nf": HID,
+                       "node_nf": NF, "global_batch": MOLS_PER_GPU * world,
+                       "parallelism": f"molecule-sharded x{world}",
+                       "unique_pairs_per_launch": pairs, "reference_edges_per_launch": edges},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS,
+                         "unit": "TFLOP/s", "frac": achieved / PEAK_F32_MFMA_TFLOPS,
+                         "traffic": load_traffic(), "kernel": "lf_flow_kernel<128,32,false>",
+                         "kernel_ms": kern_ms, "flops_per_launch": flops},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_sample)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

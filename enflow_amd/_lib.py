@@ -29,7 +29,7 @@ SIGNATURES = {
     "enflow_pack_egcl_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_pack_argmax_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_lf_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
-                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p]),
+                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p]),
     "enflow_lf_reverse_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                    _i, _f, _f, _p, _p, _p, _p]),
     "enflow_one_hot_f32": (_i, [_p, _i, _i, _p, _p]),

@@ -745,6 +745,7 @@ struct FlowArgs {
   int32_t* argmax_idx;
   int32_t* max_idx;
   int32_t* err;
+  unsigned long long* stats;   // optional: [0] += unique pairs, [1] += reference edges
 };
 
 enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
@@ -832,6 +833,12 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
       __syncthreads();
     }
     build_pairs(sm, Ml);
+    if (A.stats != nullptr && tid == 0) {
+      unsigned long long edges = 0;
+      for (int a = 0; a < n; ++a) edges += (unsigned long long)sm.cntrow[a];
+      atomicAdd(&A.stats[0], (unsigned long long)sm.npairs);
+      atomicAdd(&A.stats[1], edges);
+    }
     node_q(sm, Lp, L, n, nf);
     edge_tiles(sm, Lp, L, Ml, nf);
     node_g(sm, Lp, L, n, nf);
@@ -1097,14 +1104,16 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           const float* layers, int n_layers,
                           int dequant_kind, const float* dequant, const float* noise,
                           float dequant_scale, float dt, float cw,
-                          float* ldj_mol, float* ldj_total, int32_t* err_flag, void* stream) {
+                          float* ldj_mol, float* ldj_total, int32_t* err_flag, uint64_t* pair_stats,
+                          void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
   (void)num_atoms;
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
-             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag};
+             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
+             reinterpret_cast<unsigned long long*>(pair_stats)};
   if (num_mols > 0) {
 #define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
@@ -1126,7 +1135,7 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
   if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
   (void)num_atoms;
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
-             0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag};
+             0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag, nullptr};
   if (num_mols > 0) {
 #define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
@@ -1152,7 +1161,7 @@ int enflow_egcl_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int 
   if (rc) return rc;
   (void)num_atoms;
   FlowArgs A{mol_ptr, r_cut, box, const_cast<float*>(h), nullptr, const_cast<float*>(pos), nullptr, layer, 1, nf,
-             0, nullptr, nullptr, 0.f, 0.f, cw, nullptr, nullptr, nullptr, err_flag};
+             0, nullptr, nullptr, 0.f, 0.f, cw, nullptr, nullptr, nullptr, err_flag, nullptr};
   if (num_mols > 0) {
 #define CALL(HH, NN) hipLaunchKernelGGL((egcl_forward_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, Q, F, G)
     DISPATCH_HN(H, max_mol_atoms, CALL);
@@ -1168,7 +1177,7 @@ int enflow_argmax_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, in
   if (rc) return rc;
   (void)num_atoms;
   FlowArgs A{mol_ptr, nullptr, nullptr, const_cast<float*>(h), nullptr, nullptr, nullptr, nullptr, 0, nf,
-             ENFLOW_DEQUANT_ARGMAX, dequant, noise, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr};
+             ENFLOW_DEQUANT_ARGMAX, dequant, noise, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (num_mols > 0) {
 #define CALL(HH, NN) hipLaunchKernelGGL((argmax_forward_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, z, log_q_mol)
     DISPATCH_HN(H, max_mol_atoms, CALL);
@@ -1185,7 +1194,7 @@ int enflow_neighbour_pairs_f32(int num_mols, int num_atoms, int max_mol_atoms, c
   if (num_mols < 0 || max_mol_atoms > 64 || max_pairs < 0) return -1;
   (void)num_atoms;
   FlowArgs A{mol_ptr, r_cut, box, nullptr, nullptr, const_cast<float*>(pos), nullptr, nullptr, 0, 1,
-             0, nullptr, nullptr, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, err_flag};
+             0, nullptr, nullptr, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, err_flag, nullptr};
   if (num_mols > 0) {
     if (max_mol_atoms <= 32)
       hipLaunchKernelGGL((neighbour_pairs_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);

@@ -72,7 +72,7 @@ class LFIntegrator(BaseFlow):
 
     # ------------------------------------------------------------------
     def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
-                        ldj_mol, ldj_total, err):
+                        ldj_mol, ldj_total, err, pair_stats=None):
         """In-place fused forward on preallocated fp32 device buffers (no
         host sync, no allocation): the entry point the benchmark times."""
         hid, nf, cw = self._geometry()
@@ -86,7 +86,7 @@ class LFIntegrator(BaseFlow):
             _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
             _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
             _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
-            _lib.ptr(err), _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
+            _lib.ptr(err), _lib.ptr(pair_stats), _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
 
     def _state(self, data):
         _lib.require_gpu(data.pos)

@@ -87,6 +87,8 @@ int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,
  *   box [num_atoms][3], r_cut [num_mols]
  *   ldj_mol [num_mols] : per-molecule log|detJ| contributions (out)
  *   ldj_total [1]      : batch log|detJ| exactly as the reference's scalar (out)
+ *   pair_stats [2]     : optional (NULL = off); += unique neighbour pairs and
+ *                        += reference edge-list entries, summed over layers
  */
 int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
                           const int32_t* mol_ptr, const float* r_cut, const float* box,
@@ -95,7 +97,7 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
                           int dequant_kind, const float* dequant, const float* noise,
                           float dequant_scale, float dt, float coords_weight,
                           float* ldj_mol, float* ldj_total, int32_t* err_flag,
-                          void* stream);
+                          uint64_t* pair_stats, void* stream);
 
 /*
  * LFIntegrator.reverse (enflow/flow/dynamics.py:26-37), all layers fused.
