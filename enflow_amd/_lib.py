@@ -9,7 +9,7 @@ import os
 
 import torch
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libenflow_hip.so")
+LIB_PATH = os.environ.get("ENFLOW_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libenflow_hip.so")
 
 ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2

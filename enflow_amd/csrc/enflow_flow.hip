@@ -789,13 +789,38 @@ __device__ __forceinline__ bool load_molecule(Smem<H, NMAX>& sm, const FlowArgs&
 }
 
 // ---------------------------------------------------------------------------
+// diagnostic phase stamps (compiled only with -DENFLOW_STAMPS; never in the
+// product library): per phase, the summed shader-clock cycles of wave 0 of
+// every workgroup, measured between the phase's enclosing barriers.
+#ifdef ENFLOW_STAMPS
+#define NSTAMP 8
+__device__ unsigned long long enflow_stamp_acc[NSTAMP];
+#define STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[NSTAMP] = {0};
+#define STAMP(k)                                               \
+  do {                                                         \
+    unsigned long long now_ = __builtin_amdgcn_s_memtime();    \
+    st_acc[k] += now_ - st_prev;                               \
+    st_prev = now_;                                            \
+  } while (0)
+#define STAMP_FLUSH                                                              \
+  if (threadIdx.x == 0)                                                          \
+    for (int k_ = 0; k_ < NSTAMP; ++k_) atomicAdd(&enflow_stamp_acc[k_], st_acc[k_]);
+#else
+#define STAMP_DECL
+#define STAMP(k) do {} while (0)
+#define STAMP_FLUSH
+#endif
+
+// ---------------------------------------------------------------------------
 // the fused flow kernel (forward or reverse)
 // ---------------------------------------------------------------------------
 template <int H, int NMAX, bool REV>
 __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
   __shared__ Smem<H, NMAX> sm;
   MolRef M;
+  STAMP_DECL
   if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) return;
+  STAMP(0);
   const int tid = threadIdx.x;
   const int n = M.n, nf = A.nf;
   const EgclLayout L = egcl_layout(H, nf);
@@ -813,6 +838,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
       __syncthreads();
     }
   }
+  STAMP(1);
 
   for (int it = 0; it < A.n_layers; ++it) {
     // Opaque per-layer copies: stop hipcc from hoisting every nf / molecule
@@ -833,6 +859,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
       __syncthreads();
     }
     build_pairs(sm, Ml);
+    STAMP(2);
     if (A.stats != nullptr && tid == 0) {
       unsigned long long edges = 0;
       for (int a = 0; a < n; ++a) edges += (unsigned long long)sm.cntrow[a];
@@ -840,8 +867,11 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
       atomicAdd(&A.stats[1], edges);
     }
     node_q(sm, Lp, L, n, nf);
+    STAMP(3);
     edge_tiles(sm, Lp, L, Ml, nf);
+    STAMP(4);
     node_g(sm, Lp, L, n, nf);
+    STAMP(5);
     for (int a = tid; a < n; a += BLOCK) {
       const float q = sm.Q[a];
       const float eq = expf(q);
@@ -868,6 +898,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
       }
     }
     __syncthreads();
+    STAMP(6);
   }
 
   if (REV) {   // dequantize.reverse (argmax.py:27-28 / floor.py:13)
@@ -899,6 +930,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_flow_kernel(FlowArgs A) {
     if (tid == 0) A.ldj_mol[blockIdx.x] = s;
   }
   if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
+  STAMP(7);
+  STAMP_FLUSH
 }
 
 // one EGCL.forward: Q, F, G to global
@@ -1061,6 +1094,18 @@ static const double kLog2Pi = 1.8378770664093453;
   } while (0)
 
 extern "C" {
+
+#ifdef ENFLOW_STAMPS
+int enflow_read_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(enflow_stamp_acc), sizeof(unsigned long long) * NSTAMP) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[NSTAMP] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enflow_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return NSTAMP;
+}
+#endif
 
 int enflow_abi_version(void) { return ENFLOW_ABI; }
 int enflow_max_atoms(void) { return 64; }

@@ -1,0 +1,53 @@
+"""Diagnostic: per-phase cycle shares of the fused flow kernel.
+
+Builds libenflow_hip_stamps.so (-DENFLOW_STAMPS, never shipped as the product
+library), runs the bench workload through it and prints the share of wave-0
+cycles spent in each phase.  Usage (GPU box): python tools/stamps.py
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO = os.path.join(ROOT, "enflow_amd", "libenflow_hip_stamps.so")
+PHASES = ["load", "dequant", "pairs", "node_q", "edge_tiles", "node_g", "update", "writeback"]
+
+
+def main():
+    if not os.path.exists(SO):
+        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+                        "-DENFLOW_STAMPS", "-I", os.path.join(ROOT, "include"), "-o", SO,
+                        os.path.join(ROOT, "enflow_amd", "csrc", "enflow_flow.hip")], check=True)
+    os.environ["ENFLOW_LIB"] = SO
+    sys.path.insert(0, ROOT)
+    import torch
+    import bench
+    from enflow_amd import _lib
+    L = _lib.lib()
+    L.enflow_read_stamps.restype = ctypes.c_int
+    L.enflow_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    b, model, inp = bench.build_workload(0, dev)
+    work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
+    noise = torch.randn_like(inp["h"])
+    ldj_mol = torch.empty(bench.MOLS_PER_GPU, device=dev)
+    ldj = torch.empty(1, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    buf = (ctypes.c_ulonglong * 8)()
+    for rep in range(3):
+        for k in work:
+            work[k].copy_(inp[k])
+        torch.cuda.synchronize()
+        L.enflow_read_stamps(buf, 1)
+        model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                              inp["mol_ptr"], bench.ATOMS, noise, ldj_mol, ldj, err)
+        torch.cuda.synchronize()
+        L.enflow_read_stamps(buf, 1)
+    tot = sum(buf)
+    for name, v in zip(PHASES, buf):
+        print(f"{name:12s} {100.0 * v / tot:6.2f} %   {v / bench.MOLS_PER_GPU:12.0f} cycles/WG")
+
+
+if __name__ == "__main__":
+    main()
