@@ -1,0 +1,61 @@
+"""A/B several builds of libenflow_hip.so on the bench workload, interleaved
+rounds in ONE process (cdna_hip_programming.md rule 24).
+
+    python tools/ab_libs.py path/to/libA.so path/to/libB.so ...
+"""
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import bench
+    from enflow_amd import _lib
+    libs = sys.argv[1:]
+    dev = torch.device("cuda", 0)
+    b, model, inp = bench.build_workload(0, dev)
+    work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
+    noise = torch.randn_like(inp["h"])
+    ldj_mol = torch.empty(bench.MOLS_PER_GPU, device=dev)
+    ldj = torch.empty(1, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    outs = {}
+
+    def run(path, reps):
+        _lib._lib = None
+        _lib.LIB_PATH = path
+        model._layers_key = None
+        model.dequantize._packed_key = None
+        ts = []
+        for _ in range(reps):
+            for k in work:
+                work[k].copy_(inp[k])
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                                  inp["mol_ptr"], bench.ATOMS, noise, ldj_mol, ldj, err)
+            e1.record()
+            torch.cuda.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        outs[path] = (work["pos"].clone(), ldj.clone())
+        return ts
+
+    res = {p: [] for p in libs}
+    for p in libs:
+        run(p, 3)          # warm-up / pack
+    for rnd in range(6):
+        for p in libs:
+            res[p] += run(p, 5)
+    base = outs[libs[0]]
+    for p in libs:
+        same = torch.equal(outs[p][0], base[0])
+        print(f"{os.path.basename(p):40s} median {statistics.median(res[p]):.4f} ms  min {min(res[p]):.4f} ms"
+              f"  mol/s {bench.MOLS_PER_GPU / statistics.median(res[p]) * 1e3:.0f}  bitwise-equal-to-first {same}")
+
+
+if __name__ == "__main__":
+    main()

@@ -11,7 +11,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "enflow_amd", "libenflow_hip_stamps.so")
-PHASES = ["load", "dequant", "pairs", "node_q", "edge_tiles", "node_g", "update", "writeback"]
+PHASES = ["load", "dequant", "pairs", "-", "edge_tiles(all)", "node", "update", "writeback",
+          "  tiles:setup", "  gemm0", "  silu0", "  gemm1", "  silu1", "  segsum", "  gemm2+phi+force", "  tail-barrier"]
 
 
 def main():
@@ -34,7 +35,7 @@ def main():
     ldj_mol = torch.empty(bench.MOLS_PER_GPU, device=dev)
     ldj = torch.empty(1, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 16)()
     for rep in range(3):
         for k in work:
             work[k].copy_(inp[k])
@@ -44,7 +45,7 @@ def main():
                               inp["mol_ptr"], bench.ATOMS, noise, ldj_mol, ldj, err)
         torch.cuda.synchronize()
         L.enflow_read_stamps(buf, 1)
-    tot = sum(buf)
+    tot = sum(buf)       # every stamp closes the interval since the previous one: disjoint
     for name, v in zip(PHASES, buf):
         print(f"{name:12s} {100.0 * v / tot:6.2f} %   {v / bench.MOLS_PER_GPU:12.0f} cycles/WG")
 
