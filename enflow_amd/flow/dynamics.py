@@ -19,6 +19,7 @@ from .. import _lib
 from ..nn.argmax import ArgMax
 from ..nn.egcl import EGCL
 from ..nn.floor import Floor
+from ..utils.helpers import batch_meta
 from .base import BaseFlow
 
 
@@ -93,9 +94,10 @@ class LFIntegrator(BaseFlow):
         dev = data.pos.device
         f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous().clone()  # noqa: E731
         rc = torch.as_tensor(data.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous()
+        ptr, max_n = batch_meta(data, dev)
         return dict(h=f(data.h), g=f(data.g), pos=f(data.pos), vel=f(data.vel),
                     box=data.box.detach().to(device=dev, dtype=torch.float32).contiguous(), r_cut=rc,
-                    mol_ptr=data.mol_ptr, max_n=data.max_mol_atoms, dev=dev)
+                    mol_ptr=ptr, max_n=max_n, dev=dev)
 
     def forward(self, data, noise=None, check_errors=True):
         """dynamics.py:10-24.  ``noise`` optionally supplies the dequantiser's

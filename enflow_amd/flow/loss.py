@@ -8,6 +8,7 @@ reduction forms the reference's scalar.
 import torch
 
 from .. import _lib
+from ..utils.helpers import batch_meta
 
 
 class Alchemical_NLL:
@@ -22,12 +23,12 @@ class Alchemical_NLL:
         dev = out.pos.device
         f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
         h, g, pos, vel = f(out.h), f(out.g), f(out.pos), f(out.vel)
-        ptr = out.mol_ptr
+        ptr, max_n = batch_meta(out, dev)
         M = ptr.numel() - 1
         ldj_t = torch.as_tensor(ldj, device=dev).to(torch.float32).reshape(1).contiguous()
         nll_mol = torch.empty((max(M, 1), 4), dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
-        _lib.check(L.enflow_alchemical_nll_f32(M, h.shape[0], out.max_mol_atoms, h.shape[1], _lib.ptr(ptr),
+        _lib.check(L.enflow_alchemical_nll_f32(M, h.shape[0], max_n, h.shape[1], _lib.ptr(ptr),
                                                _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
                                                _lib.ptr(ldj_t), float(self.kBT), float(self.softening),
                                                float(self.z_lj), _lib.ptr(nll_mol), _lib.ptr(loss),

@@ -42,3 +42,17 @@ def mol_ptr_from_counts(N, device=None):
     ptr = torch.zeros(N.numel() + 1, dtype=torch.int32, device=device if device is not None else N.device)
     ptr[1:] = torch.cumsum(N.to(ptr.device), 0).to(torch.int32)
     return ptr
+
+
+def batch_meta(data, device):
+    """(mol_ptr int32 [M+1] on device, max atoms per molecule) for any batch
+    object with the reference's fields -- enflow_amd.data.Data caches them,
+    the reference's own enflow.data.base.Data only has N."""
+    ptr = getattr(data, "mol_ptr", None)
+    if ptr is None or ptr.device != device:
+        ptr = mol_ptr_from_counts(data.N, device=device)
+    mx = getattr(data, "max_mol_atoms", None)
+    if mx is None:
+        N = torch.as_tensor(data.N)
+        mx = int(N.max()) if N.numel() else 0
+    return ptr, mx
