@@ -164,10 +164,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    from enflow_amd.distributed import max_over_ranks
+    elapsed = max_over_ranks(elapsed, device)
 
     # kernel-only timing with HIP events on the launch stream (torch's current stream)
     stream = torch.cuda.current_stream(device)
