@@ -20,114 +20,12 @@
 //   3. deterministic segment sums of the edge messages and forces into per-atom
 //      LDS rows (each row written by the one wave holding its first pair, plus
 //      one ordered fix-up per wave boundary);
-//   4. node MLP (node_nn.0 on MFMA, node_nn.2 and vel_scaling_nn on VALU);
+//   4. node MLPs (vel_scaling_nn, node_nn) on MFMA, atoms on the lanes;
 //   5. leapfrog update + pbc, log|detJ| accumulation.
 //
 // All arithmetic is float32; MFMA f32 is an exact fmaf chain.
 
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <math.h>
-
-#include "enflow_hip.h"
-
-#define ENFLOW_ABI 1
-#define WAVES 4
-#define BLOCK 256
-#define NFMAX 8
-#define NFP 9  // LDS row stride of h / g / G (odd -> conflict-free across atoms)
-// ENFLOW_ABLATE (diagnostic builds only, outputs wrong): bit 1 = build pairs
-// only in layer 0, 2 = skip node phase, 4 = skip segment sums, 8 = SiLU -> identity,
-// 16 = skip GEMM2
-#ifndef ENFLOW_ABLATE
-#define ENFLOW_ABLATE 0
-#endif
-#ifndef ENFLOW_WAVES_PER_SIMD
-#define ENFLOW_WAVES_PER_SIMD 2   // workgroups of 4 waves per CU (VGPR budget 256 / 168 for 2 / 3)
-#endif
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// ---------------------------------------------------------------------------
-// layouts
-// ---------------------------------------------------------------------------
-// Row of the 32x32 f32 MFMA accumulator held by register r in lane half hh
-// (C/D map col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).
-__host__ __device__ constexpr int rho(int r, int hh) { return (r & 3) + 8 * (r >> 2) + 4 * hh; }
-
-__host__ __device__ inline int node_ksteps(int H, int nf) { return (H + nf + 1) / 2; }
-
-struct EgclLayout {
-  int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, total;
-};
-
-// Packed EGCL layer (floats).  *f / wn1h / wn1a sections are MFMA A-fragments
-// (32x32x2 f32: lane l supplies A[l & 31][k = l >> 5]).  The layout does not
-// depend on nf (features beyond nf are zero-padded), only its values do.
-__host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
-  (void)nf;
-  const int NT = H / 32;
-  EgclLayout L;
-  int o = 0;
-  L.we1f = o; o += NT * (NFMAX + 1) * 64;  // [t][slot][lane]: h_i pairs, h_j pairs, radial
-  L.we2f = o; o += H * H;                  // [tp][t][rg][lane][4], rho-permuted k
-  L.wc1f = o; o += H * H;                  // [tp][t][rg][lane][4], rho-permuted k
-  L.wn1h = o; o += NT * (NFMAX / 2) * 64;  // [tp][s][lane]: node_nn.0, h part
-  L.wn1a = o; o += NT * (H / 8) * 256;     // [tp][sg][lane][4]: node_nn.0, agg part
-  L.wv1f = o; o += NT * (NFMAX / 2) * 64;  // [tp][s][lane]: vel_scaling_nn.0
-  L.wn2f = o; o += NT * 4 * 256;           // [tp][rg][lane][4]: node_nn.2, rho-permuted k
-  L.be1 = o; o += H;
-  L.be2 = o; o += H;
-  L.bc1 = o; o += H;
-  L.wc2 = o; o += H;
-  L.bn1 = o; o += H;
-  L.bv1 = o; o += H;
-  L.wv2 = o; o += H;
-  L.bn2 = o; o += NFMAX;
-  L.bv2 = o; o += 4;
-  o = (o + 63) & ~63;
-  L.total = o;
-  return L;
-}
-
-struct RawEgcl {  // offsets into the raw (torch) concatenation
-  int We1, be1, We2, be2, Wn1, bn1, Wn2, bn2, Wc1, bc1, wc2, Wv1, bv1, Wv2, bv2, total;
-};
-__host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
-  RawEgcl R;
-  int o = 0;
-  R.We1 = o; o += H * (2 * nf + 1);
-  R.be1 = o; o += H;
-  R.We2 = o; o += H * H;
-  R.be2 = o; o += H;
-  R.Wn1 = o; o += H * (H + nf);
-  R.bn1 = o; o += H;
-  R.Wn2 = o; o += nf * H;
-  R.bn2 = o; o += nf;
-  R.Wc1 = o; o += H * H;
-  R.bc1 = o; o += H;
-  R.wc2 = o; o += H;
-  R.Wv1 = o; o += H * nf;
-  R.bv1 = o; o += H;
-  R.Wv2 = o; o += H;
-  R.bv2 = o; o += 1;
-  R.total = o;
-  return R;
-}
-
-struct AmLayout { int wa1t, ba1, wa2, ba2, total; };
-__host__ __device__ inline AmLayout argmax_layout(int H, int nf) {
-  AmLayout L;
-  int o = 0;
-  L.wa1t = o; o += nf * H;   // [q][k]
-  L.ba1 = o; o += H;
-  L.wa2 = o; o += 2 * nf * H; // [o][k] (torch layout)
-  L.ba2 = o; o += 2 * NFMAX;
-  o = (o + 63) & ~63;
-  L.total = o;
-  return L;
-}
+#include "flow_device.h"
 
 // ---------------------------------------------------------------------------
 // packing kernels
@@ -204,803 +102,6 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
     else { int e = idx - L.ba2; if (e < 2 * nf) v = raw[rb2 + e]; }
     out[idx] = v;
   }
-}
-
-// ---------------------------------------------------------------------------
-// device helpers
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-}
-
-typedef __amdgpu_buffer_rsrc_t rsrc_t;
-
-__device__ __forceinline__ rsrc_t weights_rsrc(const float* p, int nfloats) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, nfloats * 4, 0x00020000);
-}
-// voffset: per-lane bytes (VGPR), soffset: uniform bytes (SGPR, usually a constant)
-__device__ __forceinline__ float bload(rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
-__device__ __forceinline__ f32x4 bload4(rsrc_t r, int voff, int soff) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
-}
-
-__device__ __forceinline__ float silu_f(float x) {
-#if ENFLOW_ABLATE & 8
-  return x;
-#else
-  return x * __frcp_rn(1.0f + __expf(-x));
-#endif
-}
-
-__device__ __forceinline__ float pbc1(float x, float b) { return x - rintf(x / b) * b; }
-
-__device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
-__device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - log1pf(expf(-fabsf(x))); }
-
-// A wave's own LDS traffic is FIFO; this keeps the compiler from moving LDS
-// accesses across the point and drains outstanding ones.
-__device__ __forceinline__ void wave_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_wave_barrier();
-}
-
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int t = __shfl_up(v, off, 64);
-    if (lane >= off) v += t;
-  }
-  return v;
-}
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
-}
-
-// DPP moves (VALU, no LDS): row_shr:n = 0x110 + n, row_bcast:15 = 0x142.
-// Lanes whose source is outside the 16-lane row (or rows not in ROWMASK) get `old`.
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ int dpp_i(int old, int v) {
-  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xf, false);
-}
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xf, false));
-}
-
-// Segmented inclusive scan over the 32 pair-lanes of each wave half, for
-// contiguous segments (pairs are sorted by row): lane j ends with the sum of
-// its segment's values at lanes <= j.  m1..m16: 1.0 where the lane d to the
-// left (d = 1, 2, 4, 8, and lane 15 for the upper 16) is in the same segment.
-struct SegMasks { float m1, m2, m4, m8, m16; };
-
-__device__ __forceinline__ SegMasks seg_masks(int row) {
-  SegMasks M;
-  M.m1 = dpp_i<0x111, 0xf>(-0x7fffffff, row) == row ? 1.f : 0.f;
-  M.m2 = dpp_i<0x112, 0xf>(-0x7fffffff, row) == row ? 1.f : 0.f;
-  M.m4 = dpp_i<0x114, 0xf>(-0x7fffffff, row) == row ? 1.f : 0.f;
-  M.m8 = dpp_i<0x118, 0xf>(-0x7fffffff, row) == row ? 1.f : 0.f;
-  M.m16 = dpp_i<0x142, 0xa>(-0x7fffffff, row) == row ? 1.f : 0.f;
-  return M;
-}
-
-__device__ __forceinline__ float seg_scan(float v, const SegMasks& M) {
-  v = fmaf(M.m1, dpp_f<0x111, 0xf>(v), v);
-  v = fmaf(M.m2, dpp_f<0x112, 0xf>(v), v);
-  v = fmaf(M.m4, dpp_f<0x114, 0xf>(v), v);
-  v = fmaf(M.m8, dpp_f<0x118, 0xf>(v), v);
-  v = fmaf(M.m16, dpp_f<0x142, 0xa>(v), v);
-  return v;
-}
-
-
-// Chained GEMM  acc[tp] += W_packed[tp][t][r] * X[t][r]  over all (t, r):
-// X is an accumulator-layout register tile (lane = pair, registers = features
-// in rho order), W the fragment-packed [H][H] weight.  sched_barrier pins the
-// prefetch distance (hipcc otherwise hoists every fragment load: VGPRs).
-//  ENFLOW_CHAIN_WIDE=1: steps of NT*4 independent MFMAs (all output tiles),
-//                       fragments one step (>= 1024 cycles) ahead;
-//  ENFLOW_CHAIN_WIDE=0: one output tile at a time (a dependent MFMA chain runs
-//                       at the issue rate for 32x32x2), 3-deep fragment ring.
-#ifndef ENFLOW_CHAIN_WIDE
-#define ENFLOW_CHAIN_WIDE 1
-#endif
-template <int NT>
-__device__ __forceinline__ void chain_gemm_wide(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                                int lane) {
-  f32x4 cur[NT], nxt[NT];
-  const int vo = lane * 16;
-#pragma unroll
-  for (int tp = 0; tp < NT; ++tp) cur[tp] = bload4(W, vo, (off_floats + (tp * NT) * 4 * 256) * 4);
-#pragma unroll
-  for (int step = 0; step < NT * 4; ++step) {
-    const int t = step >> 2, rg = step & 3;
-    if (step + 1 < NT * 4) {
-      const int t2 = (step + 1) >> 2, rg2 = (step + 1) & 3;
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp) nxt[tp] = bload4(W, vo, (off_floats + ((tp * NT + t2) * 4 + rg2) * 256) * 4);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma32(cur[tp][u], X[t][4 * rg + u], acc[tp]);
-    __builtin_amdgcn_sched_barrier(0);
-    if (step + 1 < NT * 4) {
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp) cur[tp] = nxt[tp];
-    }
-  }
-}
-
-// Same wide chain with a VALU/LDS "filler" interleaved into every step: fill(step)
-// must not touch acc; sched_group_barrier asks hipcc to alternate one MFMA with
-// up to FPM filler instructions, so the filler issues while the MFMAs execute.
-template <int NT, int FPM, class Fill>
-__device__ __forceinline__ void chain_gemm_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                                int lane, Fill&& fill) {
-  f32x4 cur[NT], nxt[NT];
-  const int vo = lane * 16;
-#pragma unroll
-  for (int tp = 0; tp < NT; ++tp) cur[tp] = bload4(W, vo, (off_floats + (tp * NT) * 4 * 256) * 4);
-#pragma unroll
-  for (int step = 0; step < NT * 4; ++step) {
-    const int t = step >> 2, rg = step & 3;
-    if (step + 1 < NT * 4) {
-      const int t2 = (step + 1) >> 2, rg2 = (step + 1) & 3;
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp) nxt[tp] = bload4(W, vo, (off_floats + ((tp * NT + t2) * 4 + rg2) * 256) * 4);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma32(cur[tp][u], X[t][4 * rg + u], acc[tp]);
-    fill(step);
-#pragma unroll
-    for (int k = 0; k < 4 * NT; ++k) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);           // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, FPM, 0);   // VALU / DS
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (step + 1 < NT * 4) {
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp) cur[tp] = nxt[tp];
-    }
-  }
-}
-
-// one output tile: acc += sum_{t, r} W[tp][t][r] X[t][r], fragments 3 steps ahead
-template <int NT>
-__device__ __forceinline__ f32x16 chain_tile(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 acc, int tp,
-                                             int lane) {
-  constexpr int S = NT * 4;
-  const int vo = lane * 16;
-  f32x4 ring[3];
-#pragma unroll
-  for (int k = 0; k < 3 && k < S; ++k) ring[k] = bload4(W, vo, (off_floats + (tp * NT * 4 + k) * 256) * 4);
-#pragma unroll
-  for (int step = 0; step < S; ++step) {
-    const int t = step >> 2, rg = step & 3;
-    const f32x4 cur = ring[step % 3];
-    if (step + 3 < S) ring[step % 3] = bload4(W, vo, (off_floats + (tp * NT * 4 + step + 3) * 256) * 4);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) acc = mfma32(cur[u], X[t][4 * rg + u], acc);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  return acc;
-}
-
-template <int NT>
-__device__ __forceinline__ void chain_gemm(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                           int lane) {
-#if ENFLOW_CHAIN_WIDE
-  chain_gemm_wide<NT>(W, off_floats, X, acc, lane);
-#else
-#pragma unroll
-  for (int tp = 0; tp < NT; ++tp) acc[tp] = chain_tile<NT>(W, off_floats, X, acc[tp], tp, lane);
-#endif
-}
-
-// X[t][r] = silu(X[t][r] + bias[32 t + rho(r, hh)]); bias read from LDS as float4
-template <int NT>
-__device__ __forceinline__ void bias_silu(f32x16 (&X)[NT], const float* __restrict__ bias, int hh) {
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(bias + 32 * t + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) X[t][4 * g4 + u] = silu_f(X[t][4 * g4 + u] + b[u]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// diagnostic phase stamps (compiled only with -DENFLOW_STAMPS; never in the
-// product library): per phase, the summed shader-clock cycles of wave 0 of
-// every workgroup, measured between the phase's enclosing barriers.
-#ifdef ENFLOW_STAMPS
-#define NSTAMP 16
-__device__ unsigned long long enflow_stamp_acc[NSTAMP];
-#define STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[NSTAMP] = {0};
-#define STAMP_ARGS , unsigned long long& st_prev, unsigned long long (&st_acc)[NSTAMP]
-#define STAMP_PASS , st_prev, st_acc
-#define STAMP(k)                                               \
-  do {                                                         \
-    unsigned long long now_ = __builtin_amdgcn_s_memtime();    \
-    st_acc[k] += now_ - st_prev;                               \
-    st_prev = now_;                                            \
-  } while (0)
-#define STAMP_FLUSH                                                              \
-  if (threadIdx.x == 0)                                                          \
-    for (int k_ = 0; k_ < NSTAMP; ++k_) atomicAdd(&enflow_stamp_acc[k_], st_acc[k_]);
-#else
-#define STAMP_DECL
-#define STAMP_ARGS
-#define STAMP_PASS
-#define STAMP(k) do {} while (0)
-#define STAMP_FLUSH
-#endif
-
-// ---------------------------------------------------------------------------
-// shared memory
-// ---------------------------------------------------------------------------
-template <int H, int NMAX>
-struct Smem {
-  static constexpr int NT = H / 32;
-  static constexpr int AST = H + 5;   // agg row: H message sums, 3 force sums, pad (odd stride)
-  static constexpr int MAXP = NMAX * (NMAX - 1);
-  float pos[NMAX * 3], vel[NMAX * 3], boxa[NMAX * 3];
-  float h[NMAX * NFP], g[NMAX * NFP], G[NMAX * NFP];
-  float Q[NMAX];
-  alignas(16) float bias[4 * H];      // be1, be2, bc1, wc2 of the current layer
-  float agg[NMAX * AST];
-  float head[WAVES][H + 4];
-  float trash[WAVES][64];             // sink for the branch-free segment-sum stores
-  uint32_t pairs[MAXP];
-  uint32_t mask27[NMAX];
-  int idmap[NMAX];
-  int cntrow[NMAX];
-  int headrow[WAVES];
-  int ishead[WAVES];
-  int scan[WAVES];
-  int npairs;
-  int err;
-  float red[WAVES];
-  union {
-    int C[NMAX * NMAX];                                         // pair build
-    struct { float qp[NT][NMAX]; float gp[NT][NFMAX][NMAX]; } nd;  // node phase partials
-    float net[NMAX * 2 * NFMAX];                                // ArgMax outputs
-  } u;
-};
-
-struct MolRef {
-  int a0, n;
-  float rc;
-  float bx, by, bz;   // the molecule's edge box = box of its first atom (base.py:130)
-};
-
-// ---------------------------------------------------------------------------
-// neighbour list: Data.edges (enflow/data/base.py:122-144) for one molecule
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float shift_of(int idx, float b) { return idx == 0 ? -b : (idx == 1 ? b : 0.f); }
-
-template <int H, int NMAX>
-__device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, int tid) {
-  const int n = M.n;
-  const float rx = M.bx + M.rc, ry = M.by + M.rc, rz = M.bz + M.rc;   // helpers.py:20
-  for (int a = tid; a < n; a += BLOCK) {
-    sm.mask27[a] = 0u;
-    sm.idmap[a] = -1;
-    sm.cntrow[a] = 0;
-  }
-  for (int e = tid; e < n * n; e += BLOCK) sm.u.C[e] = 0;
-  __syncthreads();
-  // (a) image masks, one (atom, image) per thread: bit s <=> image s of atom a
-  //     lies in the ellipsoid with radii box + r_cut (helpers.py:17-22)
-  for (int e = tid; e < n * 27; e += BLOCK) {
-    const int a = e / 27, s = e - a * 27;
-    const float ix = sm.pos[a * 3 + 0] + shift_of(s % 3, M.bx);
-    const float iy = sm.pos[a * 3 + 1] + shift_of((s / 3) % 3, M.by);
-    const float iz = sm.pos[a * 3 + 2] + shift_of(s / 9, M.bz);
-    const float sx = ix / rx, sy = iy / ry, sz = iz / rz;
-    if (sx * sx + sy * sy + sz * sz <= 1.0f) atomicOr(&sm.mask27[a], 1u << s);
-  }
-  __syncthreads();
-  // (b) id_mapping[q] for q < n: the q-th surviving image in (image, atom) order (helpers.py:25-27)
-  if (tid < 64) {
-    const int lane = tid;
-    const uint32_t mk = lane < n ? sm.mask27[lane] : 0u;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int prefix = 0;
-    for (int s = 0; s < 27 && prefix < n; ++s) {
-      const bool bit = (mk >> s) & 1u;
-      const uint64_t bal = __ballot(bit);
-      if (bit) {
-        const int posF = prefix + __popcll(bal & lt);
-        if (posF < n) sm.idmap[posF] = lane;
-      }
-      prefix += __popcll(bal);
-    }
-    if (lane == 0 && prefix < n) sm.err |= ENFLOW_ERR_FEW_IMAGES;
-  }
-  __syncthreads();
-  // (c) multiplicity matrix: C[i][id_mapping[q]] += #images of i within r_cut of atom q
-  //     (base.py:133-139: both hit columns mapped through id_mapping, self pairs dropped)
-  const float r_sq = M.rc * M.rc;
-  for (int e = tid; e < n * n; e += BLOCK) {
-    const int i = e / n, q = e - i * n;
-    const int jl = sm.idmap[q];
-    if (jl == i || jl < 0) continue;   // jl < 0 only with ENFLOW_ERR_FEW_IMAGES
-    const uint32_t mk = sm.mask27[i];
-    const float px = sm.pos[i * 3 + 0], py = sm.pos[i * 3 + 1], pz = sm.pos[i * 3 + 2];
-    const float qx = sm.pos[q * 3 + 0], qy = sm.pos[q * 3 + 1], qz = sm.pos[q * 3 + 2];
-    int cnt = 0;
-    uint32_t bits = mk;
-    while (bits) {
-      const int s = __builtin_ctz(bits);
-      bits &= bits - 1;
-      const float ix = px + shift_of(s % 3, M.bx), iy = py + shift_of((s / 3) % 3, M.by),
-                  iz = pz + shift_of(s / 9, M.bz);
-      const float dx = ix - qx, dy = iy - qy, dz = iz - qz;
-      if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
-    }
-    if (cnt) {
-      atomicAdd(&sm.u.C[i * n + jl], cnt);
-      atomicAdd(&sm.cntrow[i], cnt);
-    }
-  }
-  __syncthreads();
-  // (d) compact to (row, col, mult) sorted by (row, col)
-  const int NN = n * n;
-  const int per = (NN + BLOCK - 1) / BLOCK;
-  const int e0 = tid * per, e1 = min(NN, e0 + per);
-  int local = 0;
-  for (int e = e0; e < e1; ++e) local += sm.u.C[e] > 0;
-  const int incl = wave_incl_scan(local);
-  const int lane = tid & 63, w = tid >> 6;
-  if (lane == 63) sm.scan[w] = incl;
-  __syncthreads();
-  int base = incl - local;
-  for (int k = 0; k < w; ++k) base += sm.scan[k];
-  for (int e = e0; e < e1; ++e) {
-    const int c = sm.u.C[e];
-    if (c > 0) {
-      const int i = e / n, jl = e - i * n;
-      sm.pairs[base++] = (uint32_t)i | ((uint32_t)jl << 8) | ((uint32_t)c << 16);
-    }
-  }
-  if (tid == BLOCK - 1) {
-    int tot = 0;
-    for (int k = 0; k < WAVES; ++k) tot += sm.scan[k];
-    sm.npairs = tot;
-  }
-  __syncthreads();
-}
-
-// ---------------------------------------------------------------------------
-// EGCL edge part: per-pair MLP chain on MFMA + deterministic segment sums
-// ---------------------------------------------------------------------------
-template <int H, int NMAX>
-__device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                           const MolRef& M, int nf, int tid STAMP_ARGS) {
-  constexpr int NT = H / 32;
-  constexpr int AST = Smem<H, NMAX>::AST;
-  const int lane = tid & 63, w = tid >> 6;
-  const int j = lane & 31, hh = lane >> 5;
-  const int n = M.n;
-  const int P = sm.npairs;
-  const int T = (P + 31) >> 5;
-  const int tpw = (T + WAVES - 1) / WAVES;
-
-  // zero aggregates / heads, stage biases, find each wave's head row
-  for (int e = tid; e < n * AST; e += BLOCK) sm.agg[e] = 0.f;
-  for (int e = tid; e < WAVES * (H + 4); e += BLOCK) (&sm.head[0][0])[e] = 0.f;
-  for (int k = tid; k < H; k += BLOCK) {
-    sm.bias[k] = Lp[L.be1 + k];
-    sm.bias[H + k] = Lp[L.be2 + k];
-    sm.bias[2 * H + k] = Lp[L.bc1 + k];
-    sm.bias[3 * H + k] = Lp[L.wc2 + k];
-  }
-  if (tid < WAVES) {
-    const int t0 = tid * tpw;
-    int hr = -1, ih = 0;
-    if (t0 < T) {
-      const int p0 = t0 * 32;
-      hr = (int)(sm.pairs[p0] & 0xffu);
-      ih = (p0 > 0) && ((int)(sm.pairs[p0 - 1] & 0xffu) == hr);
-    }
-    sm.headrow[tid] = hr;
-    sm.ishead[tid] = ih;
-  }
-  __syncthreads();
-
-  const int t0 = w * tpw, t1 = min(T, t0 + tpw);
-  const int headrow = sm.headrow[w];
-  const bool ishead = sm.ishead[w] != 0;
-  const int nh = (nf + 1) >> 1;
-  const rsrc_t W = weights_rsrc(Lp, L.total);
-  const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
-
-  STAMP(8);
-  for (int tile = t0; tile < t1; ++tile) {
-    const int p = tile * 32 + j;
-    const bool valid = p < P;
-    const uint32_t pr = valid ? sm.pairs[p] : 0u;
-    const int i = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
-    const float c = (float)(pr >> 16);
-    // segments = runs of equal row; invalid lanes get unique rows of their own
-    const int row = valid ? i : -1 - j;
-    const SegMasks SM = seg_masks(row);
-    const int row_next = __shfl_down(row, 1, 32);
-    const bool seg_end = valid && (j == 31 || row_next != row);
-    float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? i : 0) * AST];
-    // Edges.coord_diff with the reference's half-box image (base.py:15-19)
-    const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
-    const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
-    const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], hbz);
-    const float radial = dx * dx + dy * dy + dz * dz;                 // egcl.py:79
-
-    // ---- GEMM0: X0^T = edge_nn.0.weight . [h_i, h_j, radial]^T  (egcl.py:57-58)
-    //      9 fixed k-steps (zero-padded past nf): 4 h_i pairs, 4 h_j pairs, radial;
-    //      h rows are zero-padded in LDS, so padded steps multiply zeros
-    f32x16 x0[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
-    {
-      float cur[NT], nxt[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) cur[t] = bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1)) * 64) * 4);
-#pragma unroll
-      for (int s = 0; s < NFMAX + 1; ++s) {
-        if (s + 1 < NFMAX + 1) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) nxt[t] = bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s + 1) * 64) * 4);
-        }
-        const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh]
-                      : (s < NFMAX ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : (hh == 0 ? radial : 0.f));
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int t = 0; t < NT; ++t) x0[t] = mfma32(cur[t], b, x0[t]);
-        __builtin_amdgcn_sched_barrier(0);
-        if (s + 1 < NFMAX + 1) {
-#pragma unroll
-          for (int t = 0; t < NT; ++t) cur[t] = nxt[t];
-        }
-      }
-    }
-    STAMP(9);
-    // x0 tile 0 activated now, tiles 1.. as fillers of GEMM1's steps on tile t-1
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = silu_f(x0[0][4 * g4 + u] + b[u]);
-    }
-    STAMP(10);
-
-    // ---- GEMM1: E^T = edge_nn.2 (egcl.py:20-24)
-    f32x16 e[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) e[t] = (f32x16)0.f;
-    chain_gemm_fill<NT, 2>(W, L.we2f, x0, e, lane, [&](int step) {
-      const int t = (step >> 2) + 1, g4 = step & 3;
-      if (t < NT) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 32 * t + 8 * g4 + 4 * hh);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = silu_f(x0[t][4 * g4 + u] + b[u]);
-      }
-    });
-    STAMP(11);
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = silu_f(e[0][4 * g4 + u] + b[u]);
-    }
-    STAMP(12);
-    STAMP(13);
-    // ---- GEMM2: coord_nn.0 (egcl.py:35-42), with fillers: activate e tile t+1
-    //      and segment-sum the messages of tile t (egcl.py:64-65, multiplicity-
-    //      weighted, DPP segmented scan; the row's last lane adds to LDS, other
-    //      lanes add into a private trash slot -- branch-free)
-    float* const trash = &sm.trash[w][lane];
-    float* const dstm = seg_end ? dst_row : trash;
-    const int fstride = seg_end ? 1 : 0;
-    float part = 0.f;
-    {
-      f32x16 hc[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) hc[t] = (f32x16)0.f;
-#if ENFLOW_ABLATE & 16
-      for (int t = 0; t < NT; ++t) hc[t] = e[t];
-      if (0)
-#endif
-      chain_gemm_fill<NT, 6>(W, L.wc1f, e, hc, lane, [&](int step) {
-        const int t = step >> 2, g4 = step & 3;
-#if !(ENFLOW_ABLATE & 4)
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = seg_scan(c * e[t][4 * g4 + u], SM);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) dstm[(32 * t + 8 * g4 + 4 * hh + u) * fstride] += v[u];
-#endif
-        if (t + 1 < NT) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * (t + 1) + 8 * g4 + 4 * hh);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = silu_f(e[t + 1][4 * g4 + u] + b[u]);
-        }
-      });
-      // coord_nn.2 as a per-pair dot
-#pragma unroll
-      for (int tp = 0; tp < NT; ++tp)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 2 * H + 32 * tp + 8 * g4 + 4 * hh);
-          const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * tp + 8 * g4 + 4 * hh);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(hc[tp][4 * g4 + u] + b[u]);
-        }
-    }
-    const float phi = part + __shfl_xor(part, 32, 64);
-    // trans = clamp(coord_diff * phi, -100, 100) (egcl.py:71-72); segment sums
-    // for the mean (egcl.py:73-74); lane half 0 stores
-    const float tx = seg_scan(c * fminf(fmaxf(dx * phi, -100.f), 100.f), SM);
-    const float ty = seg_scan(c * fminf(fmaxf(dy * phi, -100.f), 100.f), SM);
-    const float tz = seg_scan(c * fminf(fmaxf(dz * phi, -100.f), 100.f), SM);
-    float* const dstf = (seg_end && hh == 0) ? dst_row : trash;
-    const int fs = (seg_end && hh == 0) ? 1 : 0;
-    dstf[(H + 0) * fs] += tx;
-    dstf[(H + 1) * fs] += ty;
-    dstf[(H + 2) * fs] += tz;
-    STAMP(14);
-  }
-  __syncthreads();
-  STAMP(15);
-  // ordered fix-up of rows that continue across a wave boundary
-  for (int f = tid; f < H + 3; f += BLOCK) {
-    for (int ww = 0; ww < WAVES; ++ww)
-      if (sm.ishead[ww]) sm.agg[sm.headrow[ww] * AST + f] += sm.head[ww][f];
-  }
-  __syncthreads();
-}
-
-// Node part of EGCL (egcl.py:26-30, 51-54, 62-67, 90-92), all on MFMA with
-// atoms on the pair lanes: wave item (tp, atom tile) computes
-//   Q partial   = vel_scaling_nn.2[32tp..] . silu(vel_scaling_nn.0 h)   (32 features)
-//   act         = silu(node_nn.0 [h, agg])                               (32 features)
-//   G partial   = node_nn.2[:, 32tp..] . act
-// and the NT partials are summed in fixed order (deterministic).
-template <int H, int NMAX>
-__device__ __forceinline__ void node_phase(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                           int n, int nf, int tid) {
-  constexpr int NT = H / 32;
-  constexpr int NA = NMAX / 32;
-  constexpr int AST = Smem<H, NMAX>::AST;
-  const int lane = tid & 63, w = tid >> 6;
-  const int j = lane & 31, hh = lane >> 5;
-  const int nh = (nf + 1) >> 1;
-  const rsrc_t W = weights_rsrc(Lp, L.total);
-  for (int item = w; item < NT * NA; item += WAVES) {
-    const int tp = item % NT, at = item / NT;
-    const int a = at * 32 + j;
-    const bool va = a < n;
-    const int ac = va ? a : 0;
-    // vel_scaling_nn: Q partial over this wave's 32 hidden features
-    f32x16 acc = (f32x16)0.f;
-    for (int s = 0; s < nh; ++s) {
-      const float b = va ? sm.h[ac * NFP + 2 * s + hh] : 0.f;
-      acc = mfma32(bload(W, lane * 4, (L.wv1f + (tp * (NFMAX / 2) + s) * 64) * 4), b, acc);
-    }
-    float part = 0.f;
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const int f0 = 32 * tp + 8 * g4 + 4 * hh;
-      const f32x4 b1 = bload4(W, 0, (L.bv1 + f0) * 4);
-      const f32x4 w2 = bload4(W, 0, (L.wv2 + f0) * 4);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(acc[4 * g4 + u] + b1[u]);
-    }
-    part += __shfl_xor(part, 32, 64);
-    if (hh == 0 && va) sm.u.nd.qp[tp][a] = part;
-    // node_nn.0 over [h, agg]
-    acc = (f32x16)0.f;
-    for (int s = 0; s < nh; ++s) {
-      const float b = va ? sm.h[ac * NFP + 2 * s + hh] : 0.f;
-      acc = mfma32(bload(W, lane * 4, (L.wn1h + (tp * (NFMAX / 2) + s) * 64) * 4), b, acc);
-    }
-    const float* arow = &sm.agg[ac * AST];
-#pragma unroll
-    for (int sg = 0; sg < H / 8; ++sg) {
-      const f32x4 a4 = bload4(W, lane * 16, (L.wn1a + (tp * (H / 8) + sg) * 256) * 4);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float b = va ? arow[2 * (4 * sg + u) + hh] : 0.f;
-        acc = mfma32(a4[u], b, acc);
-      }
-    }
-#pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b1 = bload4(W, 0, (L.bn1 + 32 * tp + 8 * g4 + 4 * hh) * 4);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(acc[4 * g4 + u] + b1[u]);
-    }
-    // node_nn.2 partial: rows q = rho(r, hh), only r < 4 (q < 8) can be < nf
-    f32x16 gacc = (f32x16)0.f;
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      const f32x4 a4 = bload4(W, lane * 16, (L.wn2f + (tp * 4 + rg) * 256) * 4);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) gacc = mfma32(a4[u], acc[4 * rg + u], gacc);
-    }
-    if (va) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = r + 4 * hh;
-        if (q < nf) sm.u.nd.gp[tp][q][a] = gacc[r];
-      }
-    }
-  }
-  __syncthreads();
-  const float bv2 = Lp[L.bv2];
-  for (int a = tid; a < n; a += BLOCK) {
-    float s = 0.f;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.qp[tp][a];
-    sm.Q[a] = s + bv2;
-  }
-  for (int e = tid; e < n * nf; e += BLOCK) {
-    const int a = e / nf, q = e - a * nf;
-    float s = 0.f;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.gp[tp][q][a];
-    sm.G[a * NFP + q] = s + Lp[L.bn2 + q];
-  }
-  __syncthreads();
-}
-
-// ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
-// returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
-template <int H, int NMAX>
-__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX>& sm, const float* __restrict__ Dp, const float* __restrict__ noise,
-                                int a0, int n, int nf) {
-  constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
-  constexpr int ACT = H + 1;            // hidden activations staged in agg (free before layer 0)
-  float* const act = sm.agg;
-  const AmLayout L = argmax_layout(H, nf);
-  const int tid = threadIdx.x;
-  {
-    const int k = tid % H, grp = tid / H;
-    if (grp < NG) {
-      const float b = Dp[L.ba1 + k];
-      for (int a = grp; a < n; a += NG) {
-        float v = b;
-        for (int q = 0; q < nf; ++q) v += Dp[L.wa1t + q * H + k] * sm.h[a * NFP + q];
-        act[a * ACT + k] = silu_f(v);
-      }
-    }
-  }
-  __syncthreads();
-  // net[a][o], o < 2 nf
-  float* net = sm.u.net;
-  for (int e = tid; e < n * 2 * nf; e += BLOCK) {
-    const int a = e / (2 * nf), o = e - a * 2 * nf;
-    float s = Dp[L.ba2 + o];
-    const float* wr = Dp + L.wa2 + o * H;
-    for (int k = 0; k < H; ++k) s += wr[k] * act[a * ACT + k];
-    net[a * 2 * NFMAX + o] = s;
-  }
-  __syncthreads();
-  float lq = 0.f;
-  if (tid < n) {
-    const int a = tid;
-    float u[NFMAX], hv[NFMAX];
-    float T = 0.f;
-#pragma unroll
-    for (int q = 0; q < NFMAX; ++q) {
-      if (q < nf) {
-        const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
-        u[q] = tr + noise[(size_t)(a0 + a) * nf + q] * expf(ls);
-        hv[q] = sm.h[a * NFP + q];
-        T += hv[q] * u[q];
-        lq += -0.5f * u[q] * u[q] - ls;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NFMAX; ++q) {
-      if (q < nf) {
-        const float z = hv[q] * u[q] + (1.f - hv[q]) * (T - softplus_f(T - u[q]));
-        lq -= (1.f - hv[q]) * logsigmoid_f(T - u[q]);
-        sm.h[a * NFP + q] = z;
-      }
-    }
-  }
-  __syncthreads();
-  return lq;
-}
-
-// deterministic block sum (thread values -> one float, fixed order)
-template <int H, int NMAX>
-__device__ __forceinline__ float block_sum(Smem<H, NMAX>& sm, float v) {
-  v = wave_sum(v);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __syncthreads();
-  if (lane == 0) sm.red[w] = v;
-  __syncthreads();
-  float s = 0.f;
-  for (int k = 0; k < WAVES; ++k) s += sm.red[k];
-  return s;
-}
-
-struct FlowArgs {
-  const int32_t* mol_ptr;
-  const float* r_cut;
-  const float* box;
-  float* h;
-  float* g;
-  float* pos;
-  float* vel;
-  const float* layers;
-  int n_layers;
-  int nf;
-  int dequant_kind;
-  const float* dequant;
-  const float* noise;
-  float dequant_scale;
-  float dt;
-  float cw;
-  float* ldj_mol;
-  int32_t* argmax_idx;
-  int32_t* max_idx;
-  int32_t* err;
-  unsigned long long* stats;   // optional: [0] += unique pairs, [1] += reference edges
-};
-
-enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
-
-template <int H, int NMAX>
-__device__ __forceinline__ bool load_molecule(Smem<H, NMAX>& sm, const FlowArgs& A, MolRef& M, int what) {
-  const int m = blockIdx.x;
-  const int tid = threadIdx.x;
-  M.a0 = A.mol_ptr[m];
-  M.n = A.mol_ptr[m + 1] - M.a0;
-  M.rc = 0.f;
-  M.bx = M.by = M.bz = 0.f;
-  if (M.n > NMAX || A.nf > NFMAX) {
-    if (tid == 0) atomicOr(A.err, M.n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
-    return false;
-  }
-  const int n = M.n, nf = A.nf;
-  if (what & LOAD_POS) {
-    M.rc = A.r_cut[m];
-    for (int e = tid; e < n * 3; e += BLOCK) {
-      sm.pos[e] = A.pos[(size_t)M.a0 * 3 + e];
-      sm.boxa[e] = A.box[(size_t)M.a0 * 3 + e];
-    }
-  }
-  if (what & LOAD_VELG)
-    for (int e = tid; e < n * 3; e += BLOCK) sm.vel[e] = A.vel[(size_t)M.a0 * 3 + e];
-  for (int e = tid; e < n * NFP; e += BLOCK) {   // rows zero-padded past nf
-    const int a = e / NFP, q = e - a * NFP;
-    const size_t src = (size_t)(M.a0 + a) * nf + q;
-    if (what & LOAD_H) sm.h[e] = q < nf ? A.h[src] : 0.f;
-    if (what & LOAD_VELG) sm.g[e] = q < nf ? A.g[src] : 0.f;
-  }
-  if (tid == 0) sm.err = 0;
-  __syncthreads();
-  if ((what & LOAD_POS) && n > 0) {
-    M.bx = sm.boxa[0];
-    M.by = sm.boxa[1];
-    M.bz = sm.boxa[2];
-  }
-  return true;
 }
 
 // ---------------------------------------------------------------------------
