@@ -1,0 +1,15 @@
+#!/bin/bash
+# One GPU-box pass: parity tests, bench line, rocprofv3 kernel-trace summary.
+# Usage (via gpurun): bash tools/gpu_check.sh <tag> [pytest-args...]
+set -euo pipefail
+TAG=${1:-rXX}; shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "$@" > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+  python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/bench_under_profiler.json" 2> "$OUT/prof.err"
+echo done
