@@ -29,7 +29,7 @@ SIGNATURES = {
     "enflow_pack_egcl_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_pack_argmax_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_lf_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
-                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p]),
+                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p, _p, _p]),
     "enflow_lf_reverse_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                    _i, _f, _f, _p, _p, _p, _p]),
     "enflow_one_hot_f32": (_i, [_p, _i, _i, _p, _p]),
@@ -39,6 +39,15 @@ SIGNATURES = {
     "enflow_neighbour_pairs_f32": (_i, [_i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p]),
     "enflow_alchemical_nll_f32": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f, _f, _f,
                                        _p, _p, _p]),
+    "enflow_lf_tape_size": (_i64, [_i, _i, _i, _i]),
+    "enflow_egcl_bwd_packed_size": (_i64, [_i, _i]),
+    "enflow_pack_egcl_bwd_f32": (_i, [_p, _i, _i, _p, _p]),
+    "enflow_lf_backward_workspace_size": (_i64, [_i, _i, _i, _i, _i, _i64]),
+    "enflow_alchemical_nll_backward_f32": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p,
+                                                _p, _p, _p, _p, _p, _p]),
+    "enflow_lf_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                    _i, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p,
+                                    _p, _i64, _i64, _p, _p]),
 }
 
 _lib = None

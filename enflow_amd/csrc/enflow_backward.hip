@@ -1,0 +1,961 @@
+// enflow_backward.hip -- training backward of the fused coupling flow on MI355X.
+//
+// Reverse-mode gradient of  loss = Alchemical_NLL(LFIntegrator(data))
+// (enflow/flow/loss.py:21-24, enflow/flow/dynamics.py:10-24, enflow/nn/egcl.py,
+// enflow/nn/argmax.py) with respect to every parameter, i.e. what the
+// reference's `loss.backward()` (enflow/main.py:219-221) produces by autograd.
+//
+// Data flow (one stream, no host synchronisation):
+//   forward (enflow_flow.hip) with a tape: per layer the layer-input state
+//     (h, g, pos, vel), the message sums and Q, plus per-molecule pair counts;
+//   nll_bwd_kernel: adjoints of the flow outputs and of log|detJ|;
+//   pair_offsets_kernel: 32-aligned per-molecule row offsets of every layer;
+//   per layer, last to first:
+//     lf_layer_bwd_kernel (one workgroup per molecule, state in LDS):
+//       leapfrog adjoint -> node MLP backward (VALU, atoms x hidden units)
+//       -> per 32-pair tile the edge chain is recomputed and back-propagated
+//       on v_mfma_f32_32x32x2_f32 (transposed weight fragments, accumulator
+//       tiles chained as B operands exactly as in the forward), writing the
+//       per-pair (input, output-gradient) rows every weight gradient needs;
+//     outer_acc_kernel + reduce_part_kernel: every weight gradient of the
+//       layer as dW = sum_rows DY^T X (chunked over rows, fixed-order reduce,
+//       deterministic), written straight into the torch parameter layout;
+//   argmax_bwd_kernel (+ its two weight gradients).
+// All arithmetic is float32.
+
+#include "flow_device.h"
+
+// ---------------------------------------------------------------------------
+// packing of the backward weight section
+// ---------------------------------------------------------------------------
+__global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
+  const EgclBwdLayout L = egcl_bwd_layout(H);
+  const RawEgcl R = raw_egcl(H, nf);
+  const int NT = H / 32;
+  const int K1 = 2 * nf + 1;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < L.total; idx += gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (idx < L.we1T) {                     // W^T chain fragments: A[row][col] = W[col][row]
+      const bool c1 = idx >= L.wc1T;
+      const int e = idx - (c1 ? L.wc1T : L.we2T);
+      const int u = e & 3, lane = (e >> 2) & 63, rg = (e >> 8) & 3, rest = e >> 10;
+      const int t = rest % NT, tp = rest / NT;
+      const int row = 32 * tp + (lane & 31), col = 32 * t + rho(4 * rg + u, lane >> 5);
+      v = raw[(c1 ? R.Wc1 : R.We2) + col * H + row];
+    } else if (idx < L.wv1T) {              // we1T[tp][rg][lane][4]: A[q][k] = We1[k][q]
+      const int e = idx - L.we1T;
+      const int u = e & 3, lane = (e >> 2) & 63, rg = (e >> 8) & 3, tp = e >> 10;
+      const int q = lane & 31, k = 32 * tp + rho(4 * rg + u, lane >> 5);
+      if (q < K1) v = raw[R.We1 + k * K1 + q];
+    } else if (idx < L.wn1T) {              // wv1T[f][k]
+      const int e = idx - L.wv1T, f = e / H, k = e % H;
+      if (f < nf) v = raw[R.Wv1 + k * nf + f];
+    } else {                                // wn1T[f][k]
+      const int e = idx - L.wn1T, f = e / H, k = e % H;
+      if (f < NFMAX) {
+        if (f < nf) v = raw[R.Wn1 + k * (H + nf) + f];
+      } else if (f - NFMAX < H) {
+        v = raw[R.Wn1 + k * (H + nf) + nf + (f - NFMAX)];
+      }
+    }
+    out[idx] = v;
+  }
+}
+
+__device__ __forceinline__ float sigmoid_f(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+
+// ---------------------------------------------------------------------------
+// per-layer backward
+// ---------------------------------------------------------------------------
+struct BwdArgs {
+  const int32_t* mol_ptr;
+  const float* r_cut;
+  const float* box;
+  const float* tape;
+  int num_atoms, num_mols, n_layers, layer, nf;
+  const float* Lp;   // packed forward layer
+  const float* Bp;   // packed backward section
+  const float* Rp;   // raw (torch-layout) layer parameters
+  float dt, cw;
+  const float* adj_ldj;
+  float* ah;         // [A][nf]  adjoints of h / g / pos / vel: layer output in, layer input out
+  float* ag;
+  float* apos;       // [A][3]
+  float* avel;
+  const int32_t* pair_off;   // this layer's [num_mols + 1] row offsets (32-aligned)
+  float* xin;        // pair rows [P][16]: h_i, h_j, radial        (X of edge_nn.0)
+  float* x1;         // [P][H] silu(edge_nn.0)                       (X of edge_nn.2)
+  float* e;          // [P][H] edge message                         (X of coord_nn.0)
+  float* sc;         // [P][H] silu(coord_nn.0)                      (X of coord_nn.2)
+  float* dp0;        // [P][H] d pre(edge_nn.0)                      (DY of edge_nn.0)
+  float* dpe;        // [P][H] d pre(edge_nn.2)                      (DY of edge_nn.2)
+  float* ac;         // [P][H] d pre(coord_nn.0)                     (DY of coord_nn.0)
+  float* aphi;       // [P]    d phi                                 (DY of coord_nn.2)
+  float* su;         // atom rows [A][H] silu(vel_scaling_nn.0)      (X of vel_scaling_nn.2)
+  float* au;         // [A][H] d pre(vel_scaling_nn.0)               (DY of vel_scaling_nn.0)
+  float* sn;         // [A][H] silu(node_nn.0)                       (X of node_nn.2)
+  float* an;         // [A][H] d pre(node_nn.0)                      (DY of node_nn.0)
+  float* aq;         // [A]    dQ                                    (DY of vel_scaling_nn.2)
+  float* agr;        // [A][nf] dG                                   (DY of node_nn.2)
+  int32_t* err;
+};
+
+template <int H, int NMAX>
+struct BwdSmem {
+  Smem<H, NMAX> f;
+  float ah[NMAX * NFP], ag[NMAX * NFP], aG[NMAX * NFP];
+  float apos[NMAX * 3], avel[NMAX * 3], aF[NMAX * 3];
+  float aQ[NMAX];
+  float au[NMAX * (H + 1)], an[NMAX * (H + 1)];
+};
+
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
+template <int H, int NMAX>
+__global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
+  __shared__ BwdSmem<H, NMAX> sb;
+  Smem<H, NMAX>& sm = sb.f;
+  constexpr int NT = H / 32;
+  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int HS = H + 1;
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int a0 = B.mol_ptr[m], n = B.mol_ptr[m + 1] - a0;
+  if (n > NMAX || B.nf > NFMAX) {
+    if (tid == 0) atomicOr(B.err, n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
+    return;
+  }
+  const int nf = B.nf;
+  const float dt = B.dt;
+  const EgclLayout L = egcl_layout(H, nf);
+  const EgclBwdLayout LB = egcl_bwd_layout(H);
+  const RawEgcl R = raw_egcl(H, nf);
+  const TapeLayout T = tape_layout(B.num_atoms, nf, H, B.n_layers);
+  const size_t la = (size_t)B.layer * B.num_atoms + a0;
+  const float* Rp = B.Rp;
+  const float* Bp = B.Bp;
+
+  // ---- layer-input state (tape), message sums, Q; adjoints of the layer output
+  for (int e = tid; e < n * 3; e += BLOCK) {
+    sm.pos[e] = B.tape[T.pos + la * 3 + e];
+    sm.vel[e] = B.tape[T.vel + la * 3 + e];
+    sm.boxa[e] = B.box[(size_t)a0 * 3 + e];
+    sb.apos[e] = B.apos[(size_t)a0 * 3 + e];
+    sb.avel[e] = B.avel[(size_t)a0 * 3 + e];
+  }
+  for (int e = tid; e < n * NFP; e += BLOCK) {
+    const int a = e / NFP, q = e - a * NFP;
+    const bool v = q < nf;
+    sm.h[e] = v ? B.tape[T.hx + (la + a) * T.ldhx + q] : 0.f;
+    sm.g[e] = v ? B.tape[T.g + (la + a) * nf + q] : 0.f;
+    sb.ah[e] = v ? B.ah[(size_t)(a0 + a) * nf + q] : 0.f;
+    sb.ag[e] = v ? B.ag[(size_t)(a0 + a) * nf + q] : 0.f;
+  }
+  for (int e = tid; e < n * H; e += BLOCK) {
+    const int a = e / H, k = e - a * H;
+    sm.agg[a * AST + k] = B.tape[T.hx + (la + a) * T.ldhx + nf + k];
+  }
+  for (int a = tid; a < n; a += BLOCK) sm.Q[a] = B.tape[T.q + la + a];
+  for (int k = tid; k < H; k += BLOCK) {
+    sm.bias[k] = B.Lp[L.be1 + k];
+    sm.bias[H + k] = B.Lp[L.be2 + k];
+    sm.bias[2 * H + k] = B.Lp[L.bc1 + k];
+    sm.bias[3 * H + k] = B.Lp[L.wc2 + k];
+  }
+  if (tid == 0) sm.err = 0;
+  __syncthreads();
+  MolRef M;
+  M.a0 = a0;
+  M.n = n;
+  M.rc = B.r_cut[m];
+  M.bx = n > 0 ? sm.boxa[0] : 0.f;
+  M.by = n > 0 ? sm.boxa[1] : 0.f;
+  M.bz = n > 0 ? sm.boxa[2] : 0.f;
+  build_pairs(sm, M, tid);   // same positions as the forward -> same pairs
+
+  // ---- leapfrog adjoint (dynamics.py:13-21 in reverse order)
+  const float aldj = B.adj_ldj[0];
+  for (int a = tid; a < n; a += BLOCK) {
+    const float eq = expf(sm.Q[a]);
+    float s = 0.f;
+    for (int d = 0; d < 3; ++d) {
+      const float avt = sb.avel[a * 3 + d] + sb.apos[a * 3 + d] * dt;   // pos' = pbc(pos + vel' dt)
+      s += sm.vel[a * 3 + d] * avt;
+      sb.avel[a * 3 + d] = eq * avt;                                   // vel' = e^Q vel + F dt
+      sb.aF[a * 3 + d] = avt * dt;
+    }
+    sb.aQ[a] = eq * s + aldj;                                          // + ldj += Q.sum()
+    for (int q = 0; q < nf; ++q) {
+      const float agt = sb.ag[a * NFP + q] + sb.ah[a * NFP + q] * dt;  // h' = h + g' dt
+      sb.ag[a * NFP + q] = agt;                                        // g' = g + G dt
+      sb.aG[a * NFP + q] = agt * dt;
+    }
+  }
+  __syncthreads();
+
+  // ---- node MLPs backward (egcl.py:26-30, 51-54, 90-92): threads = (hidden unit k, atom group)
+  {
+    constexpr int NG = BLOCK / H;
+    const int k = tid % H, grp = tid / H;
+    const float bv1 = Rp[R.bv1 + k], bn1 = Rp[R.bn1 + k], wv2 = Rp[R.Wv2 + k];
+    for (int a = grp; a < n; a += NG) {
+      float u = bv1, nn = bn1;
+      for (int f = 0; f < nf; ++f) {
+        const float hv = sm.h[a * NFP + f];
+        u = fmaf(Bp[LB.wv1T + f * H + k], hv, u);
+        nn = fmaf(Bp[LB.wn1T + f * H + k], hv, nn);
+      }
+      const float* arow = &sm.agg[a * AST];
+      const float* wcol = Bp + LB.wn1T + NFMAX * H + k;
+#pragma unroll 8
+      for (int f = 0; f < H; ++f) nn = fmaf(wcol[f * H], arow[f], nn);
+      const float s_u = sigmoid_f(u), s_n = sigmoid_f(nn);
+      const float du = s_u * (1.f + u * (1.f - s_u)), dn = s_n * (1.f + nn * (1.f - s_n));
+      const float au = sb.aQ[a] * wv2 * du;
+      float asn = 0.f;
+      for (int q = 0; q < nf; ++q) asn = fmaf(Rp[R.Wn2 + q * H + k], sb.aG[a * NFP + q], asn);
+      const float an = asn * dn;
+      const size_t row = (size_t)(a0 + a) * H + k;
+      B.su[row] = u * s_u;
+      B.au[row] = au;
+      B.sn[row] = nn * s_n;
+      B.an[row] = an;
+      sb.au[a * HS + k] = au;
+      sb.an[a * HS + k] = an;
+    }
+    for (int a = tid; a < n; a += BLOCK) B.aq[a0 + a] = sb.aQ[a];
+    for (int e = tid; e < n * nf; e += BLOCK) {
+      const int a = e / nf, q = e - a * nf;
+      B.agr[(size_t)a0 * nf + e] = sb.aG[a * NFP + q];
+    }
+    __syncthreads();
+    // d agg = node_nn.0.weight[:, nf:]^T d pre  (overwrites the message sums in LDS)
+    for (int a = grp; a < n; a += NG) {
+      float s = 0.f;
+      const float* wr = Rp + R.Wn1 + nf + k;
+#pragma unroll 8
+      for (int kk = 0; kk < H; ++kk) s = fmaf(wr[kk * (H + nf)], sb.an[a * HS + kk], s);
+      sm.agg[a * AST + k] = s;
+    }
+    // d h += vel_scaling_nn.0.weight^T d u + node_nn.0.weight[:, :nf]^T d pre
+    for (int e = tid; e < n * nf; e += BLOCK) {
+      const int a = e / nf, f = e - a * nf;
+      float s = 0.f;
+      for (int kk = 0; kk < H; ++kk)
+        s += Rp[R.Wv1 + kk * nf + f] * sb.au[a * HS + kk] + Rp[R.Wn1 + kk * (H + nf) + f] * sb.an[a * HS + kk];
+      sb.ah[a * NFP + f] += s;
+    }
+    __syncthreads();
+  }
+
+  // ---- edge chain backward, one 32-pair tile per wave step (egcl.py:57-74, 76-89)
+  {
+    const int lane = tid & 63, w = tid >> 6;
+    const int j = lane & 31, hh = lane >> 5;
+    const int P = sm.npairs;
+    const int TT = (P + 31) >> 5;
+    const int tpw = (TT + WAVES - 1) / WAVES;
+    const int t0 = w * tpw, t1 = min(TT, t0 + tpw);
+    const rsrc_t W = weights_rsrc(B.Lp, L.total);
+    const rsrc_t WB = weights_rsrc(B.Bp, LB.total);
+    const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
+    const size_t prow0 = (size_t)B.pair_off[m];
+    for (int tile = t0; tile < t1; ++tile) {
+      const int p = tile * 32 + j;
+      const bool valid = p < P;
+      const uint32_t pr = valid ? sm.pairs[p] : 0u;
+      const int i = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
+      const float c = (float)(pr >> 16);       // multiplicity; 0 on padding lanes
+      const size_t Rw = prow0 + (size_t)p;
+      const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
+      const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
+      const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], hbz);
+      const float radial = dx * dx + dy * dy + dz * dz;
+
+      // X row of edge_nn.0: [h_i, h_j, radial]
+      {
+        f32x4 v0, v1;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int q = 8 * hh + u;
+          float v = 0.f;
+          if (q < nf) v = sm.h[i * NFP + q];
+          else if (q < 2 * nf) v = sm.h[jl * NFP + q - nf];
+          else if (q == 2 * nf) v = radial;
+          v = valid ? v : 0.f;
+          if (u < 4) v0[u] = v; else v1[u - 4] = v;
+        }
+        st4(B.xin + Rw * 16 + 8 * hh, v0);
+        st4(B.xin + Rw * 16 + 8 * hh + 4, v1);
+      }
+
+      // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1
+      f32x16 x0[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
+#pragma unroll
+      for (int s = 0; s < NFMAX + 1; ++s) {
+        const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh]
+                      : (s < NFMAX ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : (hh == 0 ? radial : 0.f));
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+          x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
+      }
+      // x1 = silu(pre0) (kept: B operand of GEMM1), silu'(pre0) parked in the dp0 row
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(sm.bias + f0);
+          f32x4 xv, dv;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float z = x0[t][4 * g4 + u] + b[u];
+            const float s = sigmoid_f(z);
+            xv[u] = z * s;
+            dv[u] = s * (1.f + z * (1.f - s));
+            x0[t][4 * g4 + u] = xv[u];
+          }
+          st4(B.x1 + Rw * H + f0, xv);
+          st4(B.dp0 + Rw * H + f0, dv);
+        }
+      // GEMM1 (recompute): e = silu(edge_nn.2 x1 + be2); silu' parked in the dpe row
+      f32x16 ev[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ev[t] = (f32x16)0.f;
+      chain_gemm<NT>(W, L.we2f, x0, ev, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(sm.bias + H + f0);
+          f32x4 xv, dv;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float z = ev[t][4 * g4 + u] + b[u];
+            const float s = sigmoid_f(z);
+            xv[u] = z * s;
+            dv[u] = s * (1.f + z * (1.f - s));
+            ev[t][4 * g4 + u] = xv[u];
+          }
+          st4(B.e + Rw * H + f0, xv);
+          st4(B.dpe + Rw * H + f0, dv);
+        }
+      // GEMM2 (recompute): phi = coord_nn.2 silu(coord_nn.0 e + bc1)
+      f32x16 cv[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) cv[t] = (f32x16)0.f;
+      chain_gemm<NT>(W, L.wc1f, ev, cv, lane);
+      float part = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(sm.bias + 2 * H + f0);
+          const f32x4 w2 = ld4(sm.bias + 3 * H + f0);
+          f32x4 sv;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float z = cv[t][4 * g4 + u] + b[u];
+            const float s = sigmoid_f(z);
+            sv[u] = z * s;
+            part = fmaf(w2[u], sv[u], part);
+            cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
+          }
+          st4(B.sc + Rw * H + f0, sv);
+        }
+      const float phi = part + __shfl_xor(part, 32, 64);
+      // d phi from dF (egcl.py:71-74: mean over the row's edges, clamp, coords_weight)
+      const float inv = B.cw / fmaxf((float)sm.cntrow[i], 1.f);
+      const float gx = fabsf(dx * phi) <= 100.f ? sb.aF[i * 3 + 0] * inv : 0.f;
+      const float gy = fabsf(dy * phi) <= 100.f ? sb.aF[i * 3 + 1] * inv : 0.f;
+      const float gz = fabsf(dz * phi) <= 100.f ? sb.aF[i * 3 + 2] * inv : 0.f;
+      const float aph = c * (gx * dx + gy * dy + gz * dz);
+      if (hh == 0) B.aphi[Rw] = aph;
+      // d pre(coord_nn.0) = dphi * wc2 * silu'(c)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          f32x4 av;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            av[u] = aph * cv[t][4 * g4 + u];
+            cv[t][4 * g4 + u] = av[u];
+          }
+          st4(B.ac + Rw * H + f0, av);
+        }
+      // GEMM3: d e = c * d agg[i] + coord_nn.0.weight^T d pre(coord_nn.0)
+      f32x16 ae[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) ae[t][r] = c * sm.agg[i * AST + 32 * t + rho(r, hh)];
+      chain_gemm<NT>(WB, LB.wc1T, cv, ae, lane);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parked silu' rows written by this lane
+      // d pre(edge_nn.2) = d e * silu'(pre_e)
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 dv = ld4(B.dpe + Rw * H + f0);
+          f32x4 av;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            av[u] = ae[t][4 * g4 + u] * dv[u];
+            ae[t][4 * g4 + u] = av[u];
+          }
+          st4(B.dpe + Rw * H + f0, av);
+        }
+      // GEMM4: d x1 = edge_nn.2.weight^T d pre(edge_nn.2);  d pre0 = d x1 * silu'(pre0)
+      f32x16 ax[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) ax[t] = (f32x16)0.f;
+      chain_gemm<NT>(WB, LB.we2T, ae, ax, lane);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 dv = ld4(B.dp0 + Rw * H + f0);
+          f32x4 av;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            av[u] = ax[t][4 * g4 + u] * dv[u];
+            ax[t][4 * g4 + u] = av[u];
+          }
+          st4(B.dp0 + Rw * H + f0, av);
+        }
+      // GEMM5: d [h_i, h_j, radial] = edge_nn.0.weight^T d pre0   (rows q < 2nf+1)
+      f32x16 ain = (f32x16)0.f;
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const f32x4 a4 = bload4(WB, lane * 16, (LB.we1T + (tp * 4 + rg) * 256) * 4);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) ain = mfma32(a4[u], ax[tp][4 * rg + u], ain);
+        }
+      float arad = 0.f;
+      if (valid) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = rho(r, hh);
+          if (q < nf) atomicAdd(&sb.ah[i * NFP + q], ain[r]);
+          else if (q < 2 * nf) atomicAdd(&sb.ah[jl * NFP + q - nf], ain[r]);
+          else if (q == 2 * nf) arad = ain[r];
+        }
+      }
+      // d coord_diff (radial = |cd|^2, trans = cd * phi), d pos_i += ., d pos_j -= .
+      const float sF = hh == 0 ? c * phi : 0.f;
+      const float tx = sF * gx + 2.f * dx * arad;
+      const float ty = sF * gy + 2.f * dy * arad;
+      const float tz = sF * gz + 2.f * dz * arad;
+      if (valid && (tx != 0.f || ty != 0.f || tz != 0.f)) {
+        atomicAdd(&sb.apos[i * 3 + 0], tx);
+        atomicAdd(&sb.apos[i * 3 + 1], ty);
+        atomicAdd(&sb.apos[i * 3 + 2], tz);
+        atomicAdd(&sb.apos[jl * 3 + 0], -tx);
+        atomicAdd(&sb.apos[jl * 3 + 1], -ty);
+        atomicAdd(&sb.apos[jl * 3 + 2], -tz);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- adjoints of the layer input
+  for (int e = tid; e < n * 3; e += BLOCK) {
+    B.apos[(size_t)a0 * 3 + e] = sb.apos[e];
+    B.avel[(size_t)a0 * 3 + e] = sb.avel[e];
+  }
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    B.ah[(size_t)a0 * nf + e] = sb.ah[a * NFP + q];
+    B.ag[(size_t)a0 * nf + e] = sb.ag[a * NFP + q];
+  }
+  if (tid == 0 && sm.err) atomicOr(B.err, sm.err);
+}
+
+// ---------------------------------------------------------------------------
+// per-layer 32-aligned pair row offsets (exclusive scan, one block per layer)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) pair_offsets_kernel(const int32_t* counts, int num_mols, int32_t* offs) {
+  __shared__ int wsum[WAVES];
+  __shared__ int carry;
+  const int l = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int32_t* cnt = counts + (size_t)l * num_mols;
+  int32_t* out = offs + (size_t)l * (num_mols + 1);
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < num_mols; base += BLOCK) {
+    const int mm = base + tid;
+    const int v = mm < num_mols ? ((cnt[mm] + 31) & ~31) : 0;
+    const int incl = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int pre = carry;
+    for (int k = 0; k < w; ++k) pre += wsum[k];
+    if (mm < num_mols) out[mm] = pre + incl - v;
+    __syncthreads();
+    if (tid == BLOCK - 1) carry = pre + incl;
+    __syncthreads();
+  }
+  if (tid == 0) out[num_mols] = carry;
+}
+
+// ---------------------------------------------------------------------------
+// weight gradients: C[m][n] = sum_rows DY[row][m] X[row][n] (+ bias column
+// sum_rows DY[row][m]); rows chunked, one partial per chunk, fixed-order reduce
+// ---------------------------------------------------------------------------
+struct OuterDesc {
+  const float* DY;
+  const float* X;
+  const int32_t* rows_dev;   // device row count (NULL: rows_static)
+  float* part;
+  float* outW;               // [M][N] row-major (torch Linear weight layout)
+  float* outB;               // [M] (bias) or NULL
+  int ldd, M, ldx, N, rows_static, mb, nb, nch;
+};
+#define OUTER_MAX 8
+struct OuterBatch {
+  OuterDesc d[OUTER_MAX];
+  int nd;
+  int start[OUTER_MAX + 1];   // first workgroup of each descriptor
+};
+#define OA_ROWS 32
+#define OA_CHUNK 2048
+
+__device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
+  int k = 0;
+  while (k + 1 < ob.nd && bid >= ob.start[k + 1]) ++k;
+  return k;
+}
+
+__global__ void __launch_bounds__(256) outer_acc_kernel(OuterBatch ob) {
+  const int bid = blockIdx.x;
+  const int k = find_desc(ob, bid);
+  const OuterDesc& D = ob.d[k];
+  const int local = bid - ob.start[k];
+  const int per = D.mb * D.nb;
+  const int chunk = local / per, rem = local - chunk * per;
+  const int mbi = rem / D.nb, nbi = rem - mbi * D.nb;
+  const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
+  const int r0 = chunk * OA_CHUNK;
+  if (r0 >= rows) return;
+  const int r1 = min(rows, r0 + OA_CHUNK);
+  const int NB = D.N + (D.outB ? 1 : 0);
+  const int m0 = mbi * 64, n0 = nbi * 64;
+  __shared__ float sd[OA_ROWS][64];
+  __shared__ float sx[OA_ROWS][64];
+  const int tid = threadIdx.x, tm = tid >> 4, tn = tid & 15;
+  float acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
+  for (int rb = r0; rb < r1; rb += OA_ROWS) {
+    for (int e = tid; e < OA_ROWS * 64; e += 256) {
+      const int r = e >> 6, cc = e & 63, p = rb + r;
+      const bool pv = p < r1;
+      const int mm = m0 + cc, nn = n0 + cc;
+      sd[r][cc] = (pv && mm < D.M) ? D.DY[(size_t)p * D.ldd + mm] : 0.f;
+      sx[r][cc] = (pv && nn < D.N) ? D.X[(size_t)p * D.ldx + nn] : ((pv && nn == D.N && D.outB) ? 1.f : 0.f);
+    }
+    __syncthreads();
+#pragma unroll 8
+    for (int r = 0; r < OA_ROWS; ++r) {
+      const f32x4 a = ld4(&sd[r][tm * 4]);
+      const f32x4 b = ld4(&sx[r][tn * 4]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[u][v] = fmaf(a[u], b[v], acc[u][v]);
+    }
+    __syncthreads();
+  }
+  float* out = D.part + (size_t)chunk * D.M * NB;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int mm = m0 + tm * 4 + u, nn = n0 + tn * 4 + v;
+      if (mm < D.M && nn < NB) out[(size_t)mm * NB + nn] = acc[u][v];
+    }
+}
+
+__global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
+  const int bid = blockIdx.x;
+  const int k = find_desc(ob, bid);
+  const OuterDesc& D = ob.d[k];
+  const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
+  const int nch = (rows + OA_CHUNK - 1) / OA_CHUNK;
+  const int NB = D.N + (D.outB ? 1 : 0);
+  const int idx = (bid - ob.start[k]) * 256 + threadIdx.x;
+  if (idx >= D.M * NB) return;
+  double s = 0.0;
+  for (int ch = 0; ch < nch; ++ch) s += (double)D.part[(size_t)ch * D.M * NB + idx];
+  const int mm = idx / NB, nn = idx - mm * NB;
+  if (nn < D.N) D.outW[(size_t)mm * D.N + nn] = (float)s;
+  else D.outB[mm] = (float)s;
+}
+
+// ---------------------------------------------------------------------------
+// ArgMax.forward backward (enflow/nn/argmax.py:13-25): adjoint of z (= d h at
+// the first layer's input) and of log_q (= d ldj) -> parameter-gradient rows
+// ---------------------------------------------------------------------------
+template <int H, int NMAX>
+__global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_ptr, int nf, const float* hdata,
+                                                          const float* noise, const float* Draw, const float* az,
+                                                          const float* adj_ldj, float* apre_rows, float* spre_rows,
+                                                          float* anet_rows) {
+  __shared__ float pre[NMAX][H + 1];
+  __shared__ float net[NMAX][2 * NFMAX];
+  __shared__ float anet[NMAX][2 * NFMAX];
+  __shared__ float hs[NMAX][NFMAX];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
+  if (n > NMAX) return;
+  const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
+  for (int e = tid; e < n * nf; e += BLOCK) hs[e / nf][e % nf] = hdata[(size_t)a0 * nf + e];
+  __syncthreads();
+  constexpr int NG = BLOCK / H;
+  const int k = tid % H, grp = tid / H;
+  for (int a = grp; a < n; a += NG) {
+    float v = Draw[rb1 + k];
+    for (int f = 0; f < nf; ++f) v = fmaf(Draw[rW1 + k * nf + f], hs[a][f], v);
+    pre[a][k] = v;
+    spre_rows[(size_t)(a0 + a) * H + k] = v * sigmoid_f(v);
+  }
+  __syncthreads();
+  for (int e = tid; e < n * 2 * nf; e += BLOCK) {
+    const int a = e / (2 * nf), o = e - a * 2 * nf;
+    float s = Draw[rb2 + o];
+    for (int kk = 0; kk < H; ++kk) {
+      const float p = pre[a][kk];
+      s = fmaf(Draw[rW2 + o * H + kk], p * sigmoid_f(p), s);
+    }
+    net[a][o] = s;
+  }
+  __syncthreads();
+  const float aldj = adj_ldj[0];
+  if (tid < n) {
+    const int a = tid;
+    float u[NFMAX], hv[NFMAX], sg[NFMAX], zz[NFMAX], els[NFMAX];
+    float T = 0.f;
+#pragma unroll
+    for (int q = 0; q < NFMAX; ++q) {
+      if (q < nf) {
+        els[q] = expf(net[a][q]);
+        u[q] = net[a][nf + q] + noise[(size_t)(a0 + a) * nf + q] * els[q];
+        hv[q] = hs[a][q];
+        zz[q] = az[(size_t)(a0 + a) * nf + q];
+        T += hv[q] * u[q];
+      }
+    }
+    float S = 0.f, Az = 0.f;
+#pragma unroll
+    for (int q = 0; q < NFMAX; ++q) {
+      if (q < nf) {
+        sg[q] = sigmoid_f(T - u[q]);
+        const float w = (1.f - hv[q]) * (1.f - sg[q]);
+        S += w;
+        Az += zz[q] * w;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NFMAX; ++q) {
+      if (q < nf) {
+        const float au = zz[q] * hv[q] + (1.f - hv[q]) * zz[q] * sg[q] + hv[q] * Az +
+                         aldj * (-u[q] - hv[q] * S + (1.f - hv[q]) * (1.f - sg[q]));
+        const float als = au * noise[(size_t)(a0 + a) * nf + q] * els[q] - aldj;
+        anet[a][q] = als;
+        anet[a][nf + q] = au;
+        anet_rows[(size_t)(a0 + a) * 2 * nf + q] = als;
+        anet_rows[(size_t)(a0 + a) * 2 * nf + nf + q] = au;
+      }
+    }
+  }
+  __syncthreads();
+  for (int a = grp; a < n; a += NG) {
+    float s = 0.f;
+    for (int o = 0; o < 2 * nf; ++o) s = fmaf(Draw[rW2 + o * H + k], anet[a][o], s);
+    const float p = pre[a][k], sp = sigmoid_f(p);
+    apre_rows[(size_t)(a0 + a) * H + k] = s * sp * (1.f + p * (1.f - sp));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Alchemical_NLL backward (enflow/flow/loss.py:11-24)
+// ---------------------------------------------------------------------------
+template <int NMAX>
+__global__ void __launch_bounds__(BLOCK) nll_bwd_kernel(const int32_t* mol_ptr, int num_mols, int nf, const float* h,
+                                                      const float* g, const float* pos, const float* vel, float kBT,
+                                                      float softening, const float* grad_loss, float* ah, float* ag,
+                                                      float* apos, float* avel, float* adj_ldj) {
+  __shared__ float spos[NMAX * 3];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
+  const float s = grad_loss ? grad_loss[0] : 1.f;
+  const float invM = s / (float)num_mols;
+  const float cH = invM / kBT;
+  for (int e = tid; e < n * 3; e += BLOCK) {
+    spos[e] = pos[(size_t)a0 * 3 + e];
+    avel[(size_t)a0 * 3 + e] = cH * vel[(size_t)a0 * 3 + e];    // H = LJ + 0.5 vel^2
+  }
+  for (int e = tid; e < n * nf; e += BLOCK) {                    // -log_gaussian(h), (g)
+    ah[(size_t)a0 * nf + e] = invM * h[(size_t)a0 * nf + e];
+    ag[(size_t)a0 * nf + e] = invM * g[(size_t)a0 * nf + e];
+  }
+  __syncthreads();
+  for (int e = tid; e < n * 3; e += BLOCK) {
+    const int a = e / 3, d = e - a * 3;
+    float f = 0.f;
+    for (int b = 0; b < n; ++b) {
+      if (b == a) continue;
+      const float dx = spos[a * 3] - spos[b * 3], dy = spos[a * 3 + 1] - spos[b * 3 + 1],
+                  dz = spos[a * 3 + 2] - spos[b * 3 + 2];
+      const float d2 = dx * dx + dy * dy + dz * dz;
+      if (d2 == 0.f) continue;                                   // dist_sq != 0 (loss.py:15)
+      const float r = d2 + softening, ir = 1.f / r, ir2 = ir * ir, ir4 = ir2 * ir2;
+      const float dEdR = 4.f * (-6.f * ir4 * ir2 * ir + 3.f * ir4);
+      f += dEdR * 2.f * (spos[a * 3 + d] - spos[b * 3 + d]);
+    }
+    apos[(size_t)a0 * 3 + e] = cH * f;
+  }
+  if (m == 0 && tid == 0) adj_ldj[0] = -invM;                    // log_px += ldj
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+static inline hipStream_t SB(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int hid_ok_b(int H) { return H == 32 || H == 64 || H == 128; }
+static inline size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+struct BwdWs {
+  size_t offs, xin, x1, e, sc, dp0, dpe, ac, aphi, su, au, sn, an, aq, agr, anet, part, total;  // floats
+  size_t part_floats;
+};
+
+static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, long long prb) {
+  BwdWs W;
+  size_t o = 0;
+  const size_t P = (size_t)prb, A = (size_t)num_atoms;
+  W.offs = o; o += al64((size_t)n_layers * (num_mols + 1));
+  W.xin = o; o += al64(P * 16);
+  W.x1 = o; o += al64(P * H);
+  W.e = o; o += al64(P * H);
+  W.sc = o; o += al64(P * H);
+  W.dp0 = o; o += al64(P * H);
+  W.dpe = o; o += al64(P * H);
+  W.ac = o; o += al64(P * H);
+  W.aphi = o; o += al64(P);
+  W.su = o; o += al64(A * H);
+  W.au = o; o += al64(A * H);
+  W.sn = o; o += al64(A * H);
+  W.an = o; o += al64(A * H);
+  W.aq = o; o += al64(A);
+  W.agr = o; o += al64(A * nf);
+  W.anet = o; o += al64(A * 2 * nf);
+  const size_t chp = (size_t)cdiv(prb, OA_CHUNK), cha = (size_t)cdiv(num_atoms, OA_CHUNK);
+  // partials of one layer's 8 gradients (all in flight together)
+  W.part_floats = chp * ((size_t)H * (2 * nf + 2) + 2 * (size_t)H * (H + 1) + H) +
+                  cha * ((size_t)H * (nf + 1) + (H + 1) + (size_t)H * (H + nf + 1) + (size_t)nf * (H + 1));
+  const size_t am = cha * ((size_t)H * (nf + 1) + (size_t)2 * nf * (H + 1));
+  if (am > W.part_floats) W.part_floats = am;
+  W.part = o; o += al64(W.part_floats);
+  W.total = o;
+  return W;
+}
+
+static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, const float* X, int ldx, int N,
+                     const int32_t* rows_dev, int rows_static, int rows_bound, float*& part, float* outW,
+                     float* outB) {
+  OuterDesc& D = ob.d[ob.nd];
+  D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
+  D.rows_dev = rows_dev; D.rows_static = rows_static;
+  D.outW = outW; D.outB = outB;
+  const int NB = N + (outB ? 1 : 0);
+  D.mb = cdiv(M, 64);
+  D.nb = cdiv(NB, 64);
+  D.nch = rows_bound > 0 ? cdiv(rows_bound, OA_CHUNK) : 0;
+  D.part = part;
+  part += (size_t)D.nch * M * NB;
+  ob.start[ob.nd] = wg;
+  wg += D.nch * D.mb * D.nb;
+  ++ob.nd;
+  ob.start[ob.nd] = wg;
+}
+
+static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
+  if (wg > 0) hipLaunchKernelGGL(outer_acc_kernel, dim3(wg), dim3(256), 0, st, ob);
+  // reducer: one workgroup per 256 outputs of each descriptor
+  OuterBatch rb = ob;
+  int rw = 0;
+  for (int k = 0; k < ob.nd; ++k) {
+    rb.start[k] = rw;
+    const int NB = ob.d[k].N + (ob.d[k].outB ? 1 : 0);
+    rw += cdiv((long long)ob.d[k].M * NB, 256);
+  }
+  rb.start[ob.nd] = rw;
+  if (rw > 0) hipLaunchKernelGGL(reduce_part_kernel, dim3(rw), dim3(256), 0, st, rb);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+#define DISPATCH_HN_B(H, NMAXSEL, CALL)                      \
+  do {                                                        \
+    if (NMAXSEL <= 32) {                                      \
+      if (H == 32) { CALL(32, 32); }                          \
+      else if (H == 64) { CALL(64, 32); }                     \
+      else { CALL(128, 32); }                                 \
+    } else {                                                  \
+      if (H == 32) { CALL(32, 64); }                          \
+      else if (H == 64) { CALL(64, 64); }                     \
+      else { CALL(128, 64); }                                 \
+    }                                                         \
+  } while (0)
+
+extern "C" {
+
+int64_t enflow_lf_tape_size(int num_atoms, int nf, int H, int n_layers) {
+  if (num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || n_layers < 0) return -1;
+  return (int64_t)tape_layout(num_atoms, nf, H, n_layers).total;
+}
+
+int64_t enflow_egcl_bwd_packed_size(int H, int nf) {
+  if (!hid_ok_b(H) || nf < 1 || nf > NFMAX) return -1;
+  return egcl_bwd_layout(H).total;
+}
+
+int enflow_pack_egcl_bwd_f32(const float* raw, int H, int nf, float* packed, void* stream) {
+  if (!hid_ok_b(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
+  const int total = egcl_bwd_layout(H).total;
+  hipLaunchKernelGGL(pack_egcl_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, SB(stream), raw, H, nf, packed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int64_t enflow_lf_backward_workspace_size(int num_mols, int num_atoms, int nf, int H, int n_layers,
+                                          int64_t pair_row_bound) {
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0)
+    return -1;
+  return (int64_t)(bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound).total * sizeof(float));
+}
+
+int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf,
+                                       const int32_t* mol_ptr, const float* h, const float* g,
+                                       const float* pos, const float* vel, float kBT, float softening,
+                                       const float* grad_loss, float* adj_h, float* adj_g, float* adj_pos,
+                                       float* adj_vel, float* adj_ldj, void* stream) {
+  (void)num_atoms;
+  if (num_mols < 1 || max_mol_atoms > 64 || nf < 1 || !adj_ldj) return -1;
+  if (max_mol_atoms <= 32)
+    hipLaunchKernelGGL((nll_bwd_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, SB(stream), mol_ptr, num_mols, nf, h, g,
+                       pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos, adj_vel, adj_ldj);
+  else
+    hipLaunchKernelGGL((nll_bwd_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, SB(stream), mol_ptr, num_mols, nf, h, g,
+                       pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos, adj_vel, adj_ldj);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                           const int32_t* mol_ptr, const float* r_cut, const float* box,
+                           const float* tape, const int32_t* pair_counts,
+                           const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                           int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                           float dt, float cw,
+                           float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                           float* grad_layers, float* grad_dequant,
+                           void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                           int32_t* err_flag, void* stream) {
+  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > NFMAX ||
+      !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0 || pair_row_bound > 0x7fffffffLL)
+    return -1;
+  if (!tape || !pair_counts || !layers || !layers_bwd || !layers_raw || !adj_h || !adj_g || !adj_pos ||
+      !adj_vel || !adj_ldj || !grad_layers || !workspace || !err_flag)
+    return -1;
+  if (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!dequant_raw || !h_data || !noise || !grad_dequant)) return -1;
+  const BwdWs Wl = bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound);
+  if ((uint64_t)workspace_bytes < Wl.total * sizeof(float)) return -6;
+  if (num_mols == 0) return 0;
+  hipStream_t st = SB(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  int32_t* offs = reinterpret_cast<int32_t*>(ws + Wl.offs);
+  const EgclLayout L = egcl_layout(H, nf);
+  const EgclBwdLayout LB = egcl_bwd_layout(H);
+  const RawEgcl R = raw_egcl(H, nf);
+  const int prb = (int)pair_row_bound;
+
+  if (n_layers > 0)
+    hipLaunchKernelGGL(pair_offsets_kernel, dim3(n_layers), dim3(BLOCK), 0, st, pair_counts, num_mols, offs);
+
+  for (int l = n_layers - 1; l >= 0; --l) {
+    BwdArgs A;
+    A.mol_ptr = mol_ptr; A.r_cut = r_cut; A.box = box; A.tape = tape;
+    A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
+    A.Lp = layers + (size_t)l * L.total;
+    A.Bp = layers_bwd + (size_t)l * LB.total;
+    A.Rp = layers_raw + (size_t)l * R.total;
+    A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
+    A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
+    A.pair_off = offs + (size_t)l * (num_mols + 1);
+    A.xin = ws + Wl.xin; A.x1 = ws + Wl.x1; A.e = ws + Wl.e; A.sc = ws + Wl.sc;
+    A.dp0 = ws + Wl.dp0; A.dpe = ws + Wl.dpe; A.ac = ws + Wl.ac; A.aphi = ws + Wl.aphi;
+    A.su = ws + Wl.su; A.au = ws + Wl.au; A.sn = ws + Wl.sn; A.an = ws + Wl.an;
+    A.aq = ws + Wl.aq; A.agr = ws + Wl.agr; A.err = err_flag;
+#define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, A)
+    DISPATCH_HN_B(H, max_mol_atoms, CALL);
+#undef CALL
+    // the layer's weight gradients, straight into the torch parameter layout
+    float* G = grad_layers + (size_t)l * R.total;
+    const int32_t* prow = offs + (size_t)l * (num_mols + 1) + num_mols;
+    const float* hx = tape + tape_layout(num_atoms, nf, H, n_layers).hx +
+                      (size_t)l * num_atoms * (nf + H);
+    OuterBatch ob;
+    ob.nd = 0;
+    int wg = 0;
+    float* part = ws + Wl.part;
+    add_desc(ob, wg, ws + Wl.dp0, H, H, ws + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1);
+    add_desc(ob, wg, ws + Wl.dpe, H, H, ws + Wl.x1, H, H, prow, 0, prb, part, G + R.We2, G + R.be2);
+    add_desc(ob, wg, ws + Wl.ac, H, H, ws + Wl.e, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1);
+    add_desc(ob, wg, ws + Wl.aphi, 1, 1, ws + Wl.sc, H, H, prow, 0, prb, part, G + R.wc2, nullptr);
+    add_desc(ob, wg, ws + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
+    add_desc(ob, wg, ws + Wl.aq, 1, 1, ws + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
+    add_desc(ob, wg, ws + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,
+             G + R.bn1);
+    add_desc(ob, wg, ws + Wl.agr, nf, nf, ws + Wl.sn, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wn2,
+             G + R.bn2);
+    const int rc = run_outer(ob, wg, st);
+    if (rc) return rc;
+  }
+
+  if (dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
+    float* apre = ws + Wl.au;
+    float* spre = ws + Wl.su;
+    float* anet = ws + Wl.anet;
+#define CALL(HH, NN)                                                                                      \
+  hipLaunchKernelGGL((argmax_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, mol_ptr, nf, h_data, \
+                     noise, dequant_raw, adj_h, adj_ldj, apre, spre, anet)
+    DISPATCH_HN_B(H, max_mol_atoms, CALL);
+#undef CALL
+    const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
+    OuterBatch ob;
+    ob.nd = 0;
+    int wg = 0;
+    float* part = ws + Wl.part;
+    add_desc(ob, wg, apre, H, H, h_data, nf, nf, nullptr, num_atoms, num_atoms, part, grad_dequant + rW1,
+             grad_dequant + rb1);
+    add_desc(ob, wg, anet, 2 * nf, 2 * nf, spre, H, H, nullptr, num_atoms, num_atoms, part, grad_dequant + rW2,
+             grad_dequant + rb2);
+    const int rc = run_outer(ob, wg, st);
+    if (rc) return rc;
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+}  // extern "C"

@@ -164,6 +164,25 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
     STAMP(4);
     if (!(ENFLOW_ABLATE & 2)) node_phase(sm, Lp, L, n, nf, tid_l);
     STAMP(5);
+    if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q
+      const TapeLayout T = tape_layout(A.num_atoms, nf, H, A.n_layers);
+      const size_t la = (size_t)l * A.num_atoms + M.a0;
+      float* hx = A.tape + T.hx + la * T.ldhx;
+      for (int e = tid; e < n * T.ldhx; e += BLOCK) {
+        const int a = e / T.ldhx, c = e - a * T.ldhx;
+        hx[e] = c < nf ? sm.h[a * NFP + c] : sm.agg[a * AST + (c - nf)];
+      }
+      for (int e = tid; e < n * nf; e += BLOCK) {
+        const int a = e / nf, q = e - a * nf;
+        A.tape[T.g + la * nf + e] = sm.g[a * NFP + q];
+      }
+      for (int e = tid; e < n * 3; e += BLOCK) {
+        A.tape[T.pos + la * 3 + e] = sm.pos[e];
+        A.tape[T.vel + la * 3 + e] = sm.vel[e];
+      }
+      for (int a = tid; a < n; a += BLOCK) A.tape[T.q + la + a] = sm.Q[a];
+      if (tid == 0 && A.pair_counts != nullptr) A.pair_counts[(size_t)l * A.num_mols + blockIdx.x] = sm.npairs;
+    }
     for (int a = tid; a < n; a += BLOCK) {
       const float q = sm.Q[a];
       const float eq = expf(q);
@@ -444,15 +463,15 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           int dequant_kind, const float* dequant, const float* noise,
                           float dequant_scale, float dt, float cw,
                           float* ldj_mol, float* ldj_total, int32_t* err_flag, uint64_t* pair_stats,
-                          void* stream) {
+                          float* tape, int32_t* pair_counts, void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
-  (void)num_atoms;
+  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr)) return -1;
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
              dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
-             reinterpret_cast<unsigned long long*>(pair_stats)};
+             reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
   if (num_mols > 0) {
 #define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);

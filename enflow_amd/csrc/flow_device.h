@@ -10,7 +10,7 @@
 
 #include "enflow_hip.h"
 
-#define ENFLOW_ABI 1
+#define ENFLOW_ABI 2
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8
@@ -93,6 +93,41 @@ __host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
   R.bv2 = o; o += 1;
   R.total = o;
   return R;
+}
+
+// Backward-only packed EGCL section (floats): transposed fragments for the
+// adjoint GEMMs of the edge chain and k-contiguous node weights for the VALU
+// node backward (threads over hidden units k read coalesced rows).
+struct EgclBwdLayout { int we2T, wc1T, we1T, wv1T, wn1T, total; };
+__host__ __device__ inline EgclBwdLayout egcl_bwd_layout(int H) {
+  const int NT = H / 32;
+  EgclBwdLayout L;
+  int o = 0;
+  L.we2T = o; o += H * H;             // fragments of edge_nn.2.weight^T   (as we2f)
+  L.wc1T = o; o += H * H;             // fragments of coord_nn.0.weight^T  (as wc1f)
+  L.we1T = o; o += NT * 4 * 256;      // [tp][rg][lane][4]: A[q][k] = edge_nn.0.weight[k][q], q < 2nf+1
+  L.wv1T = o; o += NFMAX * H;         // [f][k] = vel_scaling_nn.0.weight[k][f]
+  L.wn1T = o; o += (NFMAX + H) * H;   // [f][k] = node_nn.0.weight[k][f] (rows NFMAX.. = agg part)
+  o = (o + 63) & ~63;
+  L.total = o;
+  return L;
+}
+
+// Training tape written by the forward (one block per quantity, layer-major):
+// per layer l and atom a the layer INPUT state and what the backward re-reads.
+struct TapeLayout { size_t hx, g, pos, vel, q, total; int ldhx; };
+__host__ __device__ inline TapeLayout tape_layout(int num_atoms, int nf, int H, int n_layers) {
+  TapeLayout T;
+  const size_t LA = (size_t)num_atoms * n_layers;
+  T.ldhx = nf + H;
+  size_t o = 0;
+  T.hx = o; o += LA * (nf + H);   // [l][a][h (nf) | message sums (H)]  (X of node_nn.0's gradient)
+  T.g = o; o += LA * nf;
+  T.pos = o; o += LA * 3;
+  T.vel = o; o += LA * 3;
+  T.q = o; o += LA;               // Q = vel_scaling_nn(h)
+  T.total = o;
+  return T;
 }
 
 struct AmLayout { int wa1t, ba1, wa2, ba2, total; };
@@ -863,6 +898,9 @@ struct FlowArgs {
   int32_t* max_idx;
   int32_t* err;
   unsigned long long* stats;   // optional: [0] += unique pairs, [1] += reference edges
+  float* tape;                 // optional (training): TapeLayout block
+  int32_t* pair_counts;        // optional (training): [n_layers][num_mols] unique pairs
+  int num_mols, num_atoms;
 };
 
 enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };

@@ -1,0 +1,171 @@
+"""Autograd glue of the HIP training path.
+
+``LFIntegrator.forward`` (enflow/flow/dynamics.py:10-24) and
+``Alchemical_NLL.__call__`` (enflow/flow/loss.py:21-24) become
+``torch.autograd.Function`` s whose backward passes call the C ABI
+(enflow_alchemical_nll_backward_f32, enflow_lf_backward_f32).  Parameters
+enter the flow function as inputs, so ``loss.backward()`` fills every
+``p.grad`` exactly like the reference's autograd, and DDP / optimisers / LR
+schedulers work on them unchanged (enflow/main.py:212-223).
+"""
+import torch
+
+from .. import _lib
+from ..nn.argmax import ArgMax
+
+
+def pair_row_bound(N):
+    """Upper bound of the backward's pair rows: sum of n(n-1) rounded up to 32."""
+    N = torch.as_tensor(N).reshape(-1).to(torch.int64)
+    return int((((N * (N - 1)) + 31) // 32 * 32).sum())
+
+
+class _FlowFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flow, meta, h, g, pos, vel, *params):
+        hid, nf, cw = flow._geometry()
+        kind = flow._dequant_kind()
+        dev = h.device
+        L = _lib.lib()
+        n_layers = len(flow.networks)
+        A = h.shape[0]
+        M = meta["mol_ptr"].numel() - 1
+        h_in = h.detach().clone()
+        hw, gw, pw, vw = (t.detach().clone() for t in (h, g, pos, vel))
+        tape = torch.empty(max(L.enflow_lf_tape_size(A, nf, hid, n_layers), 1), dtype=torch.float32, device=dev)
+        counts = torch.zeros(max(n_layers * M, 1), dtype=torch.int32, device=dev)
+        ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
+        ldj = torch.empty(1, dtype=torch.float32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"], meta["max_n"],
+                             meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts)
+        if meta["check_errors"]:
+            _lib.raise_on_err(err)
+        ctx.flow, ctx.meta, ctx.kind = flow, meta, kind
+        ctx.n_params = len(params)
+        ctx.save_for_backward(h_in, tape, counts)
+        return hw, gw, pw, vw, ldj.reshape(())
+
+    @staticmethod
+    def backward(ctx, gh, gg, gpos, gvel, gldj):
+        flow, meta, kind = ctx.flow, ctx.meta, ctx.kind
+        h_in, tape, counts = ctx.saved_tensors
+        hid, nf, cw = flow._geometry()
+        dev = h_in.device
+        L = _lib.lib()
+        A = h_in.shape[0]
+        M = meta["mol_ptr"].numel() - 1
+        n_layers = len(flow.networks)
+
+        def adj(t, shape):
+            if t is None:
+                return torch.zeros(shape, dtype=torch.float32, device=dev)
+            return t.detach().to(dtype=torch.float32).contiguous().clone()
+
+        ah, ag = adj(gh, (A, nf)), adj(gg, (A, nf))
+        apos, avel = adj(gpos, (A, 3)), adj(gvel, (A, 3))
+        aldj = adj(gldj, ()).reshape(1)
+        fwd, bwd, raw = flow.training_layers(dev)
+        grad_layers = torch.empty_like(raw)
+        dq_raw, grad_dq = None, None
+        if kind == _lib.DEQUANT_ARGMAX:
+            dq_raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
+                                for p in flow.dequantize.parameters()])
+            grad_dq = torch.empty_like(dq_raw)
+        prb = meta["pair_row_bound"]
+        wsb = L.enflow_lf_backward_workspace_size(M, A, nf, hid, n_layers, prb)
+        if wsb < 0:
+            raise _lib.HipPathError("enflow_lf_backward_workspace_size rejected the batch")
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        _lib.check(L.enflow_lf_backward_f32(
+            M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+            _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw),
+            n_layers, kind, _lib.ptr(dq_raw), _lib.ptr(h_in), _lib.ptr(meta["noise"]), float(flow.dt), cw,
+            _lib.ptr(ah), _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj),
+            _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
+            _lib.stream_ptr(dev)), "enflow_lf_backward_f32")
+        if meta["check_errors"]:
+            _lib.raise_on_err(err)
+        # split the flat gradients into the parameters' shapes (inputs order)
+        grads = []
+        off = 0
+        for net in flow.networks:
+            for _, p in net.named_parameters():
+                grads.append(grad_layers[off:off + p.numel()].view(p.shape).to(p.dtype))
+                off += p.numel()
+        if kind == _lib.DEQUANT_ARGMAX:
+            off = 0
+            for p in flow.dequantize.parameters():
+                grads.append(grad_dq[off:off + p.numel()].view(p.shape).to(p.dtype))
+                off += p.numel()
+        # d h of the data only exists without a learned dequantiser (z = h + noise)
+        gh_in = ah if kind != _lib.DEQUANT_ARGMAX else None
+        return (None, None, gh_in, ag, apos, avel) + tuple(grads)
+
+
+def flow_forward_train(flow, data, noise, check_errors):
+    """Differentiable LFIntegrator.forward (HIP forward with tape)."""
+    s = flow._state(data)
+    dev = s["dev"]
+    kind = flow._dequant_kind()
+    if noise is None:
+        if kind == _lib.DEQUANT_ARGMAX:
+            noise = torch.randn(s["h"].shape, device=dev, dtype=torch.float32)
+        elif kind == _lib.DEQUANT_FLOOR:
+            noise = torch.rand(s["h"].shape, device=dev, dtype=torch.float32)
+    else:
+        noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+    meta = dict(box=s["box"], r_cut=s["r_cut"], mol_ptr=s["mol_ptr"], max_n=s["max_n"], noise=noise,
+                check_errors=check_errors, pair_row_bound=pair_row_bound(data.N))
+    params = [p for n in flow.networks for _, p in n.named_parameters()]
+    if isinstance(flow.dequantize, ArgMax):
+        params += list(flow.dequantize.parameters())
+
+    def inp(t):
+        return t.to(device=dev, dtype=torch.float32)
+
+    h, g, pos, vel, ldj = _FlowFunction.apply(flow, meta, inp(data.h), inp(data.g), inp(data.pos),
+                                              inp(data.vel), *params)
+    dt = data.h.dtype
+    data.h, data.g = h.to(dt), g.to(dt)
+    data.pos, data.vel = pos.to(data.pos.dtype), vel.to(data.vel.dtype)
+    return data, ldj.to(dt)
+
+
+class _NLLFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, nll, meta, h, g, pos, vel, ldj):
+        L = _lib.lib()
+        dev = h.device
+        M = meta["mol_ptr"].numel() - 1
+        nll_mol = torch.empty((max(M, 1), 4), dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        ldj_t = ldj.detach().reshape(1).contiguous()
+        hc, gc, pc, vc = (t.detach().contiguous() for t in (h, g, pos, vel))
+        _lib.check(L.enflow_alchemical_nll_f32(M, h.shape[0], meta["max_n"], h.shape[1],
+                                               _lib.ptr(meta["mol_ptr"]), _lib.ptr(hc), _lib.ptr(gc),
+                                               _lib.ptr(pc), _lib.ptr(vc), _lib.ptr(ldj_t), float(nll.kBT),
+                                               float(nll.softening), float(nll.z_lj), _lib.ptr(nll_mol),
+                                               _lib.ptr(loss), _lib.stream_ptr(dev)), "enflow_alchemical_nll_f32")
+        ctx.nll, ctx.meta = nll, meta
+        ctx.save_for_backward(hc, gc, pc, vc)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, gloss):
+        h, g, pos, vel = ctx.saved_tensors
+        nll, meta = ctx.nll, ctx.meta
+        L = _lib.lib()
+        dev = h.device
+        M = meta["mol_ptr"].numel() - 1
+        ah, ag = torch.empty_like(h), torch.empty_like(g)
+        apos, avel = torch.empty_like(pos), torch.empty_like(vel)
+        aldj = torch.empty(1, dtype=torch.float32, device=dev)
+        gl = gloss.detach().to(torch.float32).reshape(1).contiguous()
+        _lib.check(L.enflow_alchemical_nll_backward_f32(
+            M, h.shape[0], meta["max_n"], h.shape[1], _lib.ptr(meta["mol_ptr"]), _lib.ptr(h), _lib.ptr(g),
+            _lib.ptr(pos), _lib.ptr(vel), float(nll.kBT), float(nll.softening), _lib.ptr(gl), _lib.ptr(ah),
+            _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj), _lib.stream_ptr(dev)),
+            "enflow_alchemical_nll_backward_f32")
+        return None, None, ah, ag, apos, avel, aldj.reshape(())

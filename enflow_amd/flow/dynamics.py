@@ -51,10 +51,13 @@ class LFIntegrator(BaseFlow):
             return _lib.DEQUANT_NONE
         raise NotImplementedError(f"unsupported dequantiser {type(d).__name__}")
 
+    def _params_key(self, device):
+        params = [p for n in self.networks for _, p in n.named_parameters()]
+        return (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+
     def packed_layers(self, device):
         """All layers packed back to back (cached; re-packed on any parameter change)."""
-        params = [p for n in self.networks for _, p in n.named_parameters()]
-        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        key = self._params_key(device)
         if getattr(self, "_layers_key", None) == key:
             return self._layers_buf
         hid, nf, _ = self._geometry()
@@ -66,14 +69,38 @@ class LFIntegrator(BaseFlow):
         self._layers_buf, self._layers_key = buf, key
         return buf
 
+    def training_layers(self, device):
+        """(forward-packed, backward-packed, raw) layer buffers for the HIP backward."""
+        key = self._params_key(device)
+        if getattr(self, "_train_key", None) == key:
+            return self._train_bufs
+        hid, nf, _ = self._geometry()
+        L = _lib.lib()
+        raw = torch.cat([torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
+                                    for _, p in n.named_parameters()]) for n in self.networks])
+        stride = L.enflow_egcl_bwd_packed_size(hid, nf)
+        rstride = raw.numel() // max(len(self.networks), 1)
+        bwd = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)
+        for i in range(len(self.networks)):
+            _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw[i * rstride:]), hid, nf,
+                                                  _lib.ptr(bwd[i * stride:]), _lib.stream_ptr(device)),
+                       "enflow_pack_egcl_bwd_f32")
+        self._train_bufs = (self.packed_layers(device), bwd, raw)
+        self._train_key = key
+        return self._train_bufs
+
+    def _needs_grad(self):
+        return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
+
     def _warn_grad(self):
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            warnings.warn("enflow_amd LFIntegrator: HIP backward is not implemented yet; outputs "
-                          "are detached", RuntimeWarning, stacklevel=3)
+        if self._needs_grad():
+            warnings.warn("enflow_amd LFIntegrator.reverse is not differentiable (the reference "
+                          "only trains through forward); outputs are detached",
+                          RuntimeWarning, stacklevel=3)
 
     # ------------------------------------------------------------------
     def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
-                        ldj_mol, ldj_total, err, pair_stats=None):
+                        ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None):
         """In-place fused forward on preallocated fp32 device buffers (no
         host sync, no allocation): the entry point the benchmark times."""
         hid, nf, cw = self._geometry()
@@ -87,7 +114,8 @@ class LFIntegrator(BaseFlow):
             _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
             _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
             _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
-            _lib.ptr(err), _lib.ptr(pair_stats), _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
+            _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts),
+            _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
 
     def _state(self, data):
         _lib.require_gpu(data.pos)
@@ -101,8 +129,14 @@ class LFIntegrator(BaseFlow):
 
     def forward(self, data, noise=None, check_errors=True):
         """dynamics.py:10-24.  ``noise`` optionally supplies the dequantiser's
-        draw (N(0,1) for ArgMax, U[0,1) for Floor), shape h.shape."""
-        self._warn_grad()
+        draw (N(0,1) for ArgMax, U[0,1) for Floor), shape h.shape.
+
+        With autograd enabled and trainable parameters the outputs carry a
+        grad_fn whose backward is the HIP backward (enflow_lf_backward_f32),
+        so the reference's ``loss.backward()`` / optimiser loop runs unchanged."""
+        if self._needs_grad():
+            from ._train import flow_forward_train
+            return flow_forward_train(self, data, noise, check_errors)
         s = self._state(data)
         dev = s["dev"]
         kind = self._dequant_kind()

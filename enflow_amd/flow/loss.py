@@ -3,7 +3,8 @@
 __call__(out, ldj) -> 0-d tensor, computed by enflow_alchemical_nll_f32: one
 workgroup per molecule sums the softened LJ energy over i < j pairs (zero
 distances dropped, loss.py:14-18), sum vel^2, h^2, g^2; a fixed-order double
-reduction forms the reference's scalar.
+reduction forms the reference's scalar.  When its inputs carry autograd
+history the loss is differentiable (backward: enflow_alchemical_nll_backward_f32).
 """
 import torch
 
@@ -19,6 +20,9 @@ class Alchemical_NLL:
 
     def __call__(self, out, ldj):
         _lib.require_gpu(out.pos)
+        if torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad
+                                           for t in (out.h, out.g, out.pos, out.vel, ldj)):
+            return self._differentiable(out, ldj)
         L = _lib.lib()
         dev = out.pos.device
         f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
@@ -34,3 +38,14 @@ class Alchemical_NLL:
                                                float(self.z_lj), _lib.ptr(nll_mol), _lib.ptr(loss),
                                                _lib.stream_ptr(dev)), "enflow_alchemical_nll_f32")
         return loss.reshape(()).to(out.h.dtype)
+
+    def _differentiable(self, out, ldj):
+        """Same value, with a grad_fn whose backward is enflow_alchemical_nll_backward_f32."""
+        from ._train import _NLLFunction
+        dev = out.pos.device
+        ptr, max_n = batch_meta(out, dev)
+        f = lambda t: t.to(device=dev, dtype=torch.float32)  # noqa: E731
+        ldj_t = torch.as_tensor(ldj, device=dev)
+        loss = _NLLFunction.apply(self, {"mol_ptr": ptr, "max_n": max_n}, f(out.h), f(out.g), f(out.pos),
+                                  f(out.vel), ldj_t.to(torch.float32).reshape(()))
+        return loss.to(out.h.dtype)

@@ -89,6 +89,11 @@ int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,
  *   ldj_total [1]      : batch log|detJ| exactly as the reference's scalar (out)
  *   pair_stats [2]     : optional (NULL = off); += unique neighbour pairs and
  *                        += reference edge-list entries, summed over layers
+ *   tape               : optional (NULL = inference); training tape of
+ *                        enflow_lf_tape_size floats: per layer the layer-input
+ *                        state, message sums and Q, read by enflow_lf_backward_f32
+ *   pair_counts        : [n_layers][num_mols] unique pairs per layer (required
+ *                        with tape)
  */
 int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
                           const int32_t* mol_ptr, const float* r_cut, const float* box,
@@ -97,7 +102,7 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
                           int dequant_kind, const float* dequant, const float* noise,
                           float dequant_scale, float dt, float coords_weight,
                           float* ldj_mol, float* ldj_total, int32_t* err_flag,
-                          uint64_t* pair_stats, void* stream);
+                          uint64_t* pair_stats, float* tape, int32_t* pair_counts, void* stream);
 
 /*
  * LFIntegrator.reverse (enflow/flow/dynamics.py:26-37), all layers fused.
@@ -161,6 +166,64 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
                               const float* pos, const float* vel, const float* ldj_total,
                               float kBT, float softening, float partition_func,
                               float* nll_mol, float* loss, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Training (the reference's loss.backward(), enflow/main.py:219-221):
+ * reverse-mode gradients of Alchemical_NLL(LFIntegrator(data)) w.r.t. every
+ * EGCL / ArgMax parameter, in torch parameter layout.
+ * ---------------------------------------------------------------------- */
+
+/* Floats of the training tape enflow_lf_forward_f32 writes. */
+int64_t enflow_lf_tape_size(int num_atoms, int node_nf, int hidden_nf, int n_layers);
+
+/* Backward-only packed section of one EGCL layer (transposed MFMA fragments,
+ * k-contiguous node weights): size in floats, and the packing kernel (same
+ * raw concatenation as enflow_pack_egcl_f32). */
+int64_t enflow_egcl_bwd_packed_size(int hidden_nf, int node_nf);
+int enflow_pack_egcl_bwd_f32(const float* raw, int hidden_nf, int node_nf, float* packed, void* stream);
+
+/* Bytes of scratch enflow_lf_backward_f32 needs.  pair_row_bound >= the sum
+ * over molecules of n_m (n_m - 1) rounded up to a multiple of 32. */
+int64_t enflow_lf_backward_workspace_size(int num_mols, int num_atoms, int node_nf, int hidden_nf,
+                                          int n_layers, int64_t pair_row_bound);
+
+/*
+ * Alchemical_NLL backward (enflow/flow/loss.py:11-24): adjoints of the flow
+ * outputs adj_h, adj_g [num_atoms][nf], adj_pos, adj_vel [num_atoms][3] and of
+ * log|detJ| adj_ldj [1] (all out), scaled by *grad_loss (NULL = 1).
+ */
+int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf,
+                                       const int32_t* mol_ptr, const float* h, const float* g,
+                                       const float* pos, const float* vel, float kBT, float softening,
+                                       const float* grad_loss, float* adj_h, float* adj_g, float* adj_pos,
+                                       float* adj_vel, float* adj_ldj, void* stream);
+
+/*
+ * LFIntegrator.forward backward (enflow/flow/dynamics.py:10-24 with
+ * enflow/nn/egcl.py:57-92 and enflow/nn/argmax.py:13-25).
+ *   tape, pair_counts : written by enflow_lf_forward_f32 on the same inputs
+ *   layers            : forward-packed layers (enflow_pack_egcl_f32)
+ *   layers_bwd        : backward-packed layers (enflow_pack_egcl_bwd_f32)
+ *   layers_raw        : raw torch-layout layers (stride = EGCL parameter count)
+ *   dequant_raw       : raw ArgMax parameters; h_data the flow's input h
+ *                       (before dequantisation) and noise its N(0,1) draw
+ *   adj_h/g/pos/vel   : in: adjoints of the flow outputs; out: of the inputs
+ *                       (adj_h: of the dequantised h)
+ *   adj_ldj [1]       : adjoint of log|detJ|
+ *   grad_layers       : out, [n_layers][EGCL parameter count] (named_parameters
+ *                       order, torch layouts), grad_dequant: out, ArgMax layout
+ *   workspace         : >= enflow_lf_backward_workspace_size bytes
+ */
+int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                           const int32_t* mol_ptr, const float* r_cut, const float* box,
+                           const float* tape, const int32_t* pair_counts,
+                           const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                           int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                           float dt, float coords_weight,
+                           float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                           float* grad_layers, float* grad_dequant,
+                           void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                           int32_t* err_flag, void* stream);
 
 #ifdef __cplusplus
 }

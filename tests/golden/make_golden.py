@@ -217,7 +217,47 @@ def case_flow(hid, n_layers, sizes, seed, name):
     save(name, inp, fwd)
 
 
+def case_train(hid, n_layers, sizes, seed, name, nf=5):
+    """One training step of the reference (enflow/main.py:217-221):
+    out, ldj = model(data); loss = nll(out, ldj); loss.backward() -- the
+    parameter gradients of every EGCL layer and of the ArgMax dequantiser."""
+    torch.manual_seed(seed)
+    dt = default_dt()
+    nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+    model = LFIntegrator(nets, ArgMax(nf, hid), dt=dt)   # BaseFlow casts to float64
+    b = batch_inputs(len(sizes), sizes, nf, seed=seed)
+    d = ref_data(b)
+    torch.manual_seed(seed + 1)
+    eps = torch.randn(d.h.size())
+    torch.manual_seed(seed + 1)
+    out, ldj = model(d)
+    kBT = default_kBT()
+    nll = Alchemical_NLL(kBT=kBT, softening=0.1)
+    loss = nll(out, ldj)
+    loss.backward()
+    inp = dict(b)
+    inp["eps"] = eps.numpy()
+    inp["dt"] = np.array(dt)
+    inp["kBT"] = np.array(kBT)
+    inp["softening"] = np.array(0.1)
+    inp["n_layers"] = np.array(n_layers)
+    inp["hid"] = np.array(hid)
+    res = {"loss": float(loss), "ldj": float(ldj)}
+    for i, net in enumerate(model.networks):
+        inp.update({f"p{i}.{k}": v.detach().numpy().astype(np.float32) for k, v in net.named_parameters()})
+        res.update({f"grad_p{i}.{k}": v.grad.numpy() for k, v in net.named_parameters()})
+    inp.update({f"dq.{k}": v.detach().numpy().astype(np.float32)
+                for k, v in model.dequantize.named_parameters()})
+    res.update({f"grad_dq.{k}": v.grad.numpy() for k, v in model.dequantize.named_parameters()})
+    save(name, inp, res)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "train":
+        case_train(32, 3, [22, 9, 15, 3], 21, "train_h32_L3")
+        case_train(128, 2, [22, 22], 22, "train_h128_L2")
+        case_train(64, 2, [22, 40, 7], 23, "train_h64_L2")
+        sys.exit(0)
     case_edges()
     case_egcl(32, 3)
     case_egcl(128, 4)

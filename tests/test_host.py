@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 1
+    assert L.enflow_abi_version() == 2
     assert L.enflow_max_atoms() == 64
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
@@ -48,12 +48,28 @@ def test_abi_queries():
 def test_argument_errors_launch_nothing():
     L = _lib.lib()
     # too-large molecule, bad hidden width, bad nf: rejected before any launch
-    args = [1, 100, 100, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 5
+    args = [1, 100, 100, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 7
     assert L.enflow_lf_forward_f32(*args) == -3
     args[2], args[4] = 20, 96
     assert L.enflow_lf_forward_f32(*args) == -5
     args[3], args[4] = 9, 128
     assert L.enflow_lf_forward_f32(*args) == -4
+
+
+def test_backward_sizes_and_argument_errors():
+    L = _lib.lib()
+    A, M, nf, H, nl = 22 * 4, 4, 5, 128, 8
+    assert L.enflow_lf_tape_size(A, nf, H, nl) == nl * A * (nf + H + nf + 3 + 3 + 1)
+    assert L.enflow_egcl_bwd_packed_size(H, nf) >= 2 * H * H
+    assert L.enflow_egcl_bwd_packed_size(96, nf) == -1
+    assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480) > 4 * 480 * 6 * H * 4
+    assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, -1) == -1
+    # missing tape / buffers: rejected before any launch
+    args = [M, A, 22, nf, H] + [None] * 8 + [nl, 1, None, None, None, 0.1, 1.0] + [None] * 7 + \
+        [None, 0, 480 * 4, None, None]
+    assert L.enflow_lf_backward_f32(*args) == -1
+    args[2] = 100
+    assert L.enflow_lf_backward_f32(*args) == -1
 
 
 def test_synthetic_batch_layout():

@@ -77,3 +77,25 @@ def test_multiplicity_roundtrip():
     pi, pj, pc = O.pair_multiplicity(out["row"], out["col"], n)
     assert int(pc.sum()) == len(out["row"])
     assert np.all(pc >= 1)
+
+
+TRAIN_CASES = ["train_h32_L3", "train_h128_L2", "train_h64_L2"]
+
+
+@pytest.mark.parametrize("name", TRAIN_CASES)
+def test_gradient_oracle_matches_reference_backward(name):
+    """The gradient oracle (torch float64 restatement) reproduces the reference's
+    loss.backward() on every parameter (enflow/main.py:219-221)."""
+    from oracle import enflow_oracle_grad as OG
+    inp, out = load(name)
+    nl = n_layers(inp)
+    loss, ldj, gl, gd, _ = OG.train_loss_and_grads(
+        [layer_params(inp, i) for i in range(nl)], dequant_params(inp), state(inp),
+        inp["eps"].astype(np.float64), float(inp["dt"]), float(inp["kBT"]), float(inp["softening"]))
+    assert abs(loss - out["loss"]) <= 1e-12 * abs(out["loss"])
+    assert abs(ldj - out["ldj"]) <= 1e-12 * abs(out["ldj"])
+    for i in range(nl):
+        for k, v in gl[i].items():
+            np.testing.assert_allclose(v, out[f"grad_p{i}.{k}"], rtol=1e-9, atol=1e-12 * np.abs(out[f"grad_p{i}.{k}"]).max())
+    for k, v in gd.items():
+        np.testing.assert_allclose(v, out[f"grad_dq.{k}"], rtol=1e-9, atol=1e-12 * np.abs(out[f"grad_dq.{k}"]).max())
