@@ -105,6 +105,105 @@ def workload_name():
     return f"lf_forward_{MOLS_PER_GPU}x{ATOMS}_L{LAYERS}_H{HID}_nf{NF}_f32"
 
 
+TRAIN_METRIC = "molecule-train-steps/sec (fwd+NLL+bwd+Adam, RCCL grad all-reduce), batch 1024×64 atoms per GPU"
+TRAIN_ATOMS = 64
+
+
+def train_flops(pairs, atoms, layers, hid, nf):
+    """Algorithmic FLOPs of one training step's flow part: the forward
+    (flops_per_launch) plus, per unique pair, the recomputed edge chain, its
+    adjoint GEMMs (coord_nn.0^T, edge_nn.2^T, edge_nn.0^T) and the three
+    weight-gradient outer products; per atom-layer the node MLP recompute,
+    adjoint and weight gradients."""
+    fwd_pair = 2 * hid * (2 * nf + 1) + 4 * hid * hid + 2 * hid
+    bwd_pair = fwd_pair + (4 * hid * hid + 2 * hid * (2 * nf + 1)) + (4 * hid * hid + 2 * hid * (2 * nf + 2) + 2 * hid)
+    node = (2 * hid * nf + 2 * hid) + (2 * hid * (hid + nf) + 2 * hid * nf)
+    return (flops_per_launch(pairs, atoms, layers, hid, nf) + pairs * bwd_pair +
+            atoms * layers * 3 * node)
+
+
+def run_train(args, world, rank, local, device, dist):
+    """Config 3: a full training step (the reference's loop body,
+    enflow/main.py:217-223) per GPU on 1024 synthetic 64-atom molecules."""
+    from enflow_amd.data.synthetic import make_molecules, default_dt, default_kBT
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator, Alchemical_NLL
+    from enflow_amd.data import Data
+    atoms = args.atoms or TRAIN_ATOMS
+    radius = 4.0 * (atoms / 22.0) ** (1.0 / 3.0)
+    b = make_molecules(MOLS_PER_GPU, atoms, nf=NF, seed=2000 + rank, radius=radius)
+    torch.manual_seed(0)
+    model = LFIntegrator([EGCL(NF, NF, HID) for _ in range(LAYERS)], ArgMax(NF, HID), dt=default_dt()).to(device)
+    net = model
+    if dist:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        net = DDP(model, device_ids=[local])      # main.py:159; backend nccl = RCCL
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    nll = Alchemical_NLL(kBT=default_kBT(), softening=0.1)
+    base = Data.from_arrays(b, device=device)
+    noise = torch.empty_like(base.h)
+    gen = torch.Generator(device).manual_seed(rank)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        torch.randn(noise.shape, generator=gen, out=noise)
+        out, ldj = net(base._replace(), noise=noise)
+        loss = nll(out, ldj)
+        loss.backward()
+        opt.step()
+        return loss
+
+    # pair statistics for the algorithmic FLOPs (one counted inference forward)
+    stats = torch.zeros(2, dtype=torch.int64, device=device)
+    with torch.no_grad():
+        ptr = base.mol_ptr
+        w = {k: getattr(base, k).clone() for k in ("h", "g", "pos", "vel")}
+        ldj_mol = torch.empty(MOLS_PER_GPU, dtype=torch.float32, device=device)
+        ldj = torch.empty(1, dtype=torch.float32, device=device)
+        err = torch.zeros(1, dtype=torch.int32, device=device)
+        model.forward_buffers(w["h"], w["g"], w["pos"], w["vel"], base.box, base.r_cut, ptr, atoms,
+                              torch.randn_like(w["h"]), ldj_mol, ldj, err, stats)
+    torch.cuda.synchronize()
+    if int(err.item()) != 0:
+        raise RuntimeError(f"flow kernel error flag {int(err.item())}")
+    pairs = int(stats[0].item())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    from enflow_amd.distributed import max_over_ranks
+    elapsed = max_over_ranks(time.perf_counter() - t0, device)
+    if rank == 0:
+        n_atoms = MOLS_PER_GPU * atoms
+        flops = train_flops(pairs, n_atoms, LAYERS, HID, NF)
+        ms = elapsed / args.steps * 1e3
+        line = {
+            "metric": TRAIN_METRIC, "value": MOLS_PER_GPU * world * args.steps / elapsed,
+            "unit": "molecules/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": f"synthetic (random-walk {atoms}-atom molecules, random-init weights)",
+            "config": {"workload": f"lf_train_{MOLS_PER_GPU}x{atoms}_L{LAYERS}_H{HID}_nf{NF}_f32",
+                       "molecules_per_gpu": MOLS_PER_GPU, "atoms_per_molecule": atoms,
+                       "coupling_layers": LAYERS, "hidden_nf": HID, "node_nf": NF,
+                       "global_batch": MOLS_PER_GPU * world,
+                       "parallelism": f"molecule-sharded x{world}, DDP grad all-reduce" if world > 1
+                       else "single GPU", "unique_pairs_per_layer_pass": pairs},
+            "step_tflops": flops / (ms * 1e-3) / 1e12, "flops_per_step": flops,
+            "final_loss": float(loss),
+        }
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -112,6 +211,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1536)
+    ap.add_argument("--mode", choices=("forward", "train"), default="forward",
+                    help="forward: the headline metric (configs[1]); train: configs[3] per GPU")
+    ap.add_argument("--atoms", type=int, default=None, help="train mode: atoms per molecule (default 64)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,6 +225,13 @@ def main():
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
+
+    if args.mode == "train":
+        run_train(args, world, rank, local, device, dist)
+        if dist:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     b, model, inp = build_workload(rank, device)
     n_atoms = inp["h"].shape[0]
