@@ -527,7 +527,6 @@ struct OuterBatch {
   int nd;
   int start[OUTER_MAX + 1];   // first workgroup of each descriptor
 };
-#define OA_ROWS 32
 #define OA_CHUNK 2048
 
 __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
@@ -536,56 +535,121 @@ __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
   return k;
 }
 
-__global__ void __launch_bounds__(256) outer_acc_kernel(OuterBatch ob) {
+// One workgroup = one chunk of OA_CHUNK rows x a 128-column block of X, the
+// whole M (<= 128) of DY.  Rows are staged through LDS 32 at a time (double
+// buffered: the next stage's global loads are in flight during this stage's
+// MFMAs).  Waves own 64 x 64 quadrants of the 128 x 128 output as four
+// v_mfma_f32_32x32x2_f32 accumulators; each k-step (2 rows) reads its A / B
+// fragments straight from the row-major LDS image (lanes along m / n:
+// conflict-free).  M == 1 (coord_nn.2 / vel_scaling_nn.2) is a plain column
+// reduction and runs on VALU.  The bias column (sum of DY) is accumulated by
+// the n-block-0 workgroup from the same LDS image.
+#define OB_ROWS 32
+__global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
   const OuterDesc& D = ob.d[k];
   const int local = bid - ob.start[k];
-  const int per = D.mb * D.nb;
-  const int chunk = local / per, rem = local - chunk * per;
-  const int mbi = rem / D.nb, nbi = rem - mbi * D.nb;
+  const int chunk = local / D.nb, nbi = local - chunk * D.nb;
   const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
   const int r0 = chunk * OA_CHUNK;
   if (r0 >= rows) return;
   const int r1 = min(rows, r0 + OA_CHUNK);
   const int NB = D.N + (D.outB ? 1 : 0);
-  const int m0 = mbi * 64, n0 = nbi * 64;
-  __shared__ float sd[OA_ROWS][64];
-  __shared__ float sx[OA_ROWS][64];
-  const int tid = threadIdx.x, tm = tid >> 4, tn = tid & 15;
-  float acc[4][4];
+  const int n0 = nbi * 128;
+  const int M = D.M, N = D.N;
+  __shared__ float sd[2][OB_ROWS][128];
+  __shared__ float sx[2][OB_ROWS][128];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j = lane & 31, hh = lane >> 5;
+  const int mh = w & 1, nh = w >> 1;
+  const bool do_bias = D.outB != nullptr && nbi == 0 && tid < M;
+  float bsum = 0.f;
+  f32x16 acc[2][2];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = 0.f;
-  for (int rb = r0; rb < r1; rb += OA_ROWS) {
-    for (int e = tid; e < OA_ROWS * 64; e += 256) {
-      const int r = e >> 6, cc = e & 63, p = rb + r;
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
+  float vacc = 0.f;   // M == 1 path: column n0 + tid (tid < 128)
+  float rd[16], rx[16];
+  const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
+  auto gload = [&](int st) {
+    const int rb = r0 + st * OB_ROWS;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = q * 256 + tid, r = e >> 7, c = e & 127, p = rb + r;
       const bool pv = p < r1;
-      const int mm = m0 + cc, nn = n0 + cc;
-      sd[r][cc] = (pv && mm < D.M) ? D.DY[(size_t)p * D.ldd + mm] : 0.f;
-      sx[r][cc] = (pv && nn < D.N) ? D.X[(size_t)p * D.ldx + nn] : ((pv && nn == D.N && D.outB) ? 1.f : 0.f);
+      rd[q] = (pv && c < M) ? D.DY[(size_t)p * D.ldd + c] : 0.f;
+      rx[q] = (pv && n0 + c < N) ? D.X[(size_t)p * D.ldx + n0 + c] : 0.f;
     }
-    __syncthreads();
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int e = q * 256 + tid, r = e >> 7, c = e & 127;
+      sd[buf][r][c] = rd[q];
+      sx[buf][r][c] = rx[q];
+    }
+  };
+  // wave-uniform: skip accumulator tiles that only see zero padding
+  const bool use_m1 = mh * 64 + 32 < M, use_n0 = n0 + nh * 64 < N, use_n1 = n0 + nh * 64 + 32 < N;
+  const bool live = mh * 64 < M && use_n0;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) gload(st + 1);
+    if (M > 1) {
+      if (live) {
+        if (use_m1 && use_n1) {
+#pragma unroll 4
+          for (int s = 0; s < OB_ROWS / 2; ++s) {
+            const int r = 2 * s + hh;
+            const float a0 = sd[buf][r][mh * 64 + j], a1 = sd[buf][r][mh * 64 + 32 + j];
+            const float b0 = sx[buf][r][nh * 64 + j], b1 = sx[buf][r][nh * 64 + 32 + j];
+            acc[0][0] = mfma32(a0, b0, acc[0][0]);
+            acc[0][1] = mfma32(a0, b1, acc[0][1]);
+            acc[1][0] = mfma32(a1, b0, acc[1][0]);
+            acc[1][1] = mfma32(a1, b1, acc[1][1]);
+          }
+        } else {
+#pragma unroll 4
+          for (int s = 0; s < OB_ROWS / 2; ++s) {
+            const int r = 2 * s + hh;
+            const float a0 = sd[buf][r][mh * 64 + j], a1 = sd[buf][r][mh * 64 + 32 + j];
+            const float b0 = sx[buf][r][nh * 64 + j], b1 = sx[buf][r][nh * 64 + 32 + j];
+            acc[0][0] = mfma32(a0, b0, acc[0][0]);
+            if (use_n1) acc[0][1] = mfma32(a0, b1, acc[0][1]);
+            if (use_m1) acc[1][0] = mfma32(a1, b0, acc[1][0]);
+          }
+        }
+      }
+    } else if (tid < 128) {
 #pragma unroll 8
-    for (int r = 0; r < OA_ROWS; ++r) {
-      const f32x4 a = ld4(&sd[r][tm * 4]);
-      const f32x4 b = ld4(&sx[r][tn * 4]);
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) acc[u][v] = fmaf(a[u], b[v], acc[u][v]);
+      for (int r = 0; r < OB_ROWS; ++r) vacc = fmaf(sd[buf][r][0], sx[buf][r][tid], vacc);
     }
+    if (do_bias) {
+#pragma unroll 8
+      for (int r = 0; r < OB_ROWS; ++r) bsum += sd[buf][r][tid];
+    }
+    if (st + 1 < nst) lstore(buf ^ 1);
     __syncthreads();
   }
-  float* out = D.part + (size_t)chunk * D.M * NB;
+  float* out = D.part + (size_t)chunk * M * NB;
+  if (M > 1) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int mm = m0 + tm * 4 + u, nn = n0 + tn * 4 + v;
-      if (mm < D.M && nn < NB) out[(size_t)mm * NB + nn] = acc[u][v];
-    }
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int mm = mh * 64 + a * 32 + rho(r, hh), nn = n0 + nh * 64 + b * 32 + j;
+          if (mm < M && nn < N) out[(size_t)mm * NB + nn] = acc[a][b][r];
+        }
+  } else if (tid < 128 && n0 + tid < N) {
+    out[n0 + tid] = vacc;
+  }
+  if (do_bias) out[(size_t)tid * NB + N] = bsum;
 }
 
 __global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
@@ -782,13 +846,14 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.rows_dev = rows_dev; D.rows_static = rows_static;
   D.outW = outW; D.outB = outB;
   const int NB = N + (outB ? 1 : 0);
-  D.mb = cdiv(M, 64);
-  D.nb = cdiv(NB, 64);
+  D.mb = 1;
+  D.nb = cdiv(N, 128);
+  (void)NB;
   D.nch = rows_bound > 0 ? cdiv(rows_bound, OA_CHUNK) : 0;
   D.part = part;
   part += (size_t)D.nch * M * NB;
   ob.start[ob.nd] = wg;
-  wg += D.nch * D.mb * D.nb;
+  wg += D.nch * D.nb;
   ++ob.nd;
   ob.start[ob.nd] = wg;
 }
