@@ -15,6 +15,8 @@ ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2
 ERR_TOO_MANY_FEATURES = 4
 DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
+PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
+PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
 
 _i, _i64, _f, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 
@@ -29,9 +31,9 @@ SIGNATURES = {
     "enflow_pack_egcl_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_pack_argmax_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_lf_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
-                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p, _p, _p]),
+                                   _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p, _p, _i, _p]),
     "enflow_lf_reverse_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
-                                   _i, _f, _f, _p, _p, _p, _p]),
+                                   _i, _f, _f, _p, _p, _p, _i, _p]),
     "enflow_one_hot_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_egcl_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f,
                                      _p, _p, _p, _p, _p]),

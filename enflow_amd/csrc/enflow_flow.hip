@@ -86,8 +86,76 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
     else if (idx < L.wv2) v = raw[R.bv1 + idx - L.bv1];
     else if (idx < L.bn2) v = raw[R.Wv2 + idx - L.wv2];
     else if (idx < L.bv2) { int e = idx - L.bn2; if (e < nf) v = raw[R.bn2 + e]; }
-    else if (idx == L.bv2) v = raw[R.bv2];
+    else if (idx < L.scl) { if (idx == L.bv2) v = raw[R.bv2]; }
+    else if (idx < L.scl + 4) continue;      // written by egcl_scale_kernel
+    else if (idx >= L.we2x && idx < L.we2b) {  // F16X3 fragments: [tp][t][s][lane][hi 8 | lo 8] f16
+      const bool c1 = idx >= L.wc1x;
+      const int e = idx - (c1 ? L.wc1x : L.we2x);
+      const int d = e & 7, lane = (e >> 3) & 63, rest = e >> 9;
+      const int sstep = rest & 1, t = (rest >> 1) % NT, tp = (rest >> 1) / NT;
+      const float sc = out[L.scl + (c1 ? 2 : 0)];
+      const int row = 32 * tp + (lane & 31);
+      uint32_t bits = 0;
+      for (int q = 0; q < 2; ++q) {
+        const int jj = 2 * (d & 3) + q;
+        const int col = 32 * t + rho(8 * sstep + jj, lane >> 5);
+        const float w = raw[(c1 ? R.Wc1 : R.We2) + row * H + col] * sc;
+        const _Float16 hi = (_Float16)w;
+        const _Float16 part = d < 4 ? hi : (_Float16)(w - (float)hi);
+        bits |= (uint32_t)__builtin_bit_cast(uint16_t, part) << (16 * q);
+      }
+      v = __builtin_bit_cast(float, bits);
+    } else if (idx >= L.we2b && idx < L.wc1b + H * H / 2) {  // BF16 fragments: [tp][t][s][lane][8] bf16
+      const bool c1 = idx >= L.wc1b;
+      const int e = idx - (c1 ? L.wc1b : L.we2b);
+      const int d = e & 3, lane = (e >> 2) & 63, rest = e >> 8;
+      const int sstep = rest & 1, t = (rest >> 1) % NT, tp = (rest >> 1) / NT;
+      const int row = 32 * tp + (lane & 31);
+      uint32_t bits = 0;
+      for (int q = 0; q < 2; ++q) {
+        const int col = 32 * t + rho(8 * sstep + 2 * d + q, lane >> 5);
+        const __bf16 b = (__bf16)raw[(c1 ? R.Wc1 : R.We2) + row * H + col];
+        bits |= (uint32_t)__builtin_bit_cast(uint16_t, b) << (16 * q);
+      }
+      v = __builtin_bit_cast(float, bits);
+    }
     out[idx] = v;
+  }
+}
+
+// Power-of-two scales for the F16X3 fragments of edge_nn.2 / coord_nn.0:
+// 2^s with max|W| 2^s in (2^13, 2^14], so hi parts stay far below the fp16
+// maximum and lo parts of typical weights stay normal.  One block.
+__global__ void __launch_bounds__(256) egcl_scale_kernel(const float* __restrict__ raw, int H, int nf,
+                                                         float* __restrict__ out) {
+  const EgclLayout L = egcl_layout(H, nf);
+  const RawEgcl R = raw_egcl(H, nf);
+  __shared__ float red[2][256];
+  float m0 = 0.f, m1 = 0.f;
+  for (int i = threadIdx.x; i < H * H; i += 256) {
+    m0 = fmaxf(m0, fabsf(raw[R.We2 + i]));
+    m1 = fmaxf(m1, fabsf(raw[R.Wc1 + i]));
+  }
+  red[0][threadIdx.x] = m0;
+  red[1][threadIdx.x] = m1;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + off]);
+      red[1][threadIdx.x] = fmaxf(red[1][threadIdx.x], red[1][threadIdx.x + off]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 2) {
+    const float mx = red[threadIdx.x][0];
+    int ex = 0;
+    if (mx > 0.f && isfinite(mx)) {
+      frexpf(mx, &ex);              // mx = f 2^ex, f in [0.5, 1)
+      ex = 14 - ex;                 // mx 2^(14 - ex) in [2^13, 2^14)
+      ex = ex > 60 ? 60 : (ex < -60 ? -60 : ex);
+    }
+    out[L.scl + 2 * threadIdx.x] = ldexpf(1.f, ex);
+    out[L.scl + 2 * threadIdx.x + 1] = ldexpf(1.f, -ex);
   }
 }
 
@@ -107,7 +175,7 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
 // ---------------------------------------------------------------------------
 // the fused flow kernel (forward or reverse)
 // ---------------------------------------------------------------------------
-template <int H, int NMAX, bool REV>
+template <int H, int NMAX, bool REV, int PREC>
 __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(FlowArgs A) {
   __shared__ Smem<H, NMAX> sm;
   MolRef M;
@@ -160,7 +228,7 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
       atomicAdd(&A.stats[1], edges);
     }
     STAMP(3);
-    edge_tiles(sm, Lp, L, Ml, nf, tid_l STAMP_PASS);
+    edge_tiles<H, NMAX, PREC>(sm, Lp, L, Ml, nf, tid_l STAMP_PASS);
     STAMP(4);
     if (!(ENFLOW_ABLATE & 2)) node_phase(sm, Lp, L, n, nf, tid_l);
     STAMP(5);
@@ -406,6 +474,16 @@ static const double kLog2Pi = 1.8378770664093453;
     }                                                         \
   } while (0)
 
+template <int HH, int NN, bool REV>
+static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
+  if (prec == ENFLOW_PREC_F16X3)
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+  else if (prec == ENFLOW_PREC_BF16)
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+  else
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+}
+
 extern "C" {
 
 #ifdef ENFLOW_STAMPS
@@ -437,6 +515,7 @@ int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf) {
 int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {
   if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
   const int total = egcl_layout(H, nf).total;
+  hipLaunchKernelGGL(egcl_scale_kernel, dim3(1), dim3(256), 0, S(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -463,8 +542,9 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           int dequant_kind, const float* dequant, const float* noise,
                           float dequant_scale, float dt, float cw,
                           float* ldj_mol, float* ldj_total, int32_t* err_flag, uint64_t* pair_stats,
-                          float* tape, int32_t* pair_counts, void* stream) {
+                          float* tape, int32_t* pair_counts, int gemm_precision, void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (gemm_precision < ENFLOW_PREC_F32 || gemm_precision > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
@@ -473,7 +553,7 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
              dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
              reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
   if (num_mols > 0) {
-#define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
+#define CALL(HH, NN) launch_flow<HH, NN, false>(gemm_precision, num_mols, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
@@ -487,15 +567,17 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           float* h, float* g, float* pos, float* vel,
                           const float* layers, int n_layers,
                           int dequant_kind, float dt, float cw,
-                          int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, void* stream) {
+                          int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
+                          void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (gemm_precision < ENFLOW_PREC_F32 || gemm_precision > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
   (void)num_atoms;
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
              0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag, nullptr};
   if (num_mols > 0) {
-#define CALL(HH, NN) hipLaunchKernelGGL((lf_flow_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A)
+#define CALL(HH, NN) launch_flow<HH, NN, true>(gemm_precision, num_mols, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }

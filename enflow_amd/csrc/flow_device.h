@@ -38,8 +38,19 @@ __host__ __device__ constexpr int rho(int r, int hh) { return (r & 3) + 8 * (r >
 __host__ __device__ inline int node_ksteps(int H, int nf) { return (H + nf + 1) / 2; }
 
 struct EgclLayout {
-  int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, total;
+  int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, scl,
+      we2x, wc1x, we2b, wc1b, total;
 };
+
+// GEMM precision of the two H x H edge GEMMs (edge_nn.2, coord_nn.0), the
+// flow's dominant work (include/enflow_hip.h ENFLOW_PREC_*):
+//   PREC_F32   v_mfma_f32_32x32x2_f32 (exact fp32 FMA chain)
+//   PREC_F16X3 operands split x = hi + lo in fp16 (weights pre-scaled by a
+//              power of two so their lo parts stay normal), three products
+//              hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16, fp32
+//              accumulation: ~22-bit products at 16x the f32 MFMA rate / 3
+//   PREC_BF16  bf16 operands, one v_mfma_f32_32x32x16_bf16, fp32 accumulation
+enum { PREC_F32 = 0, PREC_F16X3 = 1, PREC_BF16 = 2 };
 
 // Packed EGCL layer (floats).  *f / wn1h / wn1a sections are MFMA A-fragments
 // (32x32x2 f32: lane l supplies A[l & 31][k = l >> 5]).  The layout does not
@@ -65,6 +76,12 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   L.wv2 = o; o += H;
   L.bn2 = o; o += NFMAX;
   L.bv2 = o; o += 4;
+  L.scl = o; o += 4;                       // 2^s, 2^-s of edge_nn.2 / coord_nn.0 (F16X3)
+  o = (o + 63) & ~63;
+  L.we2x = o; o += H * H;                  // [tp][t][s][lane][hi 8 x f16 | lo 8 x f16]
+  L.wc1x = o; o += H * H;
+  L.we2b = o; o += H * H / 2;              // [tp][t][s][lane][8 x bf16]
+  L.wc1b = o; o += H * H / 2;
   o = (o + 63) & ~63;
   L.total = o;
   return L;
@@ -345,6 +362,136 @@ __device__ __forceinline__ void chain_gemm(rsrc_t W, int off_floats, const f32x1
 #endif
 }
 
+// ---- split-precision chains (see PREC_*): same "weights = A, activations = B"
+// orientation, k-step s of feature tile t = registers 8s..8s+7 of X[t] (k order
+// rho-permuted, folded into the packed fragments).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma_f16(f32x4 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16 mfma_bf16(f32x4 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
+}
+__device__ __forceinline__ void split_f16(const f32x16& X, int s, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float x = X[8 * s + j];
+    const _Float16 h = (_Float16)x;
+    hi[j] = h;
+    lo[j] = (_Float16)(x - (float)h);
+  }
+}
+__device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
+  bf16x8 b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) b[j] = (__bf16)X[8 * s + j];
+  return b;
+}
+
+// acc[tp] += W[tp][t] X[t] in F16X3: 2NT k-steps of 12 MFMAs (NT = 4); the next
+// step's fragments and operand split are issued between this step's MFMAs, with
+// fill(2 step), fill(2 step + 1) (the fp32 chain's filler granularity).
+template <int NT, int FPM, class Fill>
+__device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
+                                              int lane, Fill&& fill) {
+  constexpr int S = 2 * NT;
+  f32x4 ch[NT], cl[NT], nh[NT], nl[NT];
+  const int vo = lane * 32;
+#pragma unroll
+  for (int tp = 0; tp < NT; ++tp) {
+    ch[tp] = bload4(W, vo, (off_floats + (tp * NT * 2) * 512) * 4);
+    cl[tp] = bload4(W, vo + 16, (off_floats + (tp * NT * 2) * 512) * 4);
+  }
+  f16x8 bh, bl;
+  split_f16(X[0], 0, bh, bl);
+#pragma unroll
+  for (int step = 0; step < S; ++step) {
+    if (step + 1 < S) {
+      const int t2 = (step + 1) >> 1, s2 = (step + 1) & 1;
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) {
+        nh[tp] = bload4(W, vo, (off_floats + ((tp * NT + t2) * 2 + s2) * 512) * 4);
+        nl[tp] = bload4(W, vo + 16, (off_floats + ((tp * NT + t2) * 2 + s2) * 512) * 4);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_f16(ch[tp], bh, acc[tp]);
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_f16(ch[tp], bl, acc[tp]);
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_f16(cl[tp], bh, acc[tp]);
+    fill(2 * step);
+    fill(2 * step + 1);
+    f16x8 nbh = bh, nbl = bl;
+    if (step + 1 < S) split_f16(X[(step + 1) >> 1], (step + 1) & 1, nbh, nbl);
+#pragma unroll
+    for (int k = 0; k < 3 * NT; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, FPM, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    bh = nbh;
+    bl = nbl;
+    if (step + 1 < S) {
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) {
+        ch[tp] = nh[tp];
+        cl[tp] = nl[tp];
+      }
+    }
+  }
+}
+
+// acc[tp] += W[tp][t] X[t] in BF16: 2NT k-steps of NT MFMAs.
+template <int NT, int FPM, class Fill>
+__device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
+                                               int lane, Fill&& fill) {
+  constexpr int S = 2 * NT;
+  f32x4 cb[NT], nb[NT];
+  const int vo = lane * 16;
+#pragma unroll
+  for (int tp = 0; tp < NT; ++tp) cb[tp] = bload4(W, vo, (off_floats + (tp * NT * 2) * 256) * 4);
+  bf16x8 b = to_bf16(X[0], 0);
+#pragma unroll
+  for (int step = 0; step < S; ++step) {
+    if (step + 1 < S) {
+      const int t2 = (step + 1) >> 1, s2 = (step + 1) & 1;
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) nb[tp] = bload4(W, vo, (off_floats + ((tp * NT + t2) * 2 + s2) * 256) * 4);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_bf16(cb[tp], b, acc[tp]);
+    fill(2 * step);
+    fill(2 * step + 1);
+    bf16x8 n2 = b;
+    if (step + 1 < S) n2 = to_bf16(X[(step + 1) >> 1], (step + 1) & 1);
+#pragma unroll
+    for (int k = 0; k < NT; ++k) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, 4 * FPM, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    b = n2;
+    if (step + 1 < S) {
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp) cb[tp] = nb[tp];
+    }
+  }
+}
+
+// GEMM with the precision's chain; off_* are the packed sections of the matrix
+template <int PREC, int NT, int FPM, class Fill>
+__device__ __forceinline__ void chain_prec_fill(rsrc_t W, int off_f32, int off_x3, int off_b16, const f32x16 (&X)[NT],
+                                                f32x16 (&acc)[NT], int lane, Fill&& fill) {
+  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM>(W, off_x3, X, acc, lane, fill);
+  else if constexpr (PREC == PREC_BF16) chain_b16_fill<NT, FPM>(W, off_b16, X, acc, lane, fill);
+  else chain_gemm_fill<NT, FPM>(W, off_f32, X, acc, lane, fill);
+}
+
 // X[t][r] = silu(X[t][r] + bias[32 t + rho(r, hh)]); bias read from LDS as float4
 template <int NT>
 __device__ __forceinline__ void bias_silu(f32x16 (&X)[NT], const float* __restrict__ bias, int hh) {
@@ -525,7 +672,7 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, 
 // ---------------------------------------------------------------------------
 // EGCL edge part: per-pair MLP chain on MFMA + deterministic segment sums
 // ---------------------------------------------------------------------------
-template <int H, int NMAX>
+template <int H, int NMAX, int PREC = PREC_F32>
 __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                            const MolRef& M, int nf, int tid STAMP_ARGS) {
   constexpr int NT = H / 32;
@@ -565,6 +712,9 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
   const int nh = (nf + 1) >> 1;
   const rsrc_t W = weights_rsrc(Lp, L.total);
   const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
+  // F16X3 accumulators carry the weight scale 2^s: unscale exactly in the bias fma
+  const float inv1 = PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f;
+  const float inv2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
 
   STAMP(8);
   for (int tile = t0; tile < t1; ++tile) {
@@ -627,7 +777,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
     f32x16 e[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) e[t] = (f32x16)0.f;
-    chain_gemm_fill<NT, 2>(W, L.we2f, x0, e, lane, [&](int step) {
+    chain_prec_fill<PREC, NT, 2>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 32 * t + 8 * g4 + 4 * hh);
@@ -640,7 +790,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 8 * g4 + 4 * hh);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = silu_f(e[0][4 * g4 + u] + b[u]);
+      for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = silu_f(fmaf(e[0][4 * g4 + u], inv1, b[u]));
     }
     STAMP(12);
     STAMP(13);
@@ -660,7 +810,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
       for (int t = 0; t < NT; ++t) hc[t] = e[t];
       if (0)
 #endif
-      chain_gemm_fill<NT, 6>(W, L.wc1f, e, hc, lane, [&](int step) {
+      chain_prec_fill<PREC, NT, 6>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
         const int t = step >> 2, g4 = step & 3;
 #if !(ENFLOW_ABLATE & 4)
         float v[4];
@@ -672,7 +822,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
         if (t + 1 < NT) {
           const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * (t + 1) + 8 * g4 + 4 * hh);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = silu_f(e[t + 1][4 * g4 + u] + b[u]);
+          for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = silu_f(fmaf(e[t + 1][4 * g4 + u], inv1, b[u]));
         }
       });
       // coord_nn.2 as a per-pair dot
@@ -683,7 +833,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
           const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 2 * H + 32 * tp + 8 * g4 + 4 * hh);
           const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * tp + 8 * g4 + 4 * hh);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(hc[tp][4 * g4 + u] + b[u]);
+          for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(hc[tp][4 * g4 + u], inv2, b[u]));
         }
     }
     const float phi = part + __shfl_xor(part, 32, 64);

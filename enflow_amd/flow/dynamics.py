@@ -24,6 +24,18 @@ from .base import BaseFlow
 
 
 class LFIntegrator(BaseFlow):
+    """``gemm_precision`` selects how the two H x H edge GEMMs run on the
+    matrix cores: "f32" (exact fp32 MFMA), "f16x3" (fp32 operands split into
+    fp16 hi+lo, three products, fp32 accumulation; default) or "bf16"
+    (reduced-precision generate path, BASELINE configs[2])."""
+    gemm_precision = "f16x3"
+
+    def _prec(self):
+        try:
+            return _lib.PRECISIONS[self.gemm_precision]
+        except KeyError:
+            raise ValueError(f"gemm_precision must be one of {sorted(_lib.PRECISIONS)}") from None
+
     def make_networks(self, network):
         return [network for _ in range(self.n_iter)]
 
@@ -114,7 +126,7 @@ class LFIntegrator(BaseFlow):
             _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
             _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
             _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
-            _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts),
+            _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), self._prec(),
             _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
 
     def _state(self, data):
@@ -176,7 +188,8 @@ class LFIntegrator(BaseFlow):
             s["mol_ptr"].numel() - 1, n, s["max_n"], nf, hid, _lib.ptr(s["mol_ptr"]), _lib.ptr(s["r_cut"]),
             _lib.ptr(s["box"]), _lib.ptr(s["h"]), _lib.ptr(s["g"]), _lib.ptr(s["pos"]), _lib.ptr(s["vel"]),
             _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, float(self.dt), cw,
-            _lib.ptr(idx), _lib.ptr(mx), _lib.ptr(err), _lib.stream_ptr(dev)), "enflow_lf_reverse_f32")
+            _lib.ptr(idx), _lib.ptr(mx), _lib.ptr(err), self._prec(), _lib.stream_ptr(dev)),
+            "enflow_lf_reverse_f32")
         if check_errors:
             _lib.raise_on_err(err)
         dt = data.h.dtype

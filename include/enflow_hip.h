@@ -36,6 +36,12 @@ extern "C" {
 #define ENFLOW_ERR_FEW_IMAGES       2  /* reference would IndexError (base.py:137) */
 #define ENFLOW_ERR_TOO_MANY_FEATURES 4
 
+/* Precision of the flow's two H x H edge GEMMs (edge_nn.2, coord_nn.0); all
+ * other arithmetic is fp32 in every mode.  See DESIGN.md for the error model. */
+#define ENFLOW_PREC_F32   0  /* v_mfma_f32_32x32x2_f32: exact fp32 FMA chain          */
+#define ENFLOW_PREC_F16X3 1  /* fp32 operands split hi+lo in fp16, 3 products, fp32 acc */
+#define ENFLOW_PREC_BF16  2  /* bf16 operands, fp32 accumulation                       */
+
 #define ENFLOW_DEQUANT_NONE   0
 #define ENFLOW_DEQUANT_ARGMAX 1  /* enflow/nn/argmax.py */
 #define ENFLOW_DEQUANT_FLOOR  2  /* enflow/nn/floor.py  */
@@ -94,6 +100,7 @@ int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,
  *                        state, message sums and Q, read by enflow_lf_backward_f32
  *   pair_counts        : [n_layers][num_mols] unique pairs per layer (required
  *                        with tape)
+ *   gemm_precision     : ENFLOW_PREC_* (edge_nn.2 / coord_nn.0 GEMMs)
  */
 int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
                           const int32_t* mol_ptr, const float* r_cut, const float* box,
@@ -102,7 +109,8 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
                           int dequant_kind, const float* dequant, const float* noise,
                           float dequant_scale, float dt, float coords_weight,
                           float* ldj_mol, float* ldj_total, int32_t* err_flag,
-                          uint64_t* pair_stats, float* tape, int32_t* pair_counts, void* stream);
+                          uint64_t* pair_stats, float* tape, int32_t* pair_counts,
+                          int gemm_precision, void* stream);
 
 /*
  * LFIntegrator.reverse (enflow/flow/dynamics.py:26-37), all layers fused.
@@ -118,7 +126,7 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
                           const float* layers, int n_layers,
                           int dequant_kind, float dt, float coords_weight,
                           int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
-                          void* stream);
+                          int gemm_precision, void* stream);
 
 /* helpers.one_hot (enflow/utils/helpers.py:43-52): out[num_atoms][width]. */
 int enflow_one_hot_f32(const int32_t* idx, int num_atoms, int width, float* out,

@@ -78,11 +78,17 @@ def test_argmax_matches_reference():
 # ---------------------------------------------------------------------------
 # fused flow
 # ---------------------------------------------------------------------------
+PRECS = ["f32", "f16x3"]     # both meet the fp32 bar; bf16 has its own test below
+BF16_TOL = 1e-3              # configs[2] (bf16 generate path), normwise; measured <= 1.3e-5
+
+
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
-def test_lf_forward_matches_reference(name):
+def test_lf_forward_matches_reference(name, prec):
     from enflow_amd.flow import Alchemical_NLL
     inp, out = load(name)
     model, d = flow_from_fixture(inp, DEV)
+    model.gemm_precision = prec
     with torch.no_grad():
         o, ldj = model(d, noise=torch.tensor(inp["eps"], device=DEV))
     for k in ("h", "g", "pos", "vel"):
@@ -92,11 +98,13 @@ def test_lf_forward_matches_reference(name):
     assert abs(float(nll) - float(out["nll"])) <= TOL * abs(float(out["nll"]))
 
 
+@pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
-def test_lf_reverse_matches_reference(name):
+def test_lf_reverse_matches_reference(name, prec):
     """generate direction: reverse of the reference's forward output."""
     inp, out = load(name)
     model, _ = flow_from_fixture(inp, DEV)
+    model.gemm_precision = prec
     d = data_from_fixture(inp, DEV)
     for k in ("h", "g", "pos", "vel"):
         setattr(d, k, torch.tensor(out[k], dtype=torch.float32, device=DEV))
@@ -105,6 +113,30 @@ def test_lf_reverse_matches_reference(name):
     np.testing.assert_array_equal(back.h.cpu().numpy(), out["rev_h"])
     for k in ("g", "pos", "vel"):
         assert rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) < 1e-4, k
+
+
+@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
+def test_lf_bf16_generate_and_forward(name):
+    """configs[2]: the generate (reverse) path with bf16 edge GEMMs.  The
+    one-hot h must come back exactly; continuous outputs within BF16_TOL."""
+    inp, out = load(name)
+    model, _ = flow_from_fixture(inp, DEV)
+    model.gemm_precision = "bf16"
+    d = data_from_fixture(inp, DEV)
+    for k in ("h", "g", "pos", "vel"):
+        setattr(d, k, torch.tensor(out[k], dtype=torch.float32, device=DEV))
+    with torch.no_grad():
+        back = model.reverse(d)
+    np.testing.assert_array_equal(back.h.cpu().numpy(), out["rev_h"])
+    errs = {k: rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) for k in ("g", "pos", "vel")}
+    model2, d2 = flow_from_fixture(inp, DEV)
+    model2.gemm_precision = "bf16"
+    with torch.no_grad():
+        o, ldj = model2(d2, noise=torch.tensor(inp["eps"], device=DEV))
+    errs.update({"fwd_" + k: rel_err(getattr(o, k).cpu().numpy(), out[k]) for k in ("h", "g", "pos", "vel")})
+    errs["fwd_ldj"] = abs(float(ldj) - float(out["ldj"])) / abs(float(out["ldj"]))
+    print(name, "bf16 errors", errs)
+    assert all(v < BF16_TOL for v in errs.values()), errs
 
 
 def _oracle_flow(model, batch, noise):

@@ -48,12 +48,15 @@ def test_abi_queries():
 def test_argument_errors_launch_nothing():
     L = _lib.lib()
     # too-large molecule, bad hidden width, bad nf: rejected before any launch
-    args = [1, 100, 100, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 7
+    args = [1, 100, 100, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 6 + [1, None]
     assert L.enflow_lf_forward_f32(*args) == -3
     args[2], args[4] = 20, 96
     assert L.enflow_lf_forward_f32(*args) == -5
     args[3], args[4] = 9, 128
     assert L.enflow_lf_forward_f32(*args) == -4
+    args[3] = 5
+    args[-2] = 7    # unknown GEMM precision
+    assert L.enflow_lf_forward_f32(*args) == -1
 
 
 def test_backward_sizes_and_argument_errors():
