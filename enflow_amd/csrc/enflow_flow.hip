@@ -87,8 +87,22 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
     else if (idx < L.bn2) v = raw[R.Wv2 + idx - L.wv2];
     else if (idx < L.bv2) { int e = idx - L.bn2; if (e < nf) v = raw[R.bn2 + e]; }
     else if (idx < L.scl) { if (idx == L.bv2) v = raw[R.bv2]; }
-    else if (idx < L.scl + 4) continue;      // written by egcl_scale_kernel
-    else if (idx >= L.we2x && idx < L.we2b) {  // F16X3 fragments: [tp][t][s][lane][hi 8 | lo 8] f16
+    else if (idx < L.scl + 8) continue;      // written by egcl_scale_kernel
+    else if (idx >= L.we1x && idx < L.we2x) {  // F16X3 edge_nn.0: [t][ks][lane][hi 8 | lo 8], A[m][k]
+      const int e = idx - L.we1x;
+      const int d = e & 7, lane = (e >> 3) & 63, ks = (e >> 9) & 1, t = e >> 10;
+      const float sc = out[L.scl + 4];
+      const int row = 32 * t + (lane & 31);
+      uint32_t bits = 0;
+      for (int q = 0; q < 2; ++q) {
+        const int k = 16 * ks + 8 * (lane >> 5) + 2 * (d & 3) + q;
+        const float w = k < K1 ? raw[R.We1 + row * K1 + k] * sc : 0.f;
+        const _Float16 hi = (_Float16)w;
+        const _Float16 part = d < 4 ? hi : (_Float16)(w - (float)hi);
+        bits |= (uint32_t)__builtin_bit_cast(uint16_t, part) << (16 * q);
+      }
+      v = __builtin_bit_cast(float, bits);
+    } else if (idx >= L.we2x && idx < L.we2b) {  // F16X3 fragments: [tp][t][s][lane][hi 8 | lo 8] f16
       const bool c1 = idx >= L.wc1x;
       const int e = idx - (c1 ? L.wc1x : L.we2x);
       const int d = e & 7, lane = (e >> 3) & 63, rest = e >> 9;
@@ -123,30 +137,30 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
   }
 }
 
-// Power-of-two scales for the F16X3 fragments of edge_nn.2 / coord_nn.0:
+// Power-of-two scales for the F16X3 fragments of edge_nn.2 / coord_nn.0 / edge_nn.0:
 // 2^s with max|W| 2^s in (2^13, 2^14], so hi parts stay far below the fp16
 // maximum and lo parts of typical weights stay normal.  One block.
 __global__ void __launch_bounds__(256) egcl_scale_kernel(const float* __restrict__ raw, int H, int nf,
                                                          float* __restrict__ out) {
   const EgclLayout L = egcl_layout(H, nf);
   const RawEgcl R = raw_egcl(H, nf);
-  __shared__ float red[2][256];
-  float m0 = 0.f, m1 = 0.f;
+  __shared__ float red[3][256];
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f;
   for (int i = threadIdx.x; i < H * H; i += 256) {
     m0 = fmaxf(m0, fabsf(raw[R.We2 + i]));
     m1 = fmaxf(m1, fabsf(raw[R.Wc1 + i]));
   }
+  for (int i = threadIdx.x; i < H * (2 * nf + 1); i += 256) m2 = fmaxf(m2, fabsf(raw[R.We1 + i]));
   red[0][threadIdx.x] = m0;
   red[1][threadIdx.x] = m1;
+  red[2][threadIdx.x] = m2;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) {
-      red[0][threadIdx.x] = fmaxf(red[0][threadIdx.x], red[0][threadIdx.x + off]);
-      red[1][threadIdx.x] = fmaxf(red[1][threadIdx.x], red[1][threadIdx.x + off]);
-    }
+    if (threadIdx.x < off)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + off]);
     __syncthreads();
   }
-  if (threadIdx.x < 2) {
+  if (threadIdx.x < 3) {
     const float mx = red[threadIdx.x][0];
     int ex = 0;
     if (mx > 0.f && isfinite(mx)) {
@@ -293,6 +307,7 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
         for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] = floorf(sm.h[a * NFP + q]);
       }
     }
+    __syncthreads();   // the write-back below maps threads to elements differently
   }
   // write back
   for (int e = tid; e < n * 3; e += BLOCK) {

@@ -39,7 +39,7 @@ __host__ __device__ inline int node_ksteps(int H, int nf) { return (H + nf + 1) 
 
 struct EgclLayout {
   int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, scl,
-      we2x, wc1x, we2b, wc1b, total;
+      we1x, we2x, wc1x, we2b, wc1b, total;
 };
 
 // GEMM precision of the two H x H edge GEMMs (edge_nn.2, coord_nn.0), the
@@ -76,8 +76,9 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   L.wv2 = o; o += H;
   L.bn2 = o; o += NFMAX;
   L.bv2 = o; o += 4;
-  L.scl = o; o += 4;                       // 2^s, 2^-s of edge_nn.2 / coord_nn.0 (F16X3)
+  L.scl = o; o += 8;                       // 2^s, 2^-s of edge_nn.2, coord_nn.0, edge_nn.0 (F16X3)
   o = (o + 63) & ~63;
+  L.we1x = o; o += NT * 2 * 512;           // [t][ks][lane][hi 8 | lo 8] f16, k = raw column of edge_nn.0
   L.we2x = o; o += H * H;                  // [tp][t][s][lane][hi 8 x f16 | lo 8 x f16]
   L.wc1x = o; o += H * H;
   L.we2b = o; o += H * H / 2;              // [tp][t][s][lane][8 x bf16]
@@ -390,45 +391,58 @@ __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
   return b;
 }
 
-// acc[tp] += W[tp][t] X[t] in F16X3: 2NT k-steps of 12 MFMAs (NT = 4); the next
-// step's fragments and operand split are issued between this step's MFMAs, with
-// fill(2 step), fill(2 step + 1) (the fp32 chain's filler granularity).
+// acc[tp] += W[tp][t] X[t] in F16X3.  A step is one k-slice (t, s) x one group
+// of TPG output tiles (3 TPG MFMAs), so only TPG tiles' hi/lo fragments (and
+// their prefetch) are live; the operand split of the next k-slice and the
+// filler calls (4 NT per GEMM, the fp32 chain's granularity) are interleaved
+// between the MFMAs.
 template <int NT, int FPM, class Fill>
 __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
                                               int lane, Fill&& fill) {
-  constexpr int S = 2 * NT;
-  f32x4 ch[NT], cl[NT], nh[NT], nl[NT];
+  constexpr int TPG = NT >= 2 ? 2 : 1;
+  constexpr int NGR = NT / TPG;
+  constexpr int S = NT * 2 * NGR;
+  constexpr int FPS = (4 * NT) / S;
+  f32x4 ch[TPG], cl[TPG], nh[TPG], nl[TPG];
   const int vo = lane * 32;
+  auto foff = [&](int step, int q) {
+    const int gi = step % NGR, ts = step / NGR;
+    const int tp = gi * TPG + q;
+    return (off_floats + ((tp * NT + (ts >> 1)) * 2 + (ts & 1)) * 512) * 4;
+  };
 #pragma unroll
-  for (int tp = 0; tp < NT; ++tp) {
-    ch[tp] = bload4(W, vo, (off_floats + (tp * NT * 2) * 512) * 4);
-    cl[tp] = bload4(W, vo + 16, (off_floats + (tp * NT * 2) * 512) * 4);
+  for (int q = 0; q < TPG; ++q) {
+    ch[q] = bload4(W, vo, foff(0, q));
+    cl[q] = bload4(W, vo + 16, foff(0, q));
   }
   f16x8 bh, bl;
   split_f16(X[0], 0, bh, bl);
 #pragma unroll
   for (int step = 0; step < S; ++step) {
+    const int gi = step % NGR;
     if (step + 1 < S) {
-      const int t2 = (step + 1) >> 1, s2 = (step + 1) & 1;
 #pragma unroll
-      for (int tp = 0; tp < NT; ++tp) {
-        nh[tp] = bload4(W, vo, (off_floats + ((tp * NT + t2) * 2 + s2) * 512) * 4);
-        nl[tp] = bload4(W, vo + 16, (off_floats + ((tp * NT + t2) * 2 + s2) * 512) * 4);
+      for (int q = 0; q < TPG; ++q) {
+        nh[q] = bload4(W, vo, foff(step + 1, q));
+        nl[q] = bload4(W, vo + 16, foff(step + 1, q));
       }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_f16(ch[tp], bh, acc[tp]);
+    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(ch[q], bh, acc[gi * TPG + q]);
 #pragma unroll
-    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_f16(ch[tp], bl, acc[tp]);
+    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(ch[q], bl, acc[gi * TPG + q]);
 #pragma unroll
-    for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_f16(cl[tp], bh, acc[tp]);
-    fill(2 * step);
-    fill(2 * step + 1);
+    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(cl[q], bh, acc[gi * TPG + q]);
+#pragma unroll
+    for (int f = 0; f < FPS; ++f) fill(step * FPS + f);
     f16x8 nbh = bh, nbl = bl;
-    if (step + 1 < S) split_f16(X[(step + 1) >> 1], (step + 1) & 1, nbh, nbl);
+    if (step + 1 < S && (step + 1) % NGR == 0) {
+      const int ts = (step + 1) / NGR;
+      split_f16(X[ts >> 1], ts & 1, nbh, nbl);
+    }
 #pragma unroll
-    for (int k = 0; k < 3 * NT; ++k) {
+    for (int k = 0; k < 3 * TPG; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, FPM, 0);
     }
@@ -437,9 +451,9 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
     bl = nbl;
     if (step + 1 < S) {
 #pragma unroll
-      for (int tp = 0; tp < NT; ++tp) {
-        ch[tp] = nh[tp];
-        cl[tp] = nl[tp];
+      for (int q = 0; q < TPG; ++q) {
+        ch[q] = nh[q];
+        cl[q] = nl[q];
       }
     }
   }
@@ -741,7 +755,35 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
     f32x16 x0[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
-    {
+    if constexpr (PREC == PREC_F16X3) {
+      // k = raw column of edge_nn.0: [h_i (nf), h_j (nf), radial], 16 per k-step
+      const int ks_n = (2 * nf + 1 + 15) >> 4;
+      for (int ks = 0; ks < ks_n; ++ks) {
+        f32x16 in;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int k = 16 * ks + 8 * hh + jj;
+          float v = 0.f;
+          if (k < nf) v = sm.h[i * NFP + k];
+          else if (k < 2 * nf) v = sm.h[jl * NFP + k - nf];
+          else if (k == 2 * nf) v = radial;
+          in[jj] = v;
+        }
+        f16x8 bh, bl;
+        split_f16(in, 0, bh, bl);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int so = (L.we1x + (t * 2 + ks) * 512) * 4;
+          const f32x4 ah = bload4(W, lane * 32, so), al = bload4(W, lane * 32 + 16, so);
+          x0[t] = mfma_f16(ah, bh, x0[t]);
+          x0[t] = mfma_f16(ah, bl, x0[t]);
+          x0[t] = mfma_f16(al, bh, x0[t]);
+        }
+      }
+      const float inv0 = Lp[L.scl + 5];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) x0[t] *= inv0;
+    } else {
       float cur[NT], nxt[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) cur[t] = bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1)) * 64) * 4);

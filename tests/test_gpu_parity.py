@@ -198,7 +198,11 @@ def test_floor_dequant_vs_oracle():
         back = model.reverse(o)
     # floor(h + u) after an fp32 round trip: an element whose pre-floor value
     # lands a hair under an integer legitimately floors down
-    assert (back.h.cpu().numpy() == np.floor(b["h"])).mean() > 0.99
+    got, want = back.h.cpu().numpy(), np.floor(b["h"])
+    bad = np.argwhere(got != want)
+    info = [(tuple(ix), float(got[tuple(ix)]), float(want[tuple(ix)]), float(u[tuple(ix)]),
+             float(o.h[tuple(ix)])) for ix in bad[:8]]
+    assert (got == want).mean() > 0.99, (len(bad), info)
 
 
 def test_too_large_molecule_raises():

@@ -19,7 +19,8 @@ def main():
     if not os.path.exists(SO):
         subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
                         "-DENFLOW_STAMPS", "-I", os.path.join(ROOT, "include"), "-o", SO,
-                        os.path.join(ROOT, "enflow_amd", "csrc", "enflow_flow.hip")], check=True)
+                        os.path.join(ROOT, "enflow_amd", "csrc", "enflow_flow.hip"),
+                        os.path.join(ROOT, "enflow_amd", "csrc", "enflow_backward.hip")], check=True)
     os.environ["ENFLOW_LIB"] = SO
     sys.path.insert(0, ROOT)
     import torch
