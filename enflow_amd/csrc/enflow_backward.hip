@@ -62,7 +62,7 @@ __global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int n
   }
 }
 
-__device__ __forceinline__ float sigmoid_f(float x) { return __frcp_rn(1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------
 // per-layer backward

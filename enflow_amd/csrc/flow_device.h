@@ -185,7 +185,7 @@ __device__ __forceinline__ float silu_f(float x) {
 #if ENFLOW_ABLATE & 8
   return x;
 #else
-  return x * __frcp_rn(1.0f + __expf(-x));
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));   // v_rcp_f32 (1 ulp), not an IEEE divide
 #endif
 }
 
