@@ -87,8 +87,8 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
     else if (idx < L.bn2) v = raw[R.Wv2 + idx - L.wv2];
     else if (idx < L.bv2) { int e = idx - L.bn2; if (e < nf) v = raw[R.bn2 + e]; }
     else if (idx < L.scl) { if (idx == L.bv2) v = raw[R.bv2]; }
-    else if (idx < L.scl + 8) continue;      // written by egcl_scale_kernel
-    else if (idx >= L.we1x && idx < L.we2x) {  // F16X3 edge_nn.0: [t][ks][lane][hi 8 | lo 8], A[m][k]
+    else if (idx < L.scl + 16) continue;     // written by egcl_scale_kernel
+    else if (idx >= L.we1x && idx < L.wv1x) {  // F16X3 edge_nn.0: [t][ks][lane][hi 8 | lo 8], A[m][k]
       const int e = idx - L.we1x;
       const int d = e & 7, lane = (e >> 3) & 63, ks = (e >> 9) & 1, t = e >> 10;
       const float sc = out[L.scl + 4];
@@ -97,6 +97,40 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
       for (int q = 0; q < 2; ++q) {
         const int k = 16 * ks + 8 * (lane >> 5) + 2 * (d & 3) + q;
         const float w = k < K1 ? raw[R.We1 + row * K1 + k] * sc : 0.f;
+        const _Float16 hi = (_Float16)w;
+        const _Float16 part = d < 4 ? hi : (_Float16)(w - (float)hi);
+        bits |= (uint32_t)__builtin_bit_cast(uint16_t, part) << (16 * q);
+      }
+      v = __builtin_bit_cast(float, bits);
+    } else if (idx >= L.wv1x && idx < L.we2x) {  // F16X3 node fragments: [..][lane][hi 8 | lo 8]
+      int e, sidx;
+      if (idx < L.wn1hx) { e = idx - L.wv1x; sidx = 0; }
+      else if (idx < L.wn1ax) { e = idx - L.wn1hx; sidx = 1; }
+      else if (idx < L.wn2x) { e = idx - L.wn1ax; sidx = 2; }
+      else { e = idx - L.wn2x; sidx = 3; }
+      const int d = e & 7, lane = (e >> 3) & 63, blk = e >> 9;
+      const int m = lane & 31, kh = lane >> 5;
+      const float sc = out[L.scl + (sidx == 0 ? 6 : (sidx == 3 ? 10 : 8))];
+      uint32_t bits = 0;
+      for (int q = 0; q < 2; ++q) {
+        const int jj = 2 * (d & 3) + q;
+        float w = 0.f;
+        if (sidx == 0) {                 // vel_scaling_nn.0 [H][nf], blk = tp
+          const int k = 8 * kh + jj;
+          if (k < nf) w = raw[R.Wv1 + (32 * blk + m) * nf + k];
+        } else if (sidx == 1) {          // node_nn.0 h part, blk = tp
+          const int k = 8 * kh + jj;
+          if (k < nf) w = raw[R.Wn1 + (32 * blk + m) * (H + nf) + k];
+        } else if (sidx == 2) {          // node_nn.0 agg part, blk = tp * (H / 16) + ks
+          const int tp = blk / (H / 16), ks = blk % (H / 16);
+          const int k = 16 * ks + 8 * kh + jj;
+          w = raw[R.Wn1 + (32 * tp + m) * (H + nf) + nf + k];
+        } else {                         // node_nn.2 [nf][H], blk = tp * 2 + s
+          const int tp = blk >> 1, s2 = blk & 1;
+          const int k = 32 * tp + rho(8 * s2 + jj, kh);
+          if (m < nf) w = raw[R.Wn2 + m * H + k];
+        }
+        w *= sc;
         const _Float16 hi = (_Float16)w;
         const _Float16 part = d < 4 ? hi : (_Float16)(w - (float)hi);
         bits |= (uint32_t)__builtin_bit_cast(uint16_t, part) << (16 * q);
@@ -137,30 +171,30 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
   }
 }
 
-// Power-of-two scales for the F16X3 fragments of edge_nn.2 / coord_nn.0 / edge_nn.0:
+// Power-of-two scales for the F16X3 fragments (edge_nn.2, coord_nn.0, edge_nn.0,
+// vel_scaling_nn.0, node_nn.0, node_nn.2):
 // 2^s with max|W| 2^s in (2^13, 2^14], so hi parts stay far below the fp16
 // maximum and lo parts of typical weights stay normal.  One block.
 __global__ void __launch_bounds__(256) egcl_scale_kernel(const float* __restrict__ raw, int H, int nf,
                                                          float* __restrict__ out) {
   const EgclLayout L = egcl_layout(H, nf);
   const RawEgcl R = raw_egcl(H, nf);
-  __shared__ float red[3][256];
-  float m0 = 0.f, m1 = 0.f, m2 = 0.f;
-  for (int i = threadIdx.x; i < H * H; i += 256) {
-    m0 = fmaxf(m0, fabsf(raw[R.We2 + i]));
-    m1 = fmaxf(m1, fabsf(raw[R.Wc1 + i]));
+  // matrices (in scl slot order): edge_nn.2, coord_nn.0, edge_nn.0, vel_scaling_nn.0, node_nn.0, node_nn.2
+  const int off[6] = {R.We2, R.Wc1, R.We1, R.Wv1, R.Wn1, R.Wn2};
+  const int cnt[6] = {H * H, H * H, H * (2 * nf + 1), H * nf, H * (H + nf), nf * H};
+  __shared__ float red[6][256];
+  for (int k = 0; k < 6; ++k) {
+    float mx = 0.f;
+    for (int i = threadIdx.x; i < cnt[k]; i += 256) mx = fmaxf(mx, fabsf(raw[off[k] + i]));
+    red[k][threadIdx.x] = mx;
   }
-  for (int i = threadIdx.x; i < H * (2 * nf + 1); i += 256) m2 = fmaxf(m2, fabsf(raw[R.We1 + i]));
-  red[0][threadIdx.x] = m0;
-  red[1][threadIdx.x] = m1;
-  red[2][threadIdx.x] = m2;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off)
-      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + off]);
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x < 3) {
+  if (threadIdx.x < 6) {
     const float mx = red[threadIdx.x][0];
     int ex = 0;
     if (mx > 0.f && isfinite(mx)) {
@@ -244,7 +278,10 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
     STAMP(3);
     edge_tiles<H, NMAX, PREC>(sm, Lp, L, Ml, nf, tid_l STAMP_PASS);
     STAMP(4);
-    if (!(ENFLOW_ABLATE & 2)) node_phase(sm, Lp, L, n, nf, tid_l);
+    if (!(ENFLOW_ABLATE & 2)) {
+      if constexpr (PREC == PREC_F16X3) node_phase_x3(sm, Lp, L, n, nf, tid_l);
+      else node_phase(sm, Lp, L, n, nf, tid_l);
+    }
     STAMP(5);
     if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q
       const TapeLayout T = tape_layout(A.num_atoms, nf, H, A.n_layers);

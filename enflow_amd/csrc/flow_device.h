@@ -39,7 +39,7 @@ __host__ __device__ inline int node_ksteps(int H, int nf) { return (H + nf + 1) 
 
 struct EgclLayout {
   int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, scl,
-      we1x, we2x, wc1x, we2b, wc1b, total;
+      we1x, wv1x, wn1hx, wn1ax, wn2x, we2x, wc1x, we2b, wc1b, total;
 };
 
 // GEMM precision of the two H x H edge GEMMs (edge_nn.2, coord_nn.0), the
@@ -76,9 +76,14 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   L.wv2 = o; o += H;
   L.bn2 = o; o += NFMAX;
   L.bv2 = o; o += 4;
-  L.scl = o; o += 8;                       // 2^s, 2^-s of edge_nn.2, coord_nn.0, edge_nn.0 (F16X3)
+  L.scl = o; o += 16;                      // (2^s, 2^-s) of edge_nn.2, coord_nn.0, edge_nn.0,
+                                           // vel_scaling_nn.0, node_nn.0, node_nn.2 (F16X3)
   o = (o + 63) & ~63;
   L.we1x = o; o += NT * 2 * 512;           // [t][ks][lane][hi 8 | lo 8] f16, k = raw column of edge_nn.0
+  L.wv1x = o; o += NT * 512;               // [tp][lane][hi|lo]: vel_scaling_nn.0, k = h feature
+  L.wn1hx = o; o += NT * 512;              // [tp][lane][hi|lo]: node_nn.0 h part
+  L.wn1ax = o; o += NT * (H / 16) * 512;   // [tp][ks][lane][hi|lo]: node_nn.0 agg part, k = 16 ks + 8 kh + j
+  L.wn2x = o; o += NT * 2 * 512;           // [tp][s][lane][hi|lo]: node_nn.2, A[q][32 tp + rho(8 s + j, kh)]
   L.we2x = o; o += H * H;                  // [tp][t][s][lane][hi 8 x f16 | lo 8 x f16]
   L.wc1x = o; o += H * H;
   L.we2b = o; o += H * H / 2;              // [tp][t][s][lane][8 x bf16]
@@ -396,14 +401,22 @@ __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
 // their prefetch) are live; the operand split of the next k-slice and the
 // filler calls (4 NT per GEMM, the fp32 chain's granularity) are interleaved
 // between the MFMAs.
+#ifndef ENFLOW_X3_TPG
+#define ENFLOW_X3_TPG 2      // output tiles per step
+#endif
+#ifndef ENFLOW_X3_DEPTH
+#define ENFLOW_X3_DEPTH 2    // fragment ring depth (prefetch distance + 1 steps)
+#endif
 template <int NT, int FPM, class Fill>
 __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
                                               int lane, Fill&& fill) {
-  constexpr int TPG = NT >= 2 ? 2 : 1;
+  constexpr int TPG = NT >= ENFLOW_X3_TPG ? ENFLOW_X3_TPG : NT;
   constexpr int NGR = NT / TPG;
   constexpr int S = NT * 2 * NGR;
-  constexpr int FPS = (4 * NT) / S;
-  f32x4 ch[TPG], cl[TPG], nh[TPG], nl[TPG];
+  constexpr int FPS = (4 * NT) / S > 0 ? (4 * NT) / S : 1;
+  constexpr int FTOT = 4 * NT;
+  constexpr int D = ENFLOW_X3_DEPTH;
+  f32x4 rh[D][TPG], rl[D][TPG];
   const int vo = lane * 32;
   auto foff = [&](int step, int q) {
     const int gi = step % NGR, ts = step / NGR;
@@ -411,31 +424,38 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
     return (off_floats + ((tp * NT + (ts >> 1)) * 2 + (ts & 1)) * 512) * 4;
   };
 #pragma unroll
-  for (int q = 0; q < TPG; ++q) {
-    ch[q] = bload4(W, vo, foff(0, q));
-    cl[q] = bload4(W, vo + 16, foff(0, q));
-  }
+  for (int d = 0; d < D - 1; ++d)
+    if (d < S) {
+#pragma unroll
+      for (int q = 0; q < TPG; ++q) {
+        rh[d][q] = bload4(W, vo, foff(d, q));
+        rl[d][q] = bload4(W, vo + 16, foff(d, q));
+      }
+    }
   f16x8 bh, bl;
   split_f16(X[0], 0, bh, bl);
 #pragma unroll
   for (int step = 0; step < S; ++step) {
     const int gi = step % NGR;
-    if (step + 1 < S) {
+    const int cur = step % D;
+    if (step + D - 1 < S) {
+      const int sl = (step + D - 1) % D;
 #pragma unroll
       for (int q = 0; q < TPG; ++q) {
-        nh[q] = bload4(W, vo, foff(step + 1, q));
-        nl[q] = bload4(W, vo + 16, foff(step + 1, q));
+        rh[sl][q] = bload4(W, vo, foff(step + D - 1, q));
+        rl[sl][q] = bload4(W, vo + 16, foff(step + D - 1, q));
       }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(ch[q], bh, acc[gi * TPG + q]);
+    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(rh[cur][q], bh, acc[gi * TPG + q]);
 #pragma unroll
-    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(ch[q], bl, acc[gi * TPG + q]);
+    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(rh[cur][q], bl, acc[gi * TPG + q]);
 #pragma unroll
-    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(cl[q], bh, acc[gi * TPG + q]);
+    for (int q = 0; q < TPG; ++q) acc[gi * TPG + q] = mfma_f16(rl[cur][q], bh, acc[gi * TPG + q]);
 #pragma unroll
-    for (int f = 0; f < FPS; ++f) fill(step * FPS + f);
+    for (int f = 0; f < FPS; ++f)
+      if (step * FPS + f < FTOT) fill(step * FPS + f);
     f16x8 nbh = bh, nbl = bl;
     if (step + 1 < S && (step + 1) % NGR == 0) {
       const int ts = (step + 1) / NGR;
@@ -449,13 +469,6 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
     __builtin_amdgcn_sched_barrier(0);
     bh = nbh;
     bl = nbl;
-    if (step + 1 < S) {
-#pragma unroll
-      for (int q = 0; q < TPG; ++q) {
-        ch[q] = nh[q];
-        cl[q] = nl[q];
-      }
-    }
   }
 }
 
@@ -974,6 +987,125 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX>& sm, const float* __res
       for (int r = 0; r < 4; ++r) {
         const int q = r + 4 * hh;
         if (q < nf) sm.u.nd.gp[tp][q][a] = gacc[r];
+      }
+    }
+  }
+  __syncthreads();
+  const float bv2 = Lp[L.bv2];
+  for (int a = tid; a < n; a += BLOCK) {
+    float s = 0.f;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.qp[tp][a];
+    sm.Q[a] = s + bv2;
+  }
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    float s = 0.f;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.gp[tp][q][a];
+    sm.G[a * NFP + q] = s + Lp[L.bn2 + q];
+  }
+  __syncthreads();
+}
+
+// F16X3 node phase: same items and outputs as node_phase, all products on
+// v_mfma_f32_32x32x16_f16 with hi/lo split operands (atoms on the pair lanes).
+template <int H, int NMAX>
+__device__ __forceinline__ void node_phase_x3(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
+                                              int n, int nf, int tid) {
+  constexpr int NT = H / 32;
+  constexpr int NA = NMAX / 32;
+  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int KS = H / 16;
+  const int lane = tid & 63, w = tid >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const rsrc_t W = weights_rsrc(Lp, L.total);
+  const float inv_v1 = Lp[L.scl + 7], inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
+  const int vo = lane * 32;
+  for (int item = w; item < NT * NA; item += WAVES) {
+    const int tp = item % NT, at = item / NT;
+    const int a = at * 32 + j;
+    const bool va = a < n;
+    const int ac = va ? a : 0;
+    // h operand (k = feature, lane half 0 only; nf <= 8)
+    f32x16 hin;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && hh == 0 && jj < nf) ? sm.h[ac * NFP + jj] : 0.f;
+    f16x8 hh16, hl16;
+    split_f16(hin, 0, hh16, hl16);
+    // prefetch the agg-part fragments two k-steps ahead
+    f32x4 ah[3], al[3];
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      ah[d] = bload4(W, vo, (L.wn1ax + (tp * KS + d) * 512) * 4);
+      al[d] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + d) * 512) * 4);
+    }
+    // vel_scaling_nn: Q partial over this wave's 32 hidden features
+    f32x16 acc = (f32x16)0.f;
+    {
+      const f32x4 vh = bload4(W, vo, (L.wv1x + tp * 512) * 4), vl = bload4(W, vo + 16, (L.wv1x + tp * 512) * 4);
+      acc = mfma_f16(vh, hh16, acc);
+      acc = mfma_f16(vh, hl16, acc);
+      acc = mfma_f16(vl, hh16, acc);
+    }
+    float part = 0.f;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int f0 = 32 * tp + 8 * g4 + 4 * hh;
+      const f32x4 b1 = bload4(W, 0, (L.bv1 + f0) * 4);
+      const f32x4 w2 = bload4(W, 0, (L.wv2 + f0) * 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(acc[4 * g4 + u], inv_v1, b1[u]));
+    }
+    part += __shfl_xor(part, 32, 64);
+    if (hh == 0 && va) sm.u.nd.qp[tp][a] = part;
+    // node_nn.0 over [h, agg]
+    acc = (f32x16)0.f;
+    {
+      const f32x4 nh = bload4(W, vo, (L.wn1hx + tp * 512) * 4), nl = bload4(W, vo + 16, (L.wn1hx + tp * 512) * 4);
+      acc = mfma_f16(nh, hh16, acc);
+      acc = mfma_f16(nh, hl16, acc);
+      acc = mfma_f16(nl, hh16, acc);
+    }
+    const float* arow = &sm.agg[ac * AST];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 2 < KS) {
+        ah[(ks + 2) % 3] = bload4(W, vo, (L.wn1ax + (tp * KS + ks + 2) * 512) * 4);
+        al[(ks + 2) % 3] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + ks + 2) * 512) * 4);
+      }
+      f32x16 av;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) av[jj] = va ? arow[16 * ks + 8 * hh + jj] : 0.f;
+      f16x8 bh, bl;
+      split_f16(av, 0, bh, bl);
+      acc = mfma_f16(ah[ks % 3], bh, acc);
+      acc = mfma_f16(ah[ks % 3], bl, acc);
+      acc = mfma_f16(al[ks % 3], bh, acc);
+    }
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 b1 = bload4(W, 0, (L.bn1 + 32 * tp + 8 * g4 + 4 * hh) * 4);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
+    }
+    // node_nn.2 partial: rows q = rho(r, hh), only r < 4 (q < 8) can be < nf
+    f32x16 gacc = (f32x16)0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const f32x4 gh = bload4(W, vo, (L.wn2x + (tp * 2 + s2) * 512) * 4);
+      const f32x4 gl = bload4(W, vo + 16, (L.wn2x + (tp * 2 + s2) * 512) * 4);
+      f16x8 bh, bl;
+      split_f16(acc, s2, bh, bl);
+      gacc = mfma_f16(gh, bh, gacc);
+      gacc = mfma_f16(gh, bl, gacc);
+      gacc = mfma_f16(gl, bh, gacc);
+    }
+    if (va) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = r + 4 * hh;
+        if (q < nf) sm.u.nd.gp[tp][q][a] = gacc[r] * inv_n2;
       }
     }
   }

@@ -27,17 +27,20 @@ PASSES = [
     ["SQ_INSTS_MFMA", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
      "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_VALU"],
     ["TCC_HIT_sum", "TCC_MISS_sum"],
+    ["TCP_TCC_READ_REQ_sum", "TCP_TOTAL_CACHE_ACCESSES_sum", "TCC_REQ_sum"],
+    ["SQ_INSTS_VMEM_RD", "SQ_WAIT_INST_LDS", "SQ_INSTS_SMEM", "SQ_INST_CYCLES_VMEM_RD"],
 ]
 KERNEL = "lf_flow_kernel"
 
 
 def run_pass(counters, outdir):
     env = dict(os.environ, TMPDIR="/tmp")
-    cmd = ["rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
+    # an over-capacity counter request prints error 38 and then hangs: hard kill
+    cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", *counters, "--output-format", "csv", "-d", outdir, "-o", "pmc", "--",
            sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
            "--no-cpu-baseline"]
     r = subprocess.run(cmd, cwd="/tmp", env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                       text=True, timeout=600)
+                       text=True, timeout=200)
     if r.returncode != 0:
         print(r.stderr[-3000:], file=sys.stderr)
         return {}
