@@ -249,6 +249,36 @@ __device__ __forceinline__ SegMasks seg_masks(int row) {
   return M;
 }
 
+// Four independent segmented scans as fused DPP FMAs (v += dpp(v) * mask): 20
+// VALU instead of 40 (no separate v_mov_b32_dpp).  The four chains interleave, so
+// every DPP source was written >= 3 instructions earlier; the leading s_nop
+// covers the write of the inputs by the code before the statement.
+__device__ __forceinline__ void seg_scan4(float& a, float& b, float& c, float& d, const SegMasks& M) {
+  asm("s_nop 1\n\t"
+      "v_fmac_f32_dpp %0, %0, %4 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %4 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %4 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %4 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %0, %5 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %5 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %5 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %5 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %0, %6 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %6 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %6 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %6 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %0, %7 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %7 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %7 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %7 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %0, %0, %8 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %1, %1, %8 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %2, %2, %8 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_fmac_f32_dpp %3, %3, %8 row_bcast:15 row_mask:0xa bank_mask:0xf"
+      : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+      : "v"(M.m1), "v"(M.m2), "v"(M.m4), "v"(M.m8), "v"(M.m16));
+}
+
 __device__ __forceinline__ float seg_scan(float v, const SegMasks& M) {
   v = fmaf(M.m1, dpp_f<0x111, 0xf>(v), v);
   v = fmaf(M.m2, dpp_f<0x112, 0xf>(v), v);
@@ -267,6 +297,9 @@ __device__ __forceinline__ float seg_scan(float v, const SegMasks& M) {
 //                       fragments one step (>= 1024 cycles) ahead;
 //  ENFLOW_CHAIN_WIDE=0: one output tile at a time (a dependent MFMA chain runs
 //                       at the issue rate for 32x32x2), 3-deep fragment ring.
+#ifndef ENFLOW_SEGSCAN_ASM
+#define ENFLOW_SEGSCAN_ASM 1
+#endif
 #ifndef ENFLOW_CHAIN_WIDE
 #define ENFLOW_CHAIN_WIDE 1
 #endif
@@ -870,7 +903,15 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
 #if !(ENFLOW_ABLATE & 4)
         float v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = seg_scan(c * e[t][4 * g4 + u], SM);
+        for (int u = 0; u < 4; ++u) v[u] = c * e[t][4 * g4 + u];
+#if ENFLOW_SEGSCAN_ASM
+        seg_scan4(v[0], v[1], v[2], v[3], SM);
+#else
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = seg_scan(v[u], SM);
+#endif
+        // one adder per (row, feature) and tile (rows shared with another wave go
+        // to its head buffer); plain read-modify-write: ds_add_f32 measured 1.7x slower
 #pragma unroll
         for (int u = 0; u < 4; ++u) dstm[(32 * t + 8 * g4 + 4 * hh + u) * fstride] += v[u];
 #endif
@@ -894,9 +935,17 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
     const float phi = part + __shfl_xor(part, 32, 64);
     // trans = clamp(coord_diff * phi, -100, 100) (egcl.py:71-72); segment sums
     // for the mean (egcl.py:73-74); lane half 0 stores
-    const float tx = seg_scan(c * fminf(fmaxf(dx * phi, -100.f), 100.f), SM);
-    const float ty = seg_scan(c * fminf(fmaxf(dy * phi, -100.f), 100.f), SM);
-    const float tz = seg_scan(c * fminf(fmaxf(dz * phi, -100.f), 100.f), SM);
+    float tx = c * fminf(fmaxf(dx * phi, -100.f), 100.f);
+    float ty = c * fminf(fmaxf(dy * phi, -100.f), 100.f);
+    float tz = c * fminf(fmaxf(dz * phi, -100.f), 100.f);
+#if ENFLOW_SEGSCAN_ASM
+    float tw = 0.f;
+    seg_scan4(tx, ty, tz, tw, SM);
+#else
+    tx = seg_scan(tx, SM);
+    ty = seg_scan(ty, SM);
+    tz = seg_scan(tz, SM);
+#endif
     float* const dstf = (seg_end && hh == 0) ? dst_row : trash;
     const int fs = (seg_end && hh == 0) ? 1 : 0;
     dstf[(H + 0) * fs] += tx;
