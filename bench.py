@@ -291,6 +291,8 @@ def main():
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     if rank == 0:
+        from enflow_amd import _lib as L_
+        prec_id = L_.PRECISIONS[model.gemm_precision]
         total_mols = MOLS_PER_GPU * world * args.steps
         flops = flops_per_launch(pairs, n_atoms, LAYERS, HID, NF)
         achieved = flops / (kern_ms * 1e-3) / 1e12
@@ -314,8 +316,12 @@ def main():
                        "unique_pairs_per_launch": pairs, "reference_edges_per_launch": edges},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_F32_MFMA_TFLOPS,
-                         "traffic": load_traffic(), "kernel": "lf_flow_kernel<128,32,false>",
-                         "kernel_ms": kern_ms, "flops_per_launch": flops},
+                         "traffic": load_traffic(), "kernel": f"lf_flow_kernel<128,32,false,{prec_id}>",
+                         "kernel_ms": kern_ms, "flops_per_launch": flops,
+                         "gemm_precision": model.gemm_precision,
+                         "note": "achieved = fp32-equivalent algorithmic FLOPs / event-timed launch; peak = dense "
+                                 "f32 MFMA (the arithmetic the path delivers). f16x3 runs the GEMMs as 3 "
+                                 "split-fp16 products on the f16 MFMA pipe (see DESIGN.md)"},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline:
