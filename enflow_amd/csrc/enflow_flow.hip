@@ -223,9 +223,10 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
 // ---------------------------------------------------------------------------
 // the fused flow kernel (forward or reverse)
 // ---------------------------------------------------------------------------
-template <int H, int NMAX, bool REV, int PREC>
+template <int H, int NMAX, bool REV, int PREC, int RB>
 __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(FlowArgs A) {
-  __shared__ Smem<H, NMAX> sm;
+  __shared__ Smem<H, NMAX, RB> sm;
+  constexpr bool BLOCKED = RB < NMAX;
   MolRef M;
   STAMP_DECL
   if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) return;
@@ -233,7 +234,7 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
   const int tid = threadIdx.x;
   const int n = M.n, nf = A.nf;
   const EgclLayout L = egcl_layout(H, nf);
-  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int AST = Smem<H, NMAX, RB>::AST;
   float ldj = 0.f;
 
   if (!REV) {
@@ -267,48 +268,71 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
       }
       __syncthreads();
     }
-    if (!(ENFLOW_ABLATE & 1) || it == 0) build_pairs(sm, Ml, tid_l);
-    STAMP(2);
-    if (A.stats != nullptr && tid == 0) {
-      unsigned long long edges = 0;
-      for (int a = 0; a < n; ++a) edges += (unsigned long long)sm.cntrow[a];
-      atomicAdd(&A.stats[0], (unsigned long long)sm.npairs);
-      atomicAdd(&A.stats[1], edges);
-    }
-    STAMP(3);
-    edge_tiles<H, NMAX, PREC>(sm, Lp, L, Ml, nf, tid_l STAMP_PASS);
-    STAMP(4);
-    if (!(ENFLOW_ABLATE & 2)) {
-      if constexpr (PREC == PREC_F16X3) node_phase_x3(sm, Lp, L, n, nf, tid_l);
-      else node_phase(sm, Lp, L, n, nf, tid_l);
-    }
-    STAMP(5);
-    if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q
-      const TapeLayout T = tape_layout(A.num_atoms, nf, H, A.n_layers);
-      const size_t la = (size_t)l * A.num_atoms + M.a0;
-      float* hx = A.tape + T.hx + la * T.ldhx;
-      for (int e = tid; e < n * T.ldhx; e += BLOCK) {
-        const int a = e / T.ldhx, c = e - a * T.ldhx;
-        hx[e] = c < nf ? sm.h[a * NFP + c] : sm.agg[a * AST + (c - nf)];
+    if (!(ENFLOW_ABLATE & 1) || it == 0) build_images(sm, Ml, tid_l);
+    int npairs_layer = 0;
+    auto block_pass = [&](const int r0, const int rb) {
+      if (!(ENFLOW_ABLATE & 1) || it == 0) build_block_pairs(sm, Ml, tid_l, r0, rb);
+      STAMP(2);
+      npairs_layer += sm.npairs;
+      if (A.stats != nullptr && tid == 0) {
+        unsigned long long edges = 0;
+        for (int a = 0; a < rb; ++a) edges += (unsigned long long)sm.cntrow[r0 + a];
+        atomicAdd(&A.stats[0], (unsigned long long)sm.npairs);
+        atomicAdd(&A.stats[1], edges);
       }
-      for (int e = tid; e < n * nf; e += BLOCK) {
-        const int a = e / nf, q = e - a * nf;
-        A.tape[T.g + la * nf + e] = sm.g[a * NFP + q];
+      STAMP(3);
+      edge_tiles<H, NMAX, RB, PREC>(sm, Lp, L, Ml, nf, tid_l, r0, rb STAMP_PASS);
+      STAMP(4);
+      if (!(ENFLOW_ABLATE & 2)) {
+        if constexpr (PREC == PREC_F16X3) node_phase_x3(sm, Lp, L, n, nf, tid_l, r0, rb);
+        else node_phase(sm, Lp, L, n, nf, tid_l, r0, rb);
       }
-      for (int e = tid; e < n * 3; e += BLOCK) {
-        A.tape[T.pos + la * 3 + e] = sm.pos[e];
-        A.tape[T.vel + la * 3 + e] = sm.vel[e];
+      STAMP(5);
+      if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q
+        const TapeLayout T = tape_layout(A.num_atoms, nf, H, A.n_layers);
+        const size_t la = (size_t)l * A.num_atoms + M.a0 + r0;
+        float* hx = A.tape + T.hx + la * T.ldhx;
+        for (int e = tid; e < rb * T.ldhx; e += BLOCK) {
+          const int a = e / T.ldhx, c = e - a * T.ldhx;
+          hx[e] = c < nf ? sm.h[(r0 + a) * NFP + c] : sm.agg[a * AST + (c - nf)];
+        }
+        for (int e = tid; e < rb * nf; e += BLOCK) {
+          const int a = e / nf, q = e - a * nf;
+          A.tape[T.g + la * nf + e] = sm.g[(r0 + a) * NFP + q];
+        }
+        for (int e = tid; e < rb * 3; e += BLOCK) {
+          A.tape[T.pos + la * 3 + e] = sm.pos[r0 * 3 + e];
+          A.tape[T.vel + la * 3 + e] = sm.vel[r0 * 3 + e];
+        }
+        for (int a = tid; a < rb; a += BLOCK) A.tape[T.q + la + a] = sm.Q[r0 + a];
       }
-      for (int a = tid; a < n; a += BLOCK) A.tape[T.q + la + a] = sm.Q[a];
-      if (tid == 0 && A.pair_counts != nullptr) A.pair_counts[(size_t)l * A.num_mols + blockIdx.x] = sm.npairs;
+      if constexpr (BLOCKED) {   // park the block's forces (egcl.py:73-74)
+        for (int e = tid; e < rb * 3; e += BLOCK) {
+          const int a = e / 3, d = e - a * 3;
+          const float inv = 1.f / fmaxf((float)sm.cntrow[r0 + a], 1.f);
+          sm.F[(r0 + a) * 3 + d] = sm.agg[a * AST + H + d] * inv * A.cw;
+        }
+        __syncthreads();
+      }
+    };
+    if constexpr (BLOCKED) {
+      for (int r0 = 0; r0 < n; r0 += RB) block_pass(r0, min(RB, n - r0));
+    } else {
+      block_pass(0, n);   // the whole molecule in one pass
     }
+    if (!REV && A.tape != nullptr && tid == 0 && A.pair_counts != nullptr)
+      A.pair_counts[(size_t)l * A.num_mols + blockIdx.x] = npairs_layer;
     for (int a = tid; a < n; a += BLOCK) {
       const float q = sm.Q[a];
       const float eq = expf(q);
       const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);   // helpers.py:63-70
+      auto force = [&](int d) {
+        if constexpr (BLOCKED) return sm.F[a * 3 + d];
+        else return sm.agg[a * AST + H + d] * inv * A.cw;
+      };
       if (!REV) {  // dynamics.py:15-22
         for (int d = 0; d < 3; ++d) {
-          const float F = sm.agg[a * AST + H + d] * inv * A.cw;
+          const float F = force(d);
           const float v = eq * sm.vel[a * 3 + d] + F * A.dt;
           sm.vel[a * 3 + d] = v;
           sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, sm.boxa[a * 3 + d]);
@@ -322,7 +346,7 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
       } else {     // dynamics.py:32-35
         for (int qf = 0; qf < nf; ++qf) sm.g[a * NFP + qf] -= sm.G[a * NFP + qf] * A.dt;
         for (int d = 0; d < 3; ++d) {
-          const float F = sm.agg[a * AST + H + d] * inv * A.cw;
+          const float F = force(d);
           sm.vel[a * 3 + d] = (sm.vel[a * 3 + d] - F * A.dt) / eq;
         }
       }
@@ -366,34 +390,40 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
 }
 
 // one EGCL.forward: Q, F, G to global
-template <int H, int NMAX>
+template <int H, int NMAX, int RB>
 __global__ void __launch_bounds__(BLOCK, 2) egcl_forward_kernel(FlowArgs A, float* Qo, float* Fo, float* Go) {
-  __shared__ Smem<H, NMAX> sm;
+  __shared__ Smem<H, NMAX, RB> sm;
   MolRef M;
   if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H)) return;
   const int tid = threadIdx.x;
   const int n = M.n, nf = A.nf;
   const EgclLayout L = egcl_layout(H, nf);
-  constexpr int AST = Smem<H, NMAX>::AST;
-  build_pairs(sm, M, tid);
+  constexpr int AST = Smem<H, NMAX, RB>::AST;
+  build_images(sm, M, tid);
 #ifdef ENFLOW_STAMPS
   STAMP_DECL
 #endif
-  edge_tiles(sm, A.layers, L, M, nf, tid STAMP_PASS);
-  node_phase(sm, A.layers, L, n, nf, tid);
-  for (int a = tid; a < n; a += BLOCK) {
-    Qo[M.a0 + a] = sm.Q[a];
-    const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);
-    for (int d = 0; d < 3; ++d) Fo[(size_t)(M.a0 + a) * 3 + d] = sm.agg[a * AST + H + d] * inv * A.cw;
-    for (int q = 0; q < nf; ++q) Go[(size_t)(M.a0 + a) * nf + q] = sm.G[a * NFP + q];
+  for (int r0 = 0; r0 < n; r0 += RB) {
+    const int rb = min(RB, n - r0);
+    build_block_pairs(sm, M, tid, r0, rb);
+    edge_tiles(sm, A.layers, L, M, nf, tid, r0, rb STAMP_PASS);
+    node_phase(sm, A.layers, L, n, nf, tid, r0, rb);
+    for (int a = tid; a < rb; a += BLOCK) {
+      const int ag = r0 + a;
+      Qo[M.a0 + ag] = sm.Q[ag];
+      const float inv = 1.f / fmaxf((float)sm.cntrow[ag], 1.f);
+      for (int d = 0; d < 3; ++d) Fo[(size_t)(M.a0 + ag) * 3 + d] = sm.agg[a * AST + H + d] * inv * A.cw;
+      for (int q = 0; q < nf; ++q) Go[(size_t)(M.a0 + ag) * nf + q] = sm.G[ag * NFP + q];
+    }
+    __syncthreads();
   }
   if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
 }
 
 // ArgMax.forward only
-template <int H, int NMAX>
+template <int H, int NMAX, int RB>
 __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float* z, float* lq_mol) {
-  __shared__ Smem<H, NMAX> sm;
+  __shared__ Smem<H, NMAX, RB> sm;
   MolRef M;
   if (!load_molecule(sm, A, M, LOAD_H)) return;
   const int tid = threadIdx.x;
@@ -407,17 +437,27 @@ __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float
   if (tid == 0) lq_mol[blockIdx.x] = s;
 }
 
-// neighbour pairs only
-template <int NMAX>
+// neighbour pairs only (rows re-labelled molecule-local when row-blocked)
+template <int NMAX, int RB>
 __global__ void __launch_bounds__(BLOCK) neighbour_pairs_kernel(FlowArgs A, int max_pairs, uint32_t* pairs, int32_t* count) {
-  __shared__ Smem<32, NMAX> sm;
+  __shared__ Smem<32, NMAX, RB> sm;
   MolRef M;
   if (!load_molecule(sm, A, M, LOAD_POS)) return;
-  build_pairs(sm, M, (int)threadIdx.x);
-  const int P = sm.npairs;
-  for (int p = threadIdx.x; p < P && p < max_pairs; p += BLOCK) pairs[(size_t)blockIdx.x * max_pairs + p] = sm.pairs[p];
+  build_images(sm, M, (int)threadIdx.x);
+  int off = 0;
+  for (int r0 = 0; r0 < M.n; r0 += RB) {
+    const int rb = min(RB, M.n - r0);
+    build_block_pairs(sm, M, (int)threadIdx.x, r0, rb);
+    const int P = sm.npairs;
+    for (int p = threadIdx.x; p < P && off + p < max_pairs; p += BLOCK) {
+      const uint32_t pr = sm.pairs[p];
+      pairs[(size_t)blockIdx.x * max_pairs + off + p] = (pr & ~0xffu) | (uint32_t)(r0 + (int)(pr & 0xffu));
+    }
+    off += P;
+    __syncthreads();
+  }
   if (threadIdx.x == 0) {
-    count[blockIdx.x] = P;
+    count[blockIdx.x] = off;
     if (sm.err) atomicOr(A.err, sm.err);
   }
 }
@@ -513,27 +553,34 @@ static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); 
 static inline int hid_ok(int H) { return H == 32 || H == 64 || H == 128; }
 static const double kLog2Pi = 1.8378770664093453;
 
+// molecule-size classes: <= 32 and <= 64 atoms unblocked, <= 256 atoms in
+// row blocks of 32 (BASELINE configs[4]: 256-atom chains)
+#define MAX_ATOMS 256
 #define DISPATCH_HN(H, NMAXSEL, CALL)                        \
   do {                                                        \
     if (NMAXSEL <= 32) {                                      \
-      if (H == 32) { CALL(32, 32); }                          \
-      else if (H == 64) { CALL(64, 32); }                     \
-      else { CALL(128, 32); }                                 \
+      if (H == 32) { CALL(32, 32, 32); }                      \
+      else if (H == 64) { CALL(64, 32, 32); }                 \
+      else { CALL(128, 32, 32); }                             \
+    } else if (NMAXSEL <= 64) {                               \
+      if (H == 32) { CALL(32, 64, 64); }                      \
+      else if (H == 64) { CALL(64, 64, 64); }                 \
+      else { CALL(128, 64, 64); }                             \
     } else {                                                  \
-      if (H == 32) { CALL(32, 64); }                          \
-      else if (H == 64) { CALL(64, 64); }                     \
-      else { CALL(128, 64); }                                 \
+      if (H == 32) { CALL(32, 256, 32); }                     \
+      else if (H == 64) { CALL(64, 256, 32); }                \
+      else { CALL(128, 256, 32); }                            \
     }                                                         \
   } while (0)
 
-template <int HH, int NN, bool REV>
+template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
   if (prec == ENFLOW_PREC_F16X3)
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB>), dim3(num_mols), dim3(BLOCK), 0, st, A);
   else if (prec == ENFLOW_PREC_BF16)
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16, RBB>), dim3(num_mols), dim3(BLOCK), 0, st, A);
   else
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32, RBB>), dim3(num_mols), dim3(BLOCK), 0, st, A);
 }
 
 extern "C" {
@@ -551,7 +598,7 @@ int enflow_read_stamps(unsigned long long* host_out, int reset) {
 #endif
 
 int enflow_abi_version(void) { return ENFLOW_ABI; }
-int enflow_max_atoms(void) { return 64; }
+int enflow_max_atoms(void) { return MAX_ATOMS; }
 int enflow_max_node_nf(void) { return NFMAX; }
 int enflow_supports_hidden(int hidden_nf) { return hid_ok(hidden_nf); }
 
@@ -581,7 +628,7 @@ int enflow_pack_argmax_f32(const float* raw, int H, int nf, float* packed, void*
 
 static int check_common(int num_mols, int max_mol_atoms, int nf, int H) {
   if (num_mols < 0 || max_mol_atoms < 0) return -1;
-  if (max_mol_atoms > 64) return -3;
+  if (max_mol_atoms > MAX_ATOMS) return -3;
   if (nf < 1 || nf > NFMAX) return -4;
   if (!hid_ok(H)) return -5;
   return 0;
@@ -600,12 +647,13 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
-  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr)) return -1;
+  // training tape: the backward handles molecules of <= 64 atoms (unblocked pair lists)
+  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr || max_mol_atoms > 64)) return -1;
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
              dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
              reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
   if (num_mols > 0) {
-#define CALL(HH, NN) launch_flow<HH, NN, false>(gemm_precision, num_mols, S(stream), A)
+#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, false>(gemm_precision, num_mols, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
@@ -629,7 +677,7 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
              0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag, nullptr};
   if (num_mols > 0) {
-#define CALL(HH, NN) launch_flow<HH, NN, true>(gemm_precision, num_mols, S(stream), A)
+#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, true>(gemm_precision, num_mols, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
@@ -655,7 +703,7 @@ int enflow_egcl_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int 
   FlowArgs A{mol_ptr, r_cut, box, const_cast<float*>(h), nullptr, const_cast<float*>(pos), nullptr, layer, 1, nf,
              0, nullptr, nullptr, 0.f, 0.f, cw, nullptr, nullptr, nullptr, err_flag, nullptr};
   if (num_mols > 0) {
-#define CALL(HH, NN) hipLaunchKernelGGL((egcl_forward_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, Q, F, G)
+#define CALL(HH, NN, RBB) hipLaunchKernelGGL((egcl_forward_kernel<HH, NN, RBB>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, Q, F, G)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
@@ -671,7 +719,7 @@ int enflow_argmax_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, in
   FlowArgs A{mol_ptr, nullptr, nullptr, const_cast<float*>(h), nullptr, nullptr, nullptr, nullptr, 0, nf,
              ENFLOW_DEQUANT_ARGMAX, dequant, noise, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr};
   if (num_mols > 0) {
-#define CALL(HH, NN) hipLaunchKernelGGL((argmax_forward_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, z, log_q_mol)
+#define CALL(HH, NN, RBB) hipLaunchKernelGGL((argmax_forward_kernel<HH, NN, RBB>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, z, log_q_mol)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
@@ -683,15 +731,17 @@ int enflow_neighbour_pairs_f32(int num_mols, int num_atoms, int max_mol_atoms, c
                                const float* r_cut, const float* box, const float* pos,
                                int max_pairs, uint32_t* pairs, int32_t* pair_count,
                                int32_t* err_flag, void* stream) {
-  if (num_mols < 0 || max_mol_atoms > 64 || max_pairs < 0) return -1;
+  if (num_mols < 0 || max_mol_atoms > MAX_ATOMS || max_pairs < 0) return -1;
   (void)num_atoms;
   FlowArgs A{mol_ptr, r_cut, box, nullptr, nullptr, const_cast<float*>(pos), nullptr, nullptr, 0, 1,
              0, nullptr, nullptr, 0.f, 0.f, 0.f, nullptr, nullptr, nullptr, err_flag, nullptr};
   if (num_mols > 0) {
     if (max_mol_atoms <= 32)
-      hipLaunchKernelGGL((neighbour_pairs_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
+      hipLaunchKernelGGL((neighbour_pairs_kernel<32, 32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
+    else if (max_mol_atoms <= 64)
+      hipLaunchKernelGGL((neighbour_pairs_kernel<64, 64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
     else
-      hipLaunchKernelGGL((neighbour_pairs_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
+      hipLaunchKernelGGL((neighbour_pairs_kernel<256, 32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), A, max_pairs, pairs, pair_count);
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -701,12 +751,14 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
                               const float* pos, const float* vel, const float* ldj_total,
                               float kBT, float softening, float partition_func,
                               float* nll_mol, float* loss, void* stream) {
-  if (num_mols < 0 || max_mol_atoms > 64 || nf < 1) return -1;
+  if (num_mols < 0 || max_mol_atoms > MAX_ATOMS || nf < 1) return -1;
   if (num_mols > 0) {
     if (max_mol_atoms <= 32)
       hipLaunchKernelGGL((nll_mol_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
-    else
+    else if (max_mol_atoms <= 64)
       hipLaunchKernelGGL((nll_mol_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+    else
+      hipLaunchKernelGGL((nll_mol_kernel<256>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
   }
   hipLaunchKernelGGL(reduce_nll_kernel, dim3(1), dim3(BLOCK), 0, S(stream), nll_mol, num_mols, num_atoms, ldj_total,
                      kBT, partition_func, loss);

@@ -596,16 +596,24 @@ __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 // ---------------------------------------------------------------------------
 // shared memory
 // ---------------------------------------------------------------------------
-template <int H, int NMAX>
+// RB = rows per block.  RB == NMAX: the whole molecule's pair list and
+// aggregates are resident (one block per layer).  RB < NMAX (large molecules):
+// per layer the image masks / id_mapping are built for all atoms once, then
+// the pair list, edge tiles and node phase run one block of RB rows at a time;
+// the finished blocks' forces are parked in F and the leapfrog update runs
+// after the last block.
+template <int H, int NMAX, int RB = NMAX>
 struct Smem {
   static constexpr int NT = H / 32;
   static constexpr int AST = H + 5;   // agg row: H message sums, 3 force sums, pad (odd stride)
-  static constexpr int MAXP = NMAX * (NMAX - 1);
+  static constexpr int MAXP = RB * (NMAX - 1);
+  static constexpr bool BLOCKED = RB < NMAX;
   float pos[NMAX * 3], vel[NMAX * 3], boxa[NMAX * 3];
   float h[NMAX * NFP], g[NMAX * NFP], G[NMAX * NFP];
   float Q[NMAX];
+  float F[BLOCKED ? NMAX * 3 : 1];    // forces of finished row blocks (blocked only)
   alignas(16) float bias[4 * H];      // be1, be2, bc1, wc2 of the current layer
-  float agg[NMAX * AST];
+  float agg[RB * AST];
   float head[WAVES][H + 4];
   float trash[WAVES][64];             // sink for the branch-free segment-sum stores
   uint32_t pairs[MAXP];
@@ -619,8 +627,8 @@ struct Smem {
   int err;
   float red[WAVES];
   union {
-    int C[NMAX * NMAX];                                         // pair build
-    struct { float qp[NT][NMAX]; float gp[NT][NFMAX][NMAX]; } nd;  // node phase partials
+    int C[RB * NMAX];                                           // pair build (block rows x atoms)
+    struct { float qp[NT][RB]; float gp[NT][NFMAX][RB]; } nd;   // node phase partials
     float net[NMAX * 2 * NFMAX];                                // ArgMax outputs
   } u;
 };
@@ -636,8 +644,9 @@ struct MolRef {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float shift_of(int idx, float b) { return idx == 0 ? -b : (idx == 1 ? b : 0.f); }
 
-template <int H, int NMAX>
-__device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, int tid) {
+// (a) image masks and (b) id_mapping for all atoms of the molecule (once per layer)
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void build_images(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid) {
   const int n = M.n;
   const float rx = M.bx + M.rc, ry = M.by + M.rc, rz = M.bz + M.rc;   // helpers.py:20
   for (int a = tid; a < n; a += BLOCK) {
@@ -645,7 +654,6 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, 
     sm.idmap[a] = -1;
     sm.cntrow[a] = 0;
   }
-  for (int e = tid; e < n * n; e += BLOCK) sm.u.C[e] = 0;
   __syncthreads();
   // (a) image masks, one (atom, image) per thread: bit s <=> image s of atom a
   //     lies in the ellipsoid with radii box + r_cut (helpers.py:17-22)
@@ -661,26 +669,39 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, 
   // (b) id_mapping[q] for q < n: the q-th surviving image in (image, atom) order (helpers.py:25-27)
   if (tid < 64) {
     const int lane = tid;
-    const uint32_t mk = lane < n ? sm.mask27[lane] : 0u;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int prefix = 0;
     for (int s = 0; s < 27 && prefix < n; ++s) {
-      const bool bit = (mk >> s) & 1u;
-      const uint64_t bal = __ballot(bit);
-      if (bit) {
-        const int posF = prefix + __popcll(bal & lt);
-        if (posF < n) sm.idmap[posF] = lane;
+      for (int ch = 0; ch < n; ch += 64) {
+        const int a = ch + lane;
+        const uint32_t mk = a < n ? sm.mask27[a] : 0u;
+        const bool bit = (mk >> s) & 1u;
+        const uint64_t bal = __ballot(bit);
+        if (bit) {
+          const int posF = prefix + __popcll(bal & lt);
+          if (posF < n) sm.idmap[posF] = a;
+        }
+        prefix += __popcll(bal);
       }
-      prefix += __popcll(bal);
     }
     if (lane == 0 && prefix < n) sm.err |= ENFLOW_ERR_FEW_IMAGES;
   }
   __syncthreads();
-  // (c) multiplicity matrix: C[i][id_mapping[q]] += #images of i within r_cut of atom q
-  //     (base.py:133-139: both hit columns mapped through id_mapping, self pairs dropped)
+}
+
+// (c) multiplicity matrix of rows r0 .. r0 + rb - 1: C[i][id_mapping[q]] += #images
+//     of i within r_cut of atom q (base.py:133-139: both hit columns mapped through
+//     id_mapping, self pairs dropped), (d) compaction to (local row, col, mult)
+//     sorted by (row, col).
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid, int r0, int rb) {
+  const int n = M.n;
+  for (int e = tid; e < rb * n; e += BLOCK) sm.u.C[e] = 0;
+  __syncthreads();
   const float r_sq = M.rc * M.rc;
-  for (int e = tid; e < n * n; e += BLOCK) {
-    const int i = e / n, q = e - i * n;
+  for (int e = tid; e < rb * n; e += BLOCK) {
+    const int il = e / n, q = e - il * n;
+    const int i = r0 + il;
     const int jl = sm.idmap[q];
     if (jl == i || jl < 0) continue;   // jl < 0 only with ENFLOW_ERR_FEW_IMAGES
     const uint32_t mk = sm.mask27[i];
@@ -697,13 +718,12 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, 
       if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
     }
     if (cnt) {
-      atomicAdd(&sm.u.C[i * n + jl], cnt);
+      atomicAdd(&sm.u.C[il * n + jl], cnt);
       atomicAdd(&sm.cntrow[i], cnt);
     }
   }
   __syncthreads();
-  // (d) compact to (row, col, mult) sorted by (row, col)
-  const int NN = n * n;
+  const int NN = rb * n;
   const int per = (NN + BLOCK - 1) / BLOCK;
   const int e0 = tid * per, e1 = min(NN, e0 + per);
   int local = 0;
@@ -717,8 +737,8 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, 
   for (int e = e0; e < e1; ++e) {
     const int c = sm.u.C[e];
     if (c > 0) {
-      const int i = e / n, jl = e - i * n;
-      sm.pairs[base++] = (uint32_t)i | ((uint32_t)jl << 8) | ((uint32_t)c << 16);
+      const int il = e / n, jl = e - il * n;
+      sm.pairs[base++] = (uint32_t)il | ((uint32_t)jl << 8) | ((uint32_t)c << 16);
     }
   }
   if (tid == BLOCK - 1) {
@@ -729,23 +749,30 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX>& sm, const MolRef& M, 
   __syncthreads();
 }
 
+// whole-molecule pair list (one block)
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void build_pairs(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid) {
+  static_assert(RB == NMAX, "build_pairs needs the unblocked image");
+  build_images(sm, M, tid);
+  build_block_pairs(sm, M, tid, 0, M.n);
+}
+
 // ---------------------------------------------------------------------------
 // EGCL edge part: per-pair MLP chain on MFMA + deterministic segment sums
 // ---------------------------------------------------------------------------
-template <int H, int NMAX, int PREC = PREC_F32>
-__device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                           const MolRef& M, int nf, int tid STAMP_ARGS) {
+template <int H, int NMAX, int RB, int PREC = PREC_F32>
+__device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
+                                           const MolRef& M, int nf, int tid, int r0, int rb STAMP_ARGS) {
   constexpr int NT = H / 32;
-  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int AST = Smem<H, NMAX, RB>::AST;
   const int lane = tid & 63, w = tid >> 6;
   const int j = lane & 31, hh = lane >> 5;
-  const int n = M.n;
   const int P = sm.npairs;
   const int T = (P + 31) >> 5;
   const int tpw = (T + WAVES - 1) / WAVES;
 
   // zero aggregates / heads, stage biases, find each wave's head row
-  for (int e = tid; e < n * AST; e += BLOCK) sm.agg[e] = 0.f;
+  for (int e = tid; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
   for (int e = tid; e < WAVES * (H + 4); e += BLOCK) (&sm.head[0][0])[e] = 0.f;
   for (int k = tid; k < H; k += BLOCK) {
     sm.bias[k] = Lp[L.be1 + k];
@@ -781,14 +808,15 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
     const int p = tile * 32 + j;
     const bool valid = p < P;
     const uint32_t pr = valid ? sm.pairs[p] : 0u;
-    const int i = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
+    const int il = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
+    const int i = r0 + il;                 // atom of the row (il: row within the block)
     const float c = (float)(pr >> 16);
     // segments = runs of equal row; invalid lanes get unique rows of their own
-    const int row = valid ? i : -1 - j;
+    const int row = valid ? il : -1 - j;
     const SegMasks SM = seg_masks(row);
     const int row_next = __shfl_down(row, 1, 32);
     const bool seg_end = valid && (j == 31 || row_next != row);
-    float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? i : 0) * AST];
+    float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? il : 0) * AST];
     // Edges.coord_diff with the reference's half-box image (base.py:15-19)
     const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
     const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
@@ -963,31 +991,54 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX>& sm, const float* __res
   __syncthreads();
 }
 
+// Q and G of the block's atoms from the per-wave partials (fixed order)
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void node_partials_reduce(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp,
+                                                     const EgclLayout& L, int nf, int tid, int r0, int rb) {
+  constexpr int NT = H / 32;
+  const float bv2 = Lp[L.bv2];
+  for (int a = tid; a < rb; a += BLOCK) {
+    float s = 0.f;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.qp[tp][a];
+    sm.Q[r0 + a] = s + bv2;
+  }
+  for (int e = tid; e < rb * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    float s = 0.f;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.gp[tp][q][a];
+    sm.G[(r0 + a) * NFP + q] = s + Lp[L.bn2 + q];
+  }
+  __syncthreads();
+}
+
 // Node part of EGCL (egcl.py:26-30, 51-54, 62-67, 90-92), all on MFMA with
 // atoms on the pair lanes: wave item (tp, atom tile) computes
 //   Q partial   = vel_scaling_nn.2[32tp..] . silu(vel_scaling_nn.0 h)   (32 features)
 //   act         = silu(node_nn.0 [h, agg])                               (32 features)
 //   G partial   = node_nn.2[:, 32tp..] . act
 // and the NT partials are summed in fixed order (deterministic).
-template <int H, int NMAX>
-__device__ __forceinline__ void node_phase(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                           int n, int nf, int tid) {
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
+                                           int n, int nf, int tid, int r0, int rb) {
   constexpr int NT = H / 32;
-  constexpr int NA = NMAX / 32;
-  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int NA = RB / 32;
+  constexpr int AST = Smem<H, NMAX, RB>::AST;
   const int lane = tid & 63, w = tid >> 6;
   const int j = lane & 31, hh = lane >> 5;
   const int nh = (nf + 1) >> 1;
   const rsrc_t W = weights_rsrc(Lp, L.total);
   for (int item = w; item < NT * NA; item += WAVES) {
     const int tp = item % NT, at = item / NT;
-    const int a = at * 32 + j;
-    const bool va = a < n;
+    const int a = at * 32 + j;              // row within the block
+    const bool va = a < rb;
     const int ac = va ? a : 0;
+    const int ag = r0 + ac;                 // atom
     // vel_scaling_nn: Q partial over this wave's 32 hidden features
     f32x16 acc = (f32x16)0.f;
     for (int s = 0; s < nh; ++s) {
-      const float b = va ? sm.h[ac * NFP + 2 * s + hh] : 0.f;
+      const float b = va ? sm.h[ag * NFP + 2 * s + hh] : 0.f;
       acc = mfma32(bload(W, lane * 4, (L.wv1f + (tp * (NFMAX / 2) + s) * 64) * 4), b, acc);
     }
     float part = 0.f;
@@ -1004,7 +1055,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX>& sm, const float* __res
     // node_nn.0 over [h, agg]
     acc = (f32x16)0.f;
     for (int s = 0; s < nh; ++s) {
-      const float b = va ? sm.h[ac * NFP + 2 * s + hh] : 0.f;
+      const float b = va ? sm.h[ag * NFP + 2 * s + hh] : 0.f;
       acc = mfma32(bload(W, lane * 4, (L.wn1h + (tp * (NFMAX / 2) + s) * 64) * 4), b, acc);
     }
     const float* arow = &sm.agg[ac * AST];
@@ -1040,31 +1091,17 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX>& sm, const float* __res
     }
   }
   __syncthreads();
-  const float bv2 = Lp[L.bv2];
-  for (int a = tid; a < n; a += BLOCK) {
-    float s = 0.f;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.qp[tp][a];
-    sm.Q[a] = s + bv2;
-  }
-  for (int e = tid; e < n * nf; e += BLOCK) {
-    const int a = e / nf, q = e - a * nf;
-    float s = 0.f;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.gp[tp][q][a];
-    sm.G[a * NFP + q] = s + Lp[L.bn2 + q];
-  }
-  __syncthreads();
+  node_partials_reduce(sm, Lp, L, nf, tid, r0, rb);
 }
 
 // F16X3 node phase: same items and outputs as node_phase, all products on
 // v_mfma_f32_32x32x16_f16 with hi/lo split operands (atoms on the pair lanes).
-template <int H, int NMAX>
-__device__ __forceinline__ void node_phase_x3(Smem<H, NMAX>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                              int n, int nf, int tid) {
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
+                                              int n, int nf, int tid, int r0, int rb) {
   constexpr int NT = H / 32;
-  constexpr int NA = NMAX / 32;
-  constexpr int AST = Smem<H, NMAX>::AST;
+  constexpr int NA = RB / 32;
+  constexpr int AST = Smem<H, NMAX, RB>::AST;
   constexpr int KS = H / 16;
   const int lane = tid & 63, w = tid >> 6;
   const int j = lane & 31, hh = lane >> 5;
@@ -1073,13 +1110,14 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX>& sm, const float* __
   const int vo = lane * 32;
   for (int item = w; item < NT * NA; item += WAVES) {
     const int tp = item % NT, at = item / NT;
-    const int a = at * 32 + j;
-    const bool va = a < n;
+    const int a = at * 32 + j;              // row within the block
+    const bool va = a < rb;
     const int ac = va ? a : 0;
+    const int ag = r0 + ac;                 // atom
     // h operand (k = feature, lane half 0 only; nf <= 8)
     f32x16 hin;
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && hh == 0 && jj < nf) ? sm.h[ac * NFP + jj] : 0.f;
+    for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && hh == 0 && jj < nf) ? sm.h[ag * NFP + jj] : 0.f;
     f16x8 hh16, hl16;
     split_f16(hin, 0, hh16, hl16);
     // prefetch the agg-part fragments two k-steps ahead
@@ -1159,58 +1197,47 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX>& sm, const float* __
     }
   }
   __syncthreads();
-  const float bv2 = Lp[L.bv2];
-  for (int a = tid; a < n; a += BLOCK) {
-    float s = 0.f;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.qp[tp][a];
-    sm.Q[a] = s + bv2;
-  }
-  for (int e = tid; e < n * nf; e += BLOCK) {
-    const int a = e / nf, q = e - a * nf;
-    float s = 0.f;
-#pragma unroll
-    for (int tp = 0; tp < NT; ++tp) s += sm.u.nd.gp[tp][q][a];
-    sm.G[a * NFP + q] = s + Lp[L.bn2 + q];
-  }
-  __syncthreads();
+  node_partials_reduce(sm, Lp, L, nf, tid, r0, rb);
 }
 
 // ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
 // returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
-template <int H, int NMAX>
-__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX>& sm, const float* __restrict__ Dp, const float* __restrict__ noise,
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const float* __restrict__ noise,
                                 int a0, int n, int nf) {
   constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
   constexpr int ACT = H + 1;            // hidden activations staged in agg (free before layer 0)
+  static_assert(RB * (H + 5) >= RB * ACT, "agg too small for the ArgMax activations");
   float* const act = sm.agg;
   const AmLayout L = argmax_layout(H, nf);
   const int tid = threadIdx.x;
-  {
-    const int k = tid % H, grp = tid / H;
-    if (grp < NG) {
-      const float b = Dp[L.ba1 + k];
-      for (int a = grp; a < n; a += NG) {
-        float v = b;
-        for (int q = 0; q < nf; ++q) v += Dp[L.wa1t + q * H + k] * sm.h[a * NFP + q];
-        act[a * ACT + k] = silu_f(v);
+  float* net = sm.u.net;
+  for (int c0 = 0; c0 < n; c0 += RB) {   // atoms in chunks of RB (the agg image)
+    const int cn = min(RB, n - c0);
+    {
+      const int k = tid % H, grp = tid / H;
+      if (grp < NG) {
+        const float b = Dp[L.ba1 + k];
+        for (int a = grp; a < cn; a += NG) {
+          float v = b;
+          for (int q = 0; q < nf; ++q) v += Dp[L.wa1t + q * H + k] * sm.h[(c0 + a) * NFP + q];
+          act[a * ACT + k] = silu_f(v);
+        }
       }
     }
+    __syncthreads();
+    // net[a][o], o < 2 nf
+    for (int e = tid; e < cn * 2 * nf; e += BLOCK) {
+      const int a = e / (2 * nf), o = e - a * 2 * nf;
+      float s = Dp[L.ba2 + o];
+      const float* wr = Dp + L.wa2 + o * H;
+      for (int k = 0; k < H; ++k) s += wr[k] * act[a * ACT + k];
+      net[(c0 + a) * 2 * NFMAX + o] = s;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  // net[a][o], o < 2 nf
-  float* net = sm.u.net;
-  for (int e = tid; e < n * 2 * nf; e += BLOCK) {
-    const int a = e / (2 * nf), o = e - a * 2 * nf;
-    float s = Dp[L.ba2 + o];
-    const float* wr = Dp + L.wa2 + o * H;
-    for (int k = 0; k < H; ++k) s += wr[k] * act[a * ACT + k];
-    net[a * 2 * NFMAX + o] = s;
-  }
-  __syncthreads();
   float lq = 0.f;
-  if (tid < n) {
-    const int a = tid;
+  for (int a = tid; a < n; a += BLOCK) {
     float u[NFMAX], hv[NFMAX];
     float T = 0.f;
 #pragma unroll
@@ -1237,8 +1264,8 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX>& sm, const float* 
 }
 
 // deterministic block sum (thread values -> one float, fixed order)
-template <int H, int NMAX>
-__device__ __forceinline__ float block_sum(Smem<H, NMAX>& sm, float v) {
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ float block_sum(Smem<H, NMAX, RB>& sm, float v) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __syncthreads();
@@ -1278,8 +1305,8 @@ struct FlowArgs {
 
 enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
 
-template <int H, int NMAX>
-__device__ __forceinline__ bool load_molecule(Smem<H, NMAX>& sm, const FlowArgs& A, MolRef& M, int what) {
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowArgs& A, MolRef& M, int what) {
   const int m = blockIdx.x;
   const int tid = threadIdx.x;
   M.a0 = A.mol_ptr[m];

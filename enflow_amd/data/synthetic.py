@@ -59,11 +59,15 @@ def _types(n, rng):
 
 
 def make_molecules(num_mols, n_atoms=22, nf=5, seed=0, r_cut_ang=3.0,
-                   box_ang=None, kelvin=300.0, radius=4.0, min_extent=4.6):
+                   box_ang=None, kelvin=300.0, radius=4.0, min_extent=4.6, chain=False):
     """Return a dict batch: h, g, pos, vel, box [A,3], r_cut [M], mol_ptr [M+1].
 
     ``n_atoms`` is an int or a per-molecule sequence (ragged batch).
+    ``chain=True``: unconfined self-avoiding random walks (BASELINE configs[4]'s
+    long chains) instead of compact ones.
     """
+    if chain:
+        radius = np.inf
     rng = np.random.default_rng(seed)
     sizes = [int(n_atoms)] * num_mols if np.isscalar(n_atoms) else [int(x) for x in n_atoms]
     assert len(sizes) == num_mols

@@ -46,12 +46,13 @@ class ArgMax(nn.Module):
         if N is None:
             N = torch.tensor([n])
         N = torch.as_tensor(N).reshape(-1)
-        # the kernel owns one molecule per workgroup (<= 64 atoms): split a
-        # single big "molecule" into chunks -- log_q is a plain sum over atoms
-        if int(N.max()) > 64:
+        # the kernel owns one molecule per workgroup (<= enflow_max_atoms): split
+        # a single big "molecule" into chunks -- log_q is a plain sum over atoms
+        cap = L.enflow_max_atoms()
+        if int(N.max()) > cap:
             chunks = []
             for c in N.tolist():
-                chunks += [64] * (c // 64) + ([c % 64] if c % 64 else [])
+                chunks += [cap] * (c // cap) + ([c % cap] if c % cap else [])
             N = torch.tensor(chunks)
         ptr = mol_ptr_from_counts(N, device=dev)
         hf = h.detach().to(torch.float32).contiguous()

@@ -1,0 +1,93 @@
+"""GPU parity for large molecules (BASELINE configs[4]: 256-atom chains):
+the row-blocked kernels (pair lists, edge tiles and node phase per block of 32
+rows, leapfrog update after the last block) against the CPU oracle.
+Tolerances as tests/test_gpu_parity.py (1e-5 normwise, integer work exact)."""
+import collections
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import enflow_oracle as O
+from _fixtures import rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda:0"
+SIZES = [256, 131, 40, 256, 3]
+
+
+def _batch(sizes, seed, nf=5):
+    from enflow_amd.data.synthetic import make_molecules
+    b = make_molecules(len(sizes), sizes, nf=nf, seed=seed, chain=True)
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        b[k] = b[k].astype(np.float32).astype(np.float64)
+    return b
+
+
+def _model(hid, nf, n_layers, seed):
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data.synthetic import default_dt
+    torch.manual_seed(seed)
+    return LFIntegrator([EGCL(nf, nf, hid) for _ in range(n_layers)], ArgMax(nf, hid), dt=default_dt()).to(DEV)
+
+
+def test_large_neighbour_pairs_exact():
+    from enflow_amd.data import Data
+    b = _batch(SIZES, 3)
+    e = Data.from_arrays(b, device=DEV).edges
+    got = collections.Counter(zip(e.row.cpu().tolist(), e.col.cpu().tolist()))
+    row, col, _ = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    assert got == collections.Counter(zip(row.tolist(), col.tolist()))
+    assert len(row) > 1000
+
+
+def test_large_egcl_vs_oracle():
+    from enflow_amd.nn import EGCL
+    from enflow_amd.data import Data
+    b = _batch(SIZES, 4)
+    b["h"] = np.random.default_rng(1).normal(size=b["h"].shape).astype(np.float32).astype(np.float64)
+    torch.manual_seed(2)
+    net = EGCL(5, 5, 128).to(DEV)
+    d = Data.from_arrays(b, device=DEV)
+    with torch.no_grad():
+        q, f, g = net(d.h, d.edges)
+    p = {k: v.detach().double().cpu().numpy() for k, v in net.state_dict().items()}
+    row, col, eb = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    rq, rf, rg = O.egcl_forward(p, b["h"], row, col, O.coord_diff(b["pos"], row, col, eb))
+    assert rel_err(q.cpu().numpy(), rq) < TOL
+    assert rel_err(f.cpu().numpy(), rf) < TOL
+    assert rel_err(g.cpu().numpy(), rg) < TOL
+
+
+@pytest.mark.parametrize("prec", ["f32", "f16x3"])
+def test_large_flow_forward_and_roundtrip(prec):
+    from enflow_amd.data import Data
+    b = _batch(SIZES, 5)
+    model = _model(128, 5, 3, 6)
+    model.gemm_precision = prec
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(7))
+    with torch.no_grad():
+        o, ldj = model(d, noise=noise)
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    dq = {k: v.detach().cpu().double().numpy() for k, v in model.dequantize.state_dict().items()}
+    ref, ref_ldj = O.lf_forward(layers, dq, b, noise.cpu().double().numpy(), model.dt)
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
+    with torch.no_grad():
+        back = model.reverse(o)
+    np.testing.assert_array_equal(np.argmax(back.h.cpu().numpy(), 1), np.argmax(b["h"], 1))
+    assert rel_err(back.vel.cpu().numpy(), b["vel"]) < 1e-4
+
+
+def test_large_training_is_rejected_cleanly():
+    """The training backward keeps whole-molecule pair lists (<= 64 atoms)."""
+    from enflow_amd.data import Data
+    from enflow_amd import _lib
+    b = _batch([100, 22], 8)
+    model = _model(32, 5, 1, 9)
+    with pytest.raises(_lib.HipPathError):
+        model(Data.from_arrays(b, device=DEV))

@@ -210,7 +210,7 @@ def test_too_large_molecule_raises():
     from enflow_amd.data.synthetic import make_molecules
     from enflow_amd import _lib
     model = _make_model(32, 5, 1, 0, 0.01)
-    d = Data.from_arrays(make_molecules(1, 65, seed=0), device=DEV)
+    d = Data.from_arrays(make_molecules(1, 257, seed=0, chain=True), device=DEV)
     with pytest.raises(_lib.HipPathError):
         with torch.no_grad():
             model(d)

@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 def test_abi_queries():
     L = _lib.lib()
     assert L.enflow_abi_version() == 2
-    assert L.enflow_max_atoms() == 64
+    assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
         assert L.enflow_supports_hidden(h) == 1
@@ -48,7 +48,7 @@ def test_abi_queries():
 def test_argument_errors_launch_nothing():
     L = _lib.lib()
     # too-large molecule, bad hidden width, bad nf: rejected before any launch
-    args = [1, 100, 100, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 6 + [1, None]
+    args = [1, 300, 300, 5, 128] + [None] * 8 + [1, 1, None, None, 0.0, 0.1, 1.0] + [None] * 6 + [1, None]
     assert L.enflow_lf_forward_f32(*args) == -3
     args[2], args[4] = 20, 96
     assert L.enflow_lf_forward_f32(*args) == -5
