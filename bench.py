@@ -43,14 +43,28 @@ def flops_per_launch(pairs, atoms, layers, hid, nf):
     return pairs * per_pair + atoms * layers * per_atom_layer + atoms * per_atom_dq
 
 
-def build_workload(rank, device):
+# per-mode workload (BASELINE.json configs): molecules/GPU, atoms, layers,
+# direction, GEMM precision, chain geometry, metric
+MODES = {
+    "forward": dict(mols=MOLS_PER_GPU, atoms=ATOMS, layers=LAYERS, reverse=False, prec="f16x3", chain=False,
+                    metric=METRIC, unit="molecule-transforms/s"),
+    "generate": dict(mols=1024, atoms=22, layers=8, reverse=True, prec="bf16", chain=False,
+                     metric="molecule-generations/sec (reverse/generate path, bf16), batch 1024×22 atoms",
+                     unit="molecule-generations/s"),
+    "chain": dict(mols=512, atoms=256, layers=16, reverse=False, prec="f16x3", chain=True,
+                  metric="molecule-transforms/sec (fwd+log|detJ|), 512×256-atom chains, 16 layers",
+                  unit="molecule-transforms/s"),
+}
+
+
+def build_workload(rank, device, mols=MOLS_PER_GPU, atoms=ATOMS, layers=LAYERS, chain=False):
     from enflow_amd.data.synthetic import make_molecules, default_dt
     from enflow_amd.nn import EGCL, ArgMax
     from enflow_amd.flow import LFIntegrator
     from enflow_amd.utils.helpers import mol_ptr_from_counts
-    b = make_molecules(MOLS_PER_GPU, ATOMS, nf=NF, seed=1000 + rank)
+    b = make_molecules(mols, atoms, nf=NF, seed=1000 + rank, chain=chain)
     torch.manual_seed(0)                    # same (random-init) weights on every rank
-    model = LFIntegrator([EGCL(NF, NF, HID) for _ in range(LAYERS)], ArgMax(NF, HID),
+    model = LFIntegrator([EGCL(NF, NF, HID) for _ in range(layers)], ArgMax(NF, HID),
                          dt=default_dt()).to(device)
     f = lambda k: torch.tensor(b[k], dtype=torch.float32, device=device).contiguous()  # noqa: E731
     inp = {k: f(k) for k in ("h", "g", "pos", "vel", "box", "r_cut")}
@@ -101,8 +115,11 @@ def load_traffic():
     return None
 
 
-def workload_name():
-    return f"lf_forward_{MOLS_PER_GPU}x{ATOMS}_L{LAYERS}_H{HID}_nf{NF}_f32"
+def workload_name(mode="forward"):
+    c = MODES[mode]
+    kind = "reverse" if c["reverse"] else "forward"
+    geo = "chain" if c["chain"] else ""
+    return f"lf_{kind}_{c['mols']}x{c['atoms']}{geo}_L{c['layers']}_H{HID}_nf{NF}_f32"
 
 
 TRAIN_METRIC = "molecule-train-steps/sec (fwd+NLL+bwd+Adam, RCCL grad all-reduce), batch 1024×64 atoms per GPU"
@@ -211,8 +228,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1536)
-    ap.add_argument("--mode", choices=("forward", "train"), default="forward",
-                    help="forward: the headline metric (configs[1]); train: configs[3] per GPU")
+    ap.add_argument("--mode", choices=("forward", "generate", "chain", "train"), default="forward",
+                    help="forward: the headline metric (configs[1]); generate: configs[2] (bf16 reverse); "
+                         "chain: configs[4] (256-atom chains, 16 layers); train: configs[3] per GPU")
     ap.add_argument("--atoms", type=int, default=None, help="train mode: atoms per molecule (default 64)")
     args = ap.parse_args()
 
@@ -233,31 +251,52 @@ def main():
             dist.destroy_process_group()
         return
 
-    b, model, inp = build_workload(rank, device)
+    c = MODES[args.mode]
+    mols, atoms, layers = c["mols"], c["atoms"], c["layers"]
+    b, model, inp = build_workload(rank, device, mols, atoms, layers, c["chain"])
+    model.gemm_precision = c["prec"]
     n_atoms = inp["h"].shape[0]
     work = {k: torch.empty_like(inp[k]) for k in ("h", "g", "pos", "vel")}
     noise = torch.empty_like(inp["h"])
-    ldj_mol = torch.empty(MOLS_PER_GPU, dtype=torch.float32, device=device)
+    ldj_mol = torch.empty(mols, dtype=torch.float32, device=device)
     ldj = torch.empty(1, dtype=torch.float32, device=device)
     err = torch.zeros(1, dtype=torch.int32, device=device)
     stats = torch.zeros(2, dtype=torch.int64, device=device)
+    idx = torch.empty(n_atoms, dtype=torch.int32, device=device)
+    mx = torch.zeros(1, dtype=torch.int32, device=device)
+    onehot = torch.empty((n_atoms, NF), dtype=torch.float32, device=device)
     model.packed_layers(device)
     model.dequantize.packed(device)
     gen = torch.Generator(device).manual_seed(rank)
+    from enflow_amd import _lib as L_
+    Lh = L_.lib()
 
-    def step(st=None):
+    def fwd(st=None):
         for k in work:
             work[k].copy_(inp[k])
         torch.randn(noise.shape, generator=gen, out=noise)
         model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
-                              inp["mol_ptr"], ATOMS, noise, ldj_mol, ldj, err, st)
+                              inp["mol_ptr"], atoms, noise, ldj_mol, ldj, err, st)
 
-    # one counted run: pair statistics for the roofline's algorithmic FLOPs
-    step(stats)
+    # one counted forward: pair statistics for the roofline's algorithmic FLOPs
+    fwd(stats)
     torch.cuda.synchronize()
     pairs, edges = (int(x) for x in stats.tolist())
     if int(err.item()) != 0:
         raise RuntimeError(f"flow kernel error flag {int(err.item())}")
+    if c["reverse"]:
+        # generate direction: invert a forward output (main.py:263-278)
+        gsrc = {k: work[k].clone() for k in work}
+
+        def step():
+            for k in work:
+                work[k].copy_(gsrc[k])
+            model.reverse_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                                  inp["mol_ptr"], atoms, idx, mx, err)
+            L_.check(Lh.enflow_one_hot_f32(L_.ptr(idx), n_atoms, NF, L_.ptr(onehot), L_.stream_ptr(device)),
+                     "one_hot")
+    else:
+        step = fwd
 
     for _ in range(args.warmup):
         step()
@@ -281,25 +320,33 @@ def main():
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     for e0, e1 in evs:
         for k in work:
-            work[k].copy_(inp[k])
-        torch.randn(noise.shape, generator=gen, out=noise)
-        e0.record(stream)
-        model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
-                              inp["mol_ptr"], ATOMS, noise, ldj_mol, ldj, err)
-        e1.record(stream)
+            work[k].copy_(gsrc[k] if c["reverse"] else inp[k])
+        if c["reverse"]:
+            e0.record(stream)
+            model.reverse_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                                  inp["mol_ptr"], atoms, idx, mx, err)
+            e1.record(stream)
+        else:
+            torch.randn(noise.shape, generator=gen, out=noise)
+            e0.record(stream)
+            model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                                  inp["mol_ptr"], atoms, noise, ldj_mol, ldj, err)
+            e1.record(stream)
     torch.cuda.synchronize()
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
 
     if rank == 0:
-        from enflow_amd import _lib as L_
         prec_id = L_.PRECISIONS[model.gemm_precision]
-        total_mols = MOLS_PER_GPU * world * args.steps
-        flops = flops_per_launch(pairs, n_atoms, LAYERS, HID, NF)
+        total_mols = mols * world * args.steps
+        flops = flops_per_launch(pairs, n_atoms, layers, HID, NF)
+        if c["reverse"]:
+            flops -= n_atoms * (2 * HID * NF + 2 * HID * 2 * NF)     # no ArgMax network in reverse
         achieved = flops / (kern_ms * 1e-3) / 1e12
+        nmax = 32 if atoms <= 32 else (64 if atoms <= 64 else 256)
         line = {
-            "metric": METRIC,
+            "metric": c["metric"],
             "value": total_mols / elapsed,
-            "unit": "molecule-transforms/s",
+            "unit": c["unit"],
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -307,16 +354,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (random-walk 22-atom molecules, random-init weights)",
-            "config": {"workload": workload_name(), "molecules_per_gpu": MOLS_PER_GPU,
-                       "atoms_per_molecule": ATOMS, "coupling_layers": LAYERS, "hidden_nf": HID,
-                       "node_nf": NF, "global_batch": MOLS_PER_GPU * world,
+            "dtype": "bf16" if c["prec"] == "bf16" else "f32",
+            "data": f"synthetic (random-walk {atoms}-atom {'chains' if c['chain'] else 'molecules'}, "
+                    f"random-init weights)",
+            "config": {"workload": workload_name(args.mode), "molecules_per_gpu": mols,
+                       "atoms_per_molecule": atoms, "coupling_layers": layers, "hidden_nf": HID,
+                       "node_nf": NF, "global_batch": mols * world,
                        "parallelism": f"molecule-sharded x{world}",
                        "unique_pairs_per_launch": pairs, "reference_edges_per_launch": edges},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS,
                          "unit": "TFLOP/s", "frac": achieved / PEAK_F32_MFMA_TFLOPS,
-                         "traffic": load_traffic(), "kernel": f"lf_flow_kernel<128,32,false,{prec_id}>",
+                         "traffic": load_traffic() if args.mode == "forward" else None,
+                         "kernel": f"lf_flow_kernel<128,{nmax},{str(c['reverse']).lower()},{prec_id}>",
                          "kernel_ms": kern_ms, "flops_per_launch": flops,
                          "gemm_precision": model.gemm_precision,
                          "note": "achieved = fp32-equivalent algorithmic FLOPs / event-timed launch; peak = dense "
@@ -324,7 +373,7 @@ def main():
                                  "split-fp16 products on the f16 MFMA pipe (see DESIGN.md)"},
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.mode == "forward":
             line["cpu_baseline"] = cpu_baseline(args.cpu_sample)
         print(json.dumps(line), flush=True)
     if dist:

@@ -129,6 +129,20 @@ class LFIntegrator(BaseFlow):
             _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), self._prec(),
             _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
 
+    def reverse_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, argmax_idx, max_idx, err):
+        """In-place fused reverse on preallocated fp32 device buffers (no host
+        sync, no allocation); with ArgMax, argmax_idx / max_idx receive the
+        dequantiser's indices (enflow_one_hot_f32 materialises the one-hot)."""
+        hid, nf, cw = self._geometry()
+        kind = self._dequant_kind()
+        L = _lib.lib()
+        _lib.check(L.enflow_lf_reverse_f32(
+            mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
+            _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
+            _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
+            _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), self._prec(), _lib.stream_ptr(h.device)),
+            "enflow_lf_reverse_f32")
+
     def _state(self, data):
         _lib.require_gpu(data.pos)
         dev = data.pos.device
