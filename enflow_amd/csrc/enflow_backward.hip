@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 
   // ---- edge chain backward, one 32-pair tile per wave step (egcl.py:57-74, 76-89)
   {
-    const int lane = tid & 63, w = tid >> 6;
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
     const int j = lane & 31, hh = lane >> 5;
     const int P = sm.npairs;
     const int TT = (P + 31) >> 5;

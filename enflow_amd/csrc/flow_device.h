@@ -729,7 +729,7 @@ __device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const M
   int local = 0;
   for (int e = e0; e < e1; ++e) local += sm.u.C[e] > 0;
   const int incl = wave_incl_scan(local);
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
   if (lane == 63) sm.scan[w] = incl;
   __syncthreads();
   int base = incl - local;
@@ -765,7 +765,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
                                            const MolRef& M, int nf, int tid, int r0, int rb STAMP_ARGS) {
   constexpr int NT = H / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
   const int j = lane & 31, hh = lane >> 5;
   const int P = sm.npairs;
   const int T = (P + 31) >> 5;
@@ -1025,7 +1025,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
   constexpr int NT = H / 32;
   constexpr int NA = RB / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
   const int j = lane & 31, hh = lane >> 5;
   const int nh = (nf + 1) >> 1;
   const rsrc_t W = weights_rsrc(Lp, L.total);
@@ -1045,8 +1045,8 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const int f0 = 32 * tp + 8 * g4 + 4 * hh;
-      const f32x4 b1 = bload4(W, 0, (L.bv1 + f0) * 4);
-      const f32x4 w2 = bload4(W, 0, (L.wv2 + f0) * 4);
+      const f32x4 b1 = bload4(W, (f0 - 32 * tp) * 4, (L.bv1 + 32 * tp) * 4);   // lane part in voffset
+      const f32x4 w2 = bload4(W, (f0 - 32 * tp) * 4, (L.wv2 + 32 * tp) * 4);
 #pragma unroll
       for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(acc[4 * g4 + u] + b1[u]);
     }
@@ -1070,7 +1070,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
     }
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b1 = bload4(W, 0, (L.bn1 + 32 * tp + 8 * g4 + 4 * hh) * 4);
+      const f32x4 b1 = bload4(W, (8 * g4 + 4 * hh) * 4, (L.bn1 + 32 * tp) * 4);
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(acc[4 * g4 + u] + b1[u]);
     }
@@ -1103,7 +1103,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
   constexpr int NA = RB / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
   constexpr int KS = H / 16;
-  const int lane = tid & 63, w = tid >> 6;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
   const int j = lane & 31, hh = lane >> 5;
   const rsrc_t W = weights_rsrc(Lp, L.total);
   const float inv_v1 = Lp[L.scl + 7], inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
@@ -1139,8 +1139,8 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const int f0 = 32 * tp + 8 * g4 + 4 * hh;
-      const f32x4 b1 = bload4(W, 0, (L.bv1 + f0) * 4);
-      const f32x4 w2 = bload4(W, 0, (L.wv2 + f0) * 4);
+      const f32x4 b1 = bload4(W, (f0 - 32 * tp) * 4, (L.bv1 + 32 * tp) * 4);   // lane part in voffset
+      const f32x4 w2 = bload4(W, (f0 - 32 * tp) * 4, (L.wv2 + 32 * tp) * 4);
 #pragma unroll
       for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(acc[4 * g4 + u], inv_v1, b1[u]));
     }
@@ -1172,7 +1172,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     }
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b1 = bload4(W, 0, (L.bn1 + 32 * tp + 8 * g4 + 4 * hh) * 4);
+      const f32x4 b1 = bload4(W, (8 * g4 + 4 * hh) * 4, (L.bn1 + 32 * tp) * 4);
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
     }
