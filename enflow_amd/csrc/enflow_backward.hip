@@ -47,10 +47,33 @@ __global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int n
       const int u = e & 3, lane = (e >> 2) & 63, rg = (e >> 8) & 3, tp = e >> 10;
       const int q = lane & 31, k = 32 * tp + rho(4 * rg + u, lane >> 5);
       if (q < K1) v = raw[R.We1 + k * K1 + q];
+    } else if (idx >= L.scl && idx < L.scl + 16) {
+      continue;                             // written by egcl_bwd_scale_kernel
+    } else if (idx >= L.we2Tx && idx < L.we1Tx) {   // F16X3 W^T chain fragments [tp][t][s][lane][hi|lo]
+      const bool c1 = idx >= L.wc1Tx;
+      const int e = idx - (c1 ? L.wc1Tx : L.we2Tx);
+      const int d = e & 7, lane = (e >> 3) & 63, rest = e >> 9;
+      const int sstep = rest & 1, t = (rest >> 1) % NT, tp = (rest >> 1) / NT;
+      const float sc = out[L.scl + (c1 ? 2 : 0)];
+      const int row = 32 * tp + (lane & 31);
+      const int j0 = 2 * (d & 3);
+      const int col0 = 32 * t + rho(8 * sstep + j0, lane >> 5), col1 = 32 * t + rho(8 * sstep + j0 + 1, lane >> 5);
+      const int Wo = c1 ? R.Wc1 : R.We2;
+      v = __builtin_bit_cast(float, f16_split_bits(raw[Wo + col0 * H + row] * sc, raw[Wo + col1 * H + row] * sc, d >= 4));
+    } else if (idx >= L.we1Tx && idx < L.we1Tx + NT * 2 * 512) {   // F16X3 edge_nn.0^T [tp][s][lane][hi|lo]
+      const int e = idx - L.we1Tx;
+      const int d = e & 7, lane = (e >> 3) & 63, blk = e >> 9;
+      const int tp = blk >> 1, s2 = blk & 1;
+      const float sc = out[L.scl + 4];
+      const int q = lane & 31, j0 = 2 * (d & 3);
+      const int k0 = 32 * tp + rho(8 * s2 + j0, lane >> 5), k1 = 32 * tp + rho(8 * s2 + j0 + 1, lane >> 5);
+      const float w0 = q < K1 ? raw[R.We1 + k0 * K1 + q] * sc : 0.f;
+      const float w1 = q < K1 ? raw[R.We1 + k1 * K1 + q] * sc : 0.f;
+      v = __builtin_bit_cast(float, f16_split_bits(w0, w1, d >= 4));
     } else if (idx < L.wn1T) {              // wv1T[f][k]
       const int e = idx - L.wv1T, f = e / H, k = e % H;
       if (f < nf) v = raw[R.Wv1 + k * nf + f];
-    } else {                                // wn1T[f][k]
+    } else if (idx < L.scl) {               // wn1T[f][k]
       const int e = idx - L.wn1T, f = e / H, k = e % H;
       if (f < NFMAX) {
         if (f < nf) v = raw[R.Wn1 + k * (H + nf) + f];
@@ -60,6 +83,11 @@ __global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int n
     }
     out[idx] = v;
   }
+}
+
+__global__ void __launch_bounds__(256) egcl_bwd_scale_kernel(const float* __restrict__ raw, int H, int nf,
+                                                             float* __restrict__ out) {
+  egcl_scales_block(raw, H, nf, out + egcl_bwd_layout(H).scl);
 }
 
 __device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -109,11 +137,40 @@ struct BwdSmem {
   float au[NMAX * (H + 1)], an[NMAX * (H + 1)];
 };
 
+// Adjoint tiles span many decades (coord_nn.2 starts at gain 0.001), so before
+// an F16X3 product their values are scaled by a power of two that puts the
+// tile's max |x| in [2^12, 2^13): hi / lo parts stay normal fp16.  Returns the
+// exact inverse scale.
+template <int NT>
+__device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
+  float m = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(X[t][r]));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  int ex = 0;
+  if (m > 0.f && isfinite(m)) {
+    frexpf(m, &ex);
+    ex = 13 - ex;
+    ex = ex > 100 ? 100 : (ex < -100 ? -100 : ex);
+  }
+  const float s = ldexpf(1.f, ex);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) X[t] *= s;
+  return ldexpf(1.f, -ex);
+}
+
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
-template <int H, int NMAX>
+#ifndef ENFLOW_BWD_PREC
+#define ENFLOW_BWD_PREC PREC_F16X3
+#endif
+template <int H, int NMAX, int PREC = ENFLOW_BWD_PREC>
 __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
+  static_assert(PREC == PREC_F32 || PREC == PREC_F16X3, "backward: fp32-accurate precisions only");
   __shared__ BwdSmem<H, NMAX> sb;
   Smem<H, NMAX>& sm = sb.f;
   constexpr int NT = H / 32;
@@ -260,6 +317,11 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const rsrc_t WB = weights_rsrc(B.Bp, LB.total);
     const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
     const size_t prow0 = (size_t)B.pair_off[m];
+    const bool x3 = PREC == PREC_F16X3;
+    const float inv1 = x3 ? B.Lp[L.scl + 1] : 1.f;   // edge_nn.2 / coord_nn.0 / edge_nn.0 (and ^T)
+    const float inv2 = x3 ? B.Lp[L.scl + 3] : 1.f;
+    const float inv0 = x3 ? B.Lp[L.scl + 5] : 1.f;
+    auto nofill = [](int) {};
     for (int tile = t0; tile < t1; ++tile) {
       const int p = tile * 32 + j;
       const bool valid = p < P;
@@ -293,13 +355,42 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       f32x16 x0[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
+      if constexpr (PREC == PREC_F16X3) {
+        const int ks_n = (2 * nf + 1 + 15) >> 4;
+        for (int ks = 0; ks < ks_n; ++ks) {
+          f32x16 in;
 #pragma unroll
-      for (int s = 0; s < NFMAX + 1; ++s) {
-        const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh]
-                      : (s < NFMAX ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : (hh == 0 ? radial : 0.f));
+          for (int jj = 0; jj < 8; ++jj) {
+            const int k = 16 * ks + 8 * hh + jj;
+            float v = 0.f;
+            if (k < nf) v = sm.h[i * NFP + k];
+            else if (k < 2 * nf) v = sm.h[jl * NFP + k - nf];
+            else if (k == 2 * nf) v = radial;
+            in[jj] = v;
+          }
+          f16x8 bh, bl;
+          split_f16(in, 0, bh, bl);
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
-          x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
+          for (int t = 0; t < NT; ++t) {
+            const int so = (L.we1x + (t * 2 + ks) * 512) * 4;
+            const f32x4 ah = bload4(W, lane * 32, so), al = bload4(W, lane * 32 + 16, so);
+            x0[t] = mfma_f16(ah, bh, x0[t]);
+            x0[t] = mfma_f16(ah, bl, x0[t]);
+            x0[t] = mfma_f16(al, bh, x0[t]);
+          }
+        }
+        const float inv0 = B.Lp[L.scl + 5];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) x0[t] *= inv0;
+      } else {
+#pragma unroll
+        for (int s = 0; s < NFMAX + 1; ++s) {
+          const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh]
+                        : (s < NFMAX ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : (hh == 0 ? radial : 0.f));
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+            x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
+        }
       }
       // x1 = silu(pre0) (kept: B operand of GEMM1), silu'(pre0) parked in the dp0 row
 #pragma unroll
@@ -324,7 +415,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       f32x16 ev[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) ev[t] = (f32x16)0.f;
-      chain_gemm<NT>(W, L.we2f, x0, ev, lane);
+      chain_prec_fill<PREC, NT, 1>(W, L.we2f, L.we2x, L.we2b, x0, ev, lane, nofill);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -334,7 +425,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           f32x4 xv, dv;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const float z = ev[t][4 * g4 + u] + b[u];
+            const float z = fmaf(ev[t][4 * g4 + u], inv1, b[u]);
             const float s = sigmoid_f(z);
             xv[u] = z * s;
             dv[u] = s * (1.f + z * (1.f - s));
@@ -347,7 +438,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       f32x16 cv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) cv[t] = (f32x16)0.f;
-      chain_gemm<NT>(W, L.wc1f, ev, cv, lane);
+      chain_prec_fill<PREC, NT, 1>(W, L.wc1f, L.wc1x, L.wc1b, ev, cv, lane, nofill);
       float part = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -359,7 +450,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           f32x4 sv;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            const float z = cv[t][4 * g4 + u] + b[u];
+            const float z = fmaf(cv[t][4 * g4 + u], inv2, b[u]);
             const float s = sigmoid_f(z);
             sv[u] = z * s;
             part = fmaf(w2[u], sv[u], part);
@@ -392,10 +483,15 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       // GEMM3: d e = c * d agg[i] + coord_nn.0.weight^T d pre(coord_nn.0)
       f32x16 ae[NT];
 #pragma unroll
+      for (int t = 0; t < NT; ++t) ae[t] = (f32x16)0.f;
+      float sc3 = 1.f;
+      if constexpr (PREC == PREC_F16X3) sc3 = tile_pow2_scale(cv);   // cv already stored unscaled
+      chain_prec_fill<PREC, NT, 1>(WB, LB.wc1T, LB.wc1Tx, 0, cv, ae, lane, nofill);
+      const float u3 = inv2 * sc3;
+#pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) ae[t][r] = c * sm.agg[i * AST + 32 * t + rho(r, hh)];
-      chain_gemm<NT>(WB, LB.wc1T, cv, ae, lane);
+        for (int r = 0; r < 16; ++r) ae[t][r] = fmaf(ae[t][r], u3, c * sm.agg[i * AST + 32 * t + rho(r, hh)]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parked silu' rows written by this lane
       // d pre(edge_nn.2) = d e * silu'(pre_e)
 #pragma unroll
@@ -416,7 +512,10 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       f32x16 ax[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) ax[t] = (f32x16)0.f;
-      chain_gemm<NT>(WB, LB.we2T, ae, ax, lane);
+      float sc4 = 1.f;
+      if constexpr (PREC == PREC_F16X3) sc4 = tile_pow2_scale(ae);   // ae already stored unscaled
+      chain_prec_fill<PREC, NT, 1>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, nofill);
+      const float u4 = inv1 * sc4;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -426,21 +525,38 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           f32x4 av;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            av[u] = ax[t][4 * g4 + u] * dv[u];
+            av[u] = ax[t][4 * g4 + u] * u4 * dv[u];
             ax[t][4 * g4 + u] = av[u];
           }
           st4(B.dp0 + Rw * H + f0, av);
         }
       // GEMM5: d [h_i, h_j, radial] = edge_nn.0.weight^T d pre0   (rows q < 2nf+1)
       f32x16 ain = (f32x16)0.f;
+      if constexpr (PREC == PREC_F16X3) {
+        const float sc5 = tile_pow2_scale(ax);   // ax already stored unscaled
 #pragma unroll
-      for (int tp = 0; tp < NT; ++tp)
+        for (int tp = 0; tp < NT; ++tp)
 #pragma unroll
-        for (int rg = 0; rg < 4; ++rg) {
-          const f32x4 a4 = bload4(WB, lane * 16, (LB.we1T + (tp * 4 + rg) * 256) * 4);
+          for (int s2 = 0; s2 < 2; ++s2) {
+            const int so = (LB.we1Tx + (tp * 2 + s2) * 512) * 4;
+            const f32x4 gh = bload4(WB, lane * 32, so), gl = bload4(WB, lane * 32 + 16, so);
+            f16x8 bh, bl;
+            split_f16(ax[tp], s2, bh, bl);
+            ain = mfma_f16(gh, bh, ain);
+            ain = mfma_f16(gh, bl, ain);
+            ain = mfma_f16(gl, bh, ain);
+          }
+        ain *= inv0 * sc5;
+      } else {
 #pragma unroll
-          for (int u = 0; u < 4; ++u) ain = mfma32(a4[u], ax[tp][4 * rg + u], ain);
-        }
+        for (int tp = 0; tp < NT; ++tp)
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            const f32x4 a4 = bload4(WB, lane * 16, (LB.we1T + (tp * 4 + rg) * 256) * 4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) ain = mfma32(a4[u], ax[tp][4 * rg + u], ain);
+          }
+      }
       float arad = 0.f;
       if (valid) {
 #pragma unroll
@@ -901,6 +1017,7 @@ int64_t enflow_egcl_bwd_packed_size(int H, int nf) {
 int enflow_pack_egcl_bwd_f32(const float* raw, int H, int nf, float* packed, void* stream) {
   if (!hid_ok_b(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
   const int total = egcl_bwd_layout(H).total;
+  hipLaunchKernelGGL(egcl_bwd_scale_kernel, dim3(1), dim3(256), 0, SB(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, SB(stream), raw, H, nf, packed);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -171,40 +171,10 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
   }
 }
 
-// Power-of-two scales for the F16X3 fragments (edge_nn.2, coord_nn.0, edge_nn.0,
-// vel_scaling_nn.0, node_nn.0, node_nn.2):
-// 2^s with max|W| 2^s in (2^13, 2^14], so hi parts stay far below the fp16
-// maximum and lo parts of typical weights stay normal.  One block.
+// Power-of-two scales of the F16X3 fragments (egcl_scales_block, flow_device.h). One block.
 __global__ void __launch_bounds__(256) egcl_scale_kernel(const float* __restrict__ raw, int H, int nf,
                                                          float* __restrict__ out) {
-  const EgclLayout L = egcl_layout(H, nf);
-  const RawEgcl R = raw_egcl(H, nf);
-  // matrices (in scl slot order): edge_nn.2, coord_nn.0, edge_nn.0, vel_scaling_nn.0, node_nn.0, node_nn.2
-  const int off[6] = {R.We2, R.Wc1, R.We1, R.Wv1, R.Wn1, R.Wn2};
-  const int cnt[6] = {H * H, H * H, H * (2 * nf + 1), H * nf, H * (H + nf), nf * H};
-  __shared__ float red[6][256];
-  for (int k = 0; k < 6; ++k) {
-    float mx = 0.f;
-    for (int i = threadIdx.x; i < cnt[k]; i += 256) mx = fmaxf(mx, fabsf(raw[off[k] + i]));
-    red[k][threadIdx.x] = mx;
-  }
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o)
-      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + o]);
-    __syncthreads();
-  }
-  if (threadIdx.x < 6) {
-    const float mx = red[threadIdx.x][0];
-    int ex = 0;
-    if (mx > 0.f && isfinite(mx)) {
-      frexpf(mx, &ex);              // mx = f 2^ex, f in [0.5, 1)
-      ex = 14 - ex;                 // mx 2^(14 - ex) in [2^13, 2^14)
-      ex = ex > 60 ? 60 : (ex < -60 ? -60 : ex);
-    }
-    out[L.scl + 2 * threadIdx.x] = ldexpf(1.f, ex);
-    out[L.scl + 2 * threadIdx.x + 1] = ldexpf(1.f, -ex);
-  }
+  egcl_scales_block(raw, H, nf, out + egcl_layout(H, nf).scl);
 }
 
 __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
@@ -236,6 +206,11 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
   const EgclLayout L = egcl_layout(H, nf);
   constexpr int AST = Smem<H, NMAX, RB>::AST;
   float ldj = 0.f;
+  // per-atom pbc box (Data.pbc, base.py): LDS image, or global memory when blocked
+  auto pbox = [&](int a, int d) {
+    if constexpr (BLOCKED) return A.box[((size_t)M.a0 + a) * 3 + d];
+    else return sm.boxa[a * 3 + d];
+  };
 
   if (!REV) {
     if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
@@ -264,24 +239,38 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
       for (int a = tid; a < n; a += BLOCK) {
         for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] -= sm.g[a * NFP + q] * A.dt;
         for (int d = 0; d < 3; ++d)
-          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, sm.boxa[a * 3 + d]);
+          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, pbox(a, d));
       }
       __syncthreads();
     }
     if (!(ENFLOW_ABLATE & 1) || it == 0) build_images(sm, Ml, tid_l);
     int npairs_layer = 0;
     auto block_pass = [&](const int r0, const int rb) {
-      if (!(ENFLOW_ABLATE & 1) || it == 0) build_block_pairs(sm, Ml, tid_l, r0, rb);
+      int tot;
+      if constexpr (BLOCKED) {
+        block_counts(sm, Ml, tid_l, r0, rb);
+        tot = block_compact(sm, n, tid_l, rb, 0);
+      } else {
+        if (!(ENFLOW_ABLATE & 1) || it == 0) build_block_pairs(sm, Ml, tid_l, r0, rb);
+        tot = sm.npairs;
+      }
       STAMP(2);
-      npairs_layer += sm.npairs;
+      npairs_layer += tot;
       if (A.stats != nullptr && tid == 0) {
         unsigned long long edges = 0;
         for (int a = 0; a < rb; ++a) edges += (unsigned long long)sm.cntrow[r0 + a];
-        atomicAdd(&A.stats[0], (unsigned long long)sm.npairs);
+        atomicAdd(&A.stats[0], (unsigned long long)tot);
         atomicAdd(&A.stats[1], edges);
       }
       STAMP(3);
-      edge_tiles<H, NMAX, RB, PREC>(sm, Lp, L, Ml, nf, tid_l, r0, rb STAMP_PASS);
+      edge_tiles<H, NMAX, RB, PREC>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS);
+      if constexpr (BLOCKED) {   // blocks with more pairs than the buffer: further passes
+        constexpr int PC = Smem<H, NMAX, RB>::PC;
+        for (int p0 = PC; p0 < tot; p0 += PC) {
+          block_compact(sm, n, tid_l, rb, p0);
+          edge_tiles<H, NMAX, RB, PREC>(sm, Lp, L, Ml, nf, tid_l, r0, rb, false STAMP_PASS);
+        }
+      }
       STAMP(4);
       if (!(ENFLOW_ABLATE & 2)) {
         if constexpr (PREC == PREC_F16X3) node_phase_x3(sm, Lp, L, n, nf, tid_l, r0, rb);
@@ -335,7 +324,7 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
           const float F = force(d);
           const float v = eq * sm.vel[a * 3 + d] + F * A.dt;
           sm.vel[a * 3 + d] = v;
-          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, sm.boxa[a * 3 + d]);
+          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, pbox(a, d));
         }
         for (int qf = 0; qf < nf; ++qf) {
           const float gn = sm.g[a * NFP + qf] + sm.G[a * NFP + qf] * A.dt;
@@ -403,10 +392,16 @@ __global__ void __launch_bounds__(BLOCK, 2) egcl_forward_kernel(FlowArgs A, floa
 #ifdef ENFLOW_STAMPS
   STAMP_DECL
 #endif
+  constexpr int PC = Smem<H, NMAX, RB>::PC;
   for (int r0 = 0; r0 < n; r0 += RB) {
     const int rb = min(RB, n - r0);
-    build_block_pairs(sm, M, tid, r0, rb);
-    edge_tiles(sm, A.layers, L, M, nf, tid, r0, rb STAMP_PASS);
+    block_counts(sm, M, tid, r0, rb);
+    const int tot = block_compact(sm, n, tid, rb, 0);
+    edge_tiles(sm, A.layers, L, M, nf, tid, r0, rb, true STAMP_PASS);
+    for (int p0 = PC; p0 < tot; p0 += PC) {   // blocks with more pairs than the buffer
+      block_compact(sm, n, tid, rb, p0);
+      edge_tiles(sm, A.layers, L, M, nf, tid, r0, rb, false STAMP_PASS);
+    }
     node_phase(sm, A.layers, L, n, nf, tid, r0, rb);
     for (int a = tid; a < rb; a += BLOCK) {
       const int ag = r0 + a;
@@ -444,17 +439,22 @@ __global__ void __launch_bounds__(BLOCK) neighbour_pairs_kernel(FlowArgs A, int 
   MolRef M;
   if (!load_molecule(sm, A, M, LOAD_POS)) return;
   build_images(sm, M, (int)threadIdx.x);
+  constexpr int PC = Smem<32, NMAX, RB>::PC;
   int off = 0;
   for (int r0 = 0; r0 < M.n; r0 += RB) {
     const int rb = min(RB, M.n - r0);
-    build_block_pairs(sm, M, (int)threadIdx.x, r0, rb);
-    const int P = sm.npairs;
-    for (int p = threadIdx.x; p < P && off + p < max_pairs; p += BLOCK) {
-      const uint32_t pr = sm.pairs[p];
-      pairs[(size_t)blockIdx.x * max_pairs + off + p] = (pr & ~0xffu) | (uint32_t)(r0 + (int)(pr & 0xffu));
+    block_counts(sm, M, (int)threadIdx.x, r0, rb);
+    int tot = 0;
+    for (int p0 = 0; p0 == 0 || p0 < tot; p0 += PC) {   // compaction passes of PC pairs
+      tot = block_compact(sm, M.n, (int)threadIdx.x, rb, p0);
+      const int P = sm.npairs;
+      for (int p = threadIdx.x; p < P && off + p < max_pairs; p += BLOCK) {
+        const uint32_t pr = sm.pairs[p];
+        pairs[(size_t)blockIdx.x * max_pairs + off + p] = (pr & ~0xffu) | (uint32_t)(r0 + (int)(pr & 0xffu));
+      }
+      off += P;
+      __syncthreads();
     }
-    off += P;
-    __syncthreads();
   }
   if (threadIdx.x == 0) {
     count[blockIdx.x] = off;

@@ -121,7 +121,7 @@ __host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
 // Backward-only packed EGCL section (floats): transposed fragments for the
 // adjoint GEMMs of the edge chain and k-contiguous node weights for the VALU
 // node backward (threads over hidden units k read coalesced rows).
-struct EgclBwdLayout { int we2T, wc1T, we1T, wv1T, wn1T, total; };
+struct EgclBwdLayout { int we2T, wc1T, we1T, wv1T, wn1T, scl, we2Tx, wc1Tx, we1Tx, total; };
 __host__ __device__ inline EgclBwdLayout egcl_bwd_layout(int H) {
   const int NT = H / 32;
   EgclBwdLayout L;
@@ -131,6 +131,11 @@ __host__ __device__ inline EgclBwdLayout egcl_bwd_layout(int H) {
   L.we1T = o; o += NT * 4 * 256;      // [tp][rg][lane][4]: A[q][k] = edge_nn.0.weight[k][q], q < 2nf+1
   L.wv1T = o; o += NFMAX * H;         // [f][k] = vel_scaling_nn.0.weight[k][f]
   L.wn1T = o; o += (NFMAX + H) * H;   // [f][k] = node_nn.0.weight[k][f] (rows NFMAX.. = agg part)
+  L.scl = o; o += 16;                 // the forward's F16X3 scales (same matrices, same maxima)
+  o = (o + 63) & ~63;
+  L.we2Tx = o; o += H * H;            // F16X3 fragments of edge_nn.2.weight^T  (as we2x)
+  L.wc1Tx = o; o += H * H;            // F16X3 fragments of coord_nn.0.weight^T (as wc1x)
+  L.we1Tx = o; o += NT * 2 * 512;     // [tp][s][lane][hi|lo]: A[q][32 tp + rho(8 s + j, kh)] = We1[k][q]
   o = (o + 63) & ~63;
   L.total = o;
   return L;
@@ -151,6 +156,48 @@ __host__ __device__ inline TapeLayout tape_layout(int num_atoms, int nf, int H, 
   T.q = o; o += LA;               // Q = vel_scaling_nn(h)
   T.total = o;
   return T;
+}
+
+// Power-of-two scales for the F16X3 fragments of edge_nn.2, coord_nn.0,
+// edge_nn.0, vel_scaling_nn.0, node_nn.0, node_nn.2 (pairs (2^s, 2^-s) at
+// scl[0..11]): 2^s with max|W| 2^s in [2^13, 2^14), so hi parts stay far below
+// the fp16 maximum and lo parts of typical weights stay normal.  Run by one
+// 256-thread block.
+__device__ __forceinline__ void egcl_scales_block(const float* __restrict__ raw, int H, int nf, float* __restrict__ scl) {
+  const RawEgcl R = raw_egcl(H, nf);
+  const int off[6] = {R.We2, R.Wc1, R.We1, R.Wv1, R.Wn1, R.Wn2};
+  const int cnt[6] = {H * H, H * H, H * (2 * nf + 1), H * nf, H * (H + nf), nf * H};
+  __shared__ float red[6][256];
+  for (int k = 0; k < 6; ++k) {
+    float mx = 0.f;
+    for (int i = threadIdx.x; i < cnt[k]; i += 256) mx = fmaxf(mx, fabsf(raw[off[k] + i]));
+    red[k][threadIdx.x] = mx;
+  }
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) {
+    const float mx = red[threadIdx.x][0];
+    int ex = 0;
+    if (mx > 0.f && isfinite(mx)) {
+      frexpf(mx, &ex);              // mx = f 2^ex, f in [0.5, 1)
+      ex = 14 - ex;                 // mx 2^(14 - ex) in [2^13, 2^14)
+      ex = ex > 60 ? 60 : (ex < -60 ? -60 : ex);
+    }
+    scl[2 * threadIdx.x] = ldexpf(1.f, ex);
+    scl[2 * threadIdx.x + 1] = ldexpf(1.f, -ex);
+  }
+}
+
+// hi / lo fp16 pair of w (already scaled), packed as the two halves of a dword
+__device__ __forceinline__ uint32_t f16_split_bits(float w0, float w1, bool lo) {
+  const _Float16 h0 = (_Float16)w0, h1 = (_Float16)w1;
+  const _Float16 p0 = lo ? (_Float16)(w0 - (float)h0) : h0;
+  const _Float16 p1 = lo ? (_Float16)(w1 - (float)h1) : h1;
+  return (uint32_t)__builtin_bit_cast(uint16_t, p0) | ((uint32_t)__builtin_bit_cast(uint16_t, p1) << 16);
 }
 
 struct AmLayout { int wa1t, ba1, wa2, ba2, total; };
@@ -602,13 +649,21 @@ __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 // the pair list, edge tiles and node phase run one block of RB rows at a time;
 // the finished blocks' forces are parked in F and the leapfrog update runs
 // after the last block.
+//
+// The blocked image is kept under ~72 KB so two workgroups share a CU: 16-bit
+// multiplicity counts, a pair buffer of PC entries filled in as many
+// compaction passes as a block needs, ArgMax outputs per chunk of RB atoms,
+// per-atom boxes read from global memory.
 template <int H, int NMAX, int RB = NMAX>
 struct Smem {
   static constexpr int NT = H / 32;
   static constexpr int AST = H + 5;   // agg row: H message sums, 3 force sums, pad (odd stride)
-  static constexpr int MAXP = RB * (NMAX - 1);
   static constexpr bool BLOCKED = RB < NMAX;
-  float pos[NMAX * 3], vel[NMAX * 3], boxa[NMAX * 3];
+  static constexpr int MAXP = RB * (NMAX - 1);
+  static constexpr int PC = BLOCKED ? 512 : MAXP;                       // pair buffer entries
+  static constexpr int CW = BLOCKED ? (RB * NMAX + 1) / 2 : RB * NMAX;  // count words (blocked: 2 x 16 bit)
+  static constexpr int NETA = BLOCKED ? RB : NMAX;                      // ArgMax output rows
+  float pos[NMAX * 3], vel[NMAX * 3], boxa[BLOCKED ? 3 : NMAX * 3];
   float h[NMAX * NFP], g[NMAX * NFP], G[NMAX * NFP];
   float Q[NMAX];
   float F[BLOCKED ? NMAX * 3 : 1];    // forces of finished row blocks (blocked only)
@@ -616,22 +671,36 @@ struct Smem {
   float agg[RB * AST];
   float head[WAVES][H + 4];
   float trash[WAVES][64];             // sink for the branch-free segment-sum stores
-  uint32_t pairs[MAXP];
+  uint32_t pairs[PC];
   uint32_t mask27[NMAX];
   int idmap[NMAX];
   int cntrow[NMAX];
   int headrow[WAVES];
   int ishead[WAVES];
   int scan[WAVES];
-  int npairs;
+  int npairs;                         // pairs in the buffer (this pass)
+  int ptotal;                         // pairs of the whole block
   int err;
   float red[WAVES];
   union {
-    int C[RB * NMAX];                                           // pair build (block rows x atoms)
+    int C[CW];                                                  // pair build (block rows x atoms)
     struct { float qp[NT][RB]; float gp[NT][NFMAX][RB]; } nd;   // node phase partials
-    float net[NMAX * 2 * NFMAX];                                // ArgMax outputs
+    float net[NETA * 2 * NFMAX];                                // ArgMax outputs
   } u;
 };
+
+// multiplicity count e of the block (int, or packed 16-bit when blocked: a count
+// is at most 27 images x 27 repeated labels < 2^16)
+template <class S>
+__device__ __forceinline__ int c_get(const S& sm, int e) {
+  if constexpr (S::BLOCKED) return (sm.u.C[e >> 1] >> (16 * (e & 1))) & 0xffff;
+  else return sm.u.C[e];
+}
+template <class S>
+__device__ __forceinline__ void c_add(S& sm, int e, int v) {
+  if constexpr (S::BLOCKED) atomicAdd(&sm.u.C[e >> 1], v << (16 * (e & 1)));
+  else atomicAdd(&sm.u.C[e], v);
+}
 
 struct MolRef {
   int a0, n;
@@ -694,9 +763,10 @@ __device__ __forceinline__ void build_images(Smem<H, NMAX, RB>& sm, const MolRef
 //     id_mapping, self pairs dropped), (d) compaction to (local row, col, mult)
 //     sorted by (row, col).
 template <int H, int NMAX, int RB>
-__device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid, int r0, int rb) {
+__device__ __forceinline__ void block_counts(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid, int r0, int rb) {
   const int n = M.n;
-  for (int e = tid; e < rb * n; e += BLOCK) sm.u.C[e] = 0;
+  const int words = Smem<H, NMAX, RB>::BLOCKED ? (rb * n + 1) / 2 : rb * n;
+  for (int e = tid; e < words; e += BLOCK) sm.u.C[e] = 0;
   __syncthreads();
   const float r_sq = M.rc * M.rc;
   for (int e = tid; e < rb * n; e += BLOCK) {
@@ -718,16 +788,24 @@ __device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const M
       if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
     }
     if (cnt) {
-      atomicAdd(&sm.u.C[il * n + jl], cnt);
+      c_add(sm, il * n + jl, cnt);
       atomicAdd(&sm.cntrow[i], cnt);
     }
   }
   __syncthreads();
+}
+
+// (d) compaction of the block's counts to (local row, col, mult) sorted by
+// (row, col): the pairs of rank p0 .. p0 + PC - 1 go to the pair buffer
+// (sm.npairs of them); returns the block's total (sm.ptotal).
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ int block_compact(Smem<H, NMAX, RB>& sm, int n, int tid, int rb, int p0) {
+  constexpr int PC = Smem<H, NMAX, RB>::PC;
   const int NN = rb * n;
   const int per = (NN + BLOCK - 1) / BLOCK;
   const int e0 = tid * per, e1 = min(NN, e0 + per);
   int local = 0;
-  for (int e = e0; e < e1; ++e) local += sm.u.C[e] > 0;
+  for (int e = e0; e < e1; ++e) local += c_get(sm, e) > 0;
   const int incl = wave_incl_scan(local);
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
   if (lane == 63) sm.scan[w] = incl;
@@ -735,18 +813,30 @@ __device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const M
   int base = incl - local;
   for (int k = 0; k < w; ++k) base += sm.scan[k];
   for (int e = e0; e < e1; ++e) {
-    const int c = sm.u.C[e];
+    const int c = c_get(sm, e);
     if (c > 0) {
-      const int il = e / n, jl = e - il * n;
-      sm.pairs[base++] = (uint32_t)il | ((uint32_t)jl << 8) | ((uint32_t)c << 16);
+      if (base >= p0 && base < p0 + PC) {
+        const int il = e / n, jl = e - il * n;
+        sm.pairs[base - p0] = (uint32_t)il | ((uint32_t)jl << 8) | ((uint32_t)c << 16);
+      }
+      ++base;
     }
   }
   if (tid == BLOCK - 1) {
     int tot = 0;
     for (int k = 0; k < WAVES; ++k) tot += sm.scan[k];
-    sm.npairs = tot;
+    sm.ptotal = tot;
+    sm.npairs = min(tot - p0, PC);
   }
   __syncthreads();
+  return sm.ptotal;
+}
+
+template <int H, int NMAX, int RB>
+__device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid, int r0, int rb) {
+  static_assert(!Smem<H, NMAX, RB>::BLOCKED, "blocked images compact in passes (block_compact)");
+  block_counts(sm, M, tid, r0, rb);
+  block_compact(sm, M.n, tid, rb, 0);
 }
 
 // whole-molecule pair list (one block)
@@ -762,7 +852,8 @@ __device__ __forceinline__ void build_pairs(Smem<H, NMAX, RB>& sm, const MolRef&
 // ---------------------------------------------------------------------------
 template <int H, int NMAX, int RB, int PREC = PREC_F32>
 __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                           const MolRef& M, int nf, int tid, int r0, int rb STAMP_ARGS) {
+                                           const MolRef& M, int nf, int tid, int r0, int rb,
+                                           bool zero_agg STAMP_ARGS) {
   constexpr int NT = H / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
@@ -772,7 +863,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const int tpw = (T + WAVES - 1) / WAVES;
 
   // zero aggregates / heads, stage biases, find each wave's head row
-  for (int e = tid; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
+  if (zero_agg)   // first compaction pass of the block (later passes accumulate)
+    for (int e = tid; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
   for (int e = tid; e < WAVES * (H + 4); e += BLOCK) (&sm.head[0][0])[e] = 0.f;
   for (int k = tid; k < H; k += BLOCK) {
     sm.bias[k] = Lp[L.be1 + k];
@@ -1212,6 +1304,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
   const AmLayout L = argmax_layout(H, nf);
   const int tid = threadIdx.x;
   float* net = sm.u.net;
+  float lq = 0.f;
   for (int c0 = 0; c0 < n; c0 += RB) {   // atoms in chunks of RB (the agg image)
     const int cn = min(RB, n - c0);
     {
@@ -1232,34 +1325,34 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
       float s = Dp[L.ba2 + o];
       const float* wr = Dp + L.wa2 + o * H;
       for (int k = 0; k < H; ++k) s += wr[k] * act[a * ACT + k];
-      net[(c0 + a) * 2 * NFMAX + o] = s;
+      net[a * 2 * NFMAX + o] = s;          // chunk-local rows
+    }
+    __syncthreads();
+    for (int a = tid; a < cn; a += BLOCK) {   // z of the chunk's atoms (each atom's own h only)
+      const int ag = c0 + a;
+      float u[NFMAX], hv[NFMAX];
+      float T = 0.f;
+#pragma unroll
+      for (int q = 0; q < NFMAX; ++q) {
+        if (q < nf) {
+          const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
+          u[q] = tr + noise[(size_t)(a0 + ag) * nf + q] * expf(ls);
+          hv[q] = sm.h[ag * NFP + q];
+          T += hv[q] * u[q];
+          lq += -0.5f * u[q] * u[q] - ls;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < NFMAX; ++q) {
+        if (q < nf) {
+          const float z = hv[q] * u[q] + (1.f - hv[q]) * (T - softplus_f(T - u[q]));
+          lq -= (1.f - hv[q]) * logsigmoid_f(T - u[q]);
+          sm.h[ag * NFP + q] = z;
+        }
+      }
     }
     __syncthreads();
   }
-  float lq = 0.f;
-  for (int a = tid; a < n; a += BLOCK) {
-    float u[NFMAX], hv[NFMAX];
-    float T = 0.f;
-#pragma unroll
-    for (int q = 0; q < NFMAX; ++q) {
-      if (q < nf) {
-        const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
-        u[q] = tr + noise[(size_t)(a0 + a) * nf + q] * expf(ls);
-        hv[q] = sm.h[a * NFP + q];
-        T += hv[q] * u[q];
-        lq += -0.5f * u[q] * u[q] - ls;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NFMAX; ++q) {
-      if (q < nf) {
-        const float z = hv[q] * u[q] + (1.f - hv[q]) * (T - softplus_f(T - u[q]));
-        lq -= (1.f - hv[q]) * logsigmoid_f(T - u[q]);
-        sm.h[a * NFP + q] = z;
-      }
-    }
-  }
-  __syncthreads();
   return lq;
 }
 
@@ -1322,7 +1415,9 @@ __device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowA
     M.rc = A.r_cut[m];
     for (int e = tid; e < n * 3; e += BLOCK) {
       sm.pos[e] = A.pos[(size_t)M.a0 * 3 + e];
-      sm.boxa[e] = A.box[(size_t)M.a0 * 3 + e];
+      // blocked images keep only the first atom's box (the edge box); the
+      // per-atom pbc boxes are read from global memory in the update
+      if (!Smem<H, NMAX, RB>::BLOCKED || e < 3) sm.boxa[e] = A.box[(size_t)M.a0 * 3 + e];
     }
   }
   if (what & LOAD_VELG)

@@ -2,6 +2,7 @@
 rounds in ONE process (cdna_hip_programming.md rule 24).
 
     python tools/ab_libs.py path/to/libA.so path/to/libB.so ...
+    AB_MODE=chain python tools/ab_libs.py ...     # another bench.MODES workload (forward ones)
 """
 import os
 import statistics
@@ -17,10 +18,13 @@ def main():
     from enflow_amd import _lib
     libs = sys.argv[1:]
     dev = torch.device("cuda", 0)
-    b, model, inp = bench.build_workload(0, dev)
+    c = bench.MODES[os.environ.get("AB_MODE", "forward")]
+    b, model, inp = bench.build_workload(0, dev, c["mols"], c["atoms"], c["layers"], c["chain"])
+    model.gemm_precision = c["prec"]
+    mols, atoms = c["mols"], c["atoms"]
     work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
     noise = torch.randn_like(inp["h"])
-    ldj_mol = torch.empty(bench.MOLS_PER_GPU, device=dev)
+    ldj_mol = torch.empty(mols, device=dev)
     ldj = torch.empty(1, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     outs = {}
@@ -37,7 +41,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
-                                  inp["mol_ptr"], bench.ATOMS, noise, ldj_mol, ldj, err)
+                                  inp["mol_ptr"], atoms, noise, ldj_mol, ldj, err)
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
@@ -54,7 +58,7 @@ def main():
     for p in libs:
         same = torch.equal(outs[p][0], base[0])
         print(f"{os.path.basename(p):40s} median {statistics.median(res[p]):.4f} ms  min {min(res[p]):.4f} ms"
-              f"  mol/s {bench.MOLS_PER_GPU / statistics.median(res[p]) * 1e3:.0f}  bitwise-equal-to-first {same}")
+              f"  mol/s {mols / statistics.median(res[p]) * 1e3:.0f}  bitwise-equal-to-first {same}")
 
 
 if __name__ == "__main__":
