@@ -162,8 +162,6 @@ __device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
   return ldexpf(1.f, -ex);
 }
 
-__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
-__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
 #ifndef ENFLOW_BWD_PREC
 #define ENFLOW_BWD_PREC PREC_F16X3

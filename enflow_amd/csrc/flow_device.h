@@ -233,6 +233,9 @@ __device__ __forceinline__ f32x4 bload4(rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+
 __device__ __forceinline__ float silu_f(float x) {
 #if ENFLOW_ABLATE & 8
   return x;
@@ -668,6 +671,10 @@ struct Smem {
   float Q[NMAX];
   float F[BLOCKED ? NMAX * 3 : 1];    // forces of finished row blocks (blocked only)
   alignas(16) float bias[4 * H];      // be1, be2, bc1, wc2 of the current layer
+  // F16X3 edge_nn.0 fragments of the current layer ([t][ks][hi lanes | lo lanes]
+  // x 4 floats) for the <= 32-atom image (larger images read them from L2)
+  static constexpr bool W1X_LDS = !BLOCKED && NMAX <= 32;
+  alignas(16) float w1x[W1X_LDS ? NT * 2 * 512 : 4];
   float agg[RB * AST];
   float head[WAVES][H + 4];
   float trash[WAVES][64];             // sink for the branch-free segment-sum stores
@@ -872,6 +879,16 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     sm.bias[2 * H + k] = Lp[L.bc1 + k];
     sm.bias[3 * H + k] = Lp[L.wc2 + k];
   }
+  if constexpr (PREC == PREC_F16X3 && Smem<H, NMAX, RB>::W1X_LDS) {
+    // edge_nn.0 split fragments: one L2 pass per layer instead of one per tile
+    const int ks_n = (2 * nf + 1 + 15) >> 4;
+    for (int e = tid; e < NT * ks_n * 128; e += BLOCK) {   // 128 x 16 B per (t, ks)
+      const int blk = e >> 7, r = e & 127, ln = r >> 1, part = r & 1;
+      const int t = blk / ks_n, ks = blk - t * ks_n;
+      const f32x4 v = ld4(Lp + L.we1x + (t * 2 + ks) * 512 + ln * 8 + part * 4);
+      st4(&sm.w1x[(t * 2 + ks) * 512 + part * 256 + ln * 4], v);
+    }
+  }
   if (tid < WAVES) {
     const int t0 = tid * tpw;
     int hr = -1, ih = 0;
@@ -939,8 +956,15 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         split_f16(in, 0, bh, bl);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const int so = (L.we1x + (t * 2 + ks) * 512) * 4;
-          const f32x4 ah = bload4(W, lane * 32, so), al = bload4(W, lane * 32 + 16, so);
+          f32x4 ah, al;
+          if constexpr (Smem<H, NMAX, RB>::W1X_LDS) {
+            ah = ld4(&sm.w1x[(t * 2 + ks) * 512 + lane * 4]);
+            al = ld4(&sm.w1x[(t * 2 + ks) * 512 + 256 + lane * 4]);
+          } else {
+            const int so = (L.we1x + (t * 2 + ks) * 512) * 4;
+            ah = bload4(W, lane * 32, so);
+            al = bload4(W, lane * 32 + 16, so);
+          }
           x0[t] = mfma_f16(ah, bh, x0[t]);
           x0[t] = mfma_f16(ah, bl, x0[t]);
           x0[t] = mfma_f16(al, bh, x0[t]);
@@ -1200,6 +1224,35 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
   const rsrc_t W = weights_rsrc(Lp, L.total);
   const float inv_v1 = Lp[L.scl + 7], inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
   const int vo = lane * 32;
+  // every fragment of the wave's first item is requested before the bias
+  // staging barrier, so the L2 round trips overlap instead of serialising
+  f32x4 vh, vl, nh, nl, gfh[2], gfl[2], ah[3], al[3];
+  auto issue = [&](int it) {
+    const int tp = it % NT;
+    vh = bload4(W, vo, (L.wv1x + tp * 512) * 4);
+    vl = bload4(W, vo + 16, (L.wv1x + tp * 512) * 4);
+    nh = bload4(W, vo, (L.wn1hx + tp * 512) * 4);
+    nl = bload4(W, vo + 16, (L.wn1hx + tp * 512) * 4);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      gfh[s2] = bload4(W, vo, (L.wn2x + (tp * 2 + s2) * 512) * 4);
+      gfl[s2] = bload4(W, vo + 16, (L.wn2x + (tp * 2 + s2) * 512) * 4);
+    }
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      ah[d] = bload4(W, vo, (L.wn1ax + (tp * KS + d) * 512) * 4);
+      al[d] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + d) * 512) * 4);
+    }
+  };
+  if (w < NT * NA) issue(w);
+  // vel_scaling_nn.0 / .2 and node_nn.0 biases staged in LDS (edge_tiles' bias
+  // image is free now)
+  for (int k = tid; k < H; k += BLOCK) {
+    sm.bias[k] = Lp[L.bv1 + k];
+    sm.bias[H + k] = Lp[L.wv2 + k];
+    sm.bias[2 * H + k] = Lp[L.bn1 + k];
+  }
+  __syncthreads();
   for (int item = w; item < NT * NA; item += WAVES) {
     const int tp = item % NT, at = item / NT;
     const int a = at * 32 + j;              // row within the block
@@ -1212,27 +1265,17 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && hh == 0 && jj < nf) ? sm.h[ag * NFP + jj] : 0.f;
     f16x8 hh16, hl16;
     split_f16(hin, 0, hh16, hl16);
-    // prefetch the agg-part fragments two k-steps ahead
-    f32x4 ah[3], al[3];
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      ah[d] = bload4(W, vo, (L.wn1ax + (tp * KS + d) * 512) * 4);
-      al[d] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + d) * 512) * 4);
-    }
     // vel_scaling_nn: Q partial over this wave's 32 hidden features
     f32x16 acc = (f32x16)0.f;
-    {
-      const f32x4 vh = bload4(W, vo, (L.wv1x + tp * 512) * 4), vl = bload4(W, vo + 16, (L.wv1x + tp * 512) * 4);
-      acc = mfma_f16(vh, hh16, acc);
-      acc = mfma_f16(vh, hl16, acc);
-      acc = mfma_f16(vl, hh16, acc);
-    }
+    acc = mfma_f16(vh, hh16, acc);
+    acc = mfma_f16(vh, hl16, acc);
+    acc = mfma_f16(vl, hh16, acc);
     float part = 0.f;
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const int f0 = 32 * tp + 8 * g4 + 4 * hh;
-      const f32x4 b1 = bload4(W, (f0 - 32 * tp) * 4, (L.bv1 + 32 * tp) * 4);   // lane part in voffset
-      const f32x4 w2 = bload4(W, (f0 - 32 * tp) * 4, (L.wv2 + 32 * tp) * 4);
+      const f32x4 b1 = ld4(sm.bias + f0);
+      const f32x4 w2 = ld4(sm.bias + H + f0);
 #pragma unroll
       for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(acc[4 * g4 + u], inv_v1, b1[u]));
     }
@@ -1240,12 +1283,9 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     if (hh == 0 && va) sm.u.nd.qp[tp][a] = part;
     // node_nn.0 over [h, agg]
     acc = (f32x16)0.f;
-    {
-      const f32x4 nh = bload4(W, vo, (L.wn1hx + tp * 512) * 4), nl = bload4(W, vo + 16, (L.wn1hx + tp * 512) * 4);
-      acc = mfma_f16(nh, hh16, acc);
-      acc = mfma_f16(nh, hl16, acc);
-      acc = mfma_f16(nl, hh16, acc);
-    }
+    acc = mfma_f16(nh, hh16, acc);
+    acc = mfma_f16(nh, hl16, acc);
+    acc = mfma_f16(nl, hh16, acc);
     const float* arow = &sm.agg[ac * AST];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
@@ -1264,7 +1304,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     }
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b1 = bload4(W, (8 * g4 + 4 * hh) * 4, (L.bn1 + 32 * tp) * 4);
+      const f32x4 b1 = ld4(sm.bias + 2 * H + 32 * tp + 8 * g4 + 4 * hh);
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
     }
@@ -1272,14 +1312,13 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     f32x16 gacc = (f32x16)0.f;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      const f32x4 gh = bload4(W, vo, (L.wn2x + (tp * 2 + s2) * 512) * 4);
-      const f32x4 gl = bload4(W, vo + 16, (L.wn2x + (tp * 2 + s2) * 512) * 4);
       f16x8 bh, bl;
       split_f16(acc, s2, bh, bl);
-      gacc = mfma_f16(gh, bh, gacc);
-      gacc = mfma_f16(gh, bl, gacc);
-      gacc = mfma_f16(gl, bh, gacc);
+      gacc = mfma_f16(gfh[s2], bh, gacc);
+      gacc = mfma_f16(gfh[s2], bl, gacc);
+      gacc = mfma_f16(gfl[s2], bh, gacc);
     }
+    if (item + WAVES < NT * NA) issue(item + WAVES);
     if (va) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
