@@ -660,7 +660,7 @@ __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 template <int H, int NMAX, int RB = NMAX>
 struct Smem {
   static constexpr int NT = H / 32;
-  static constexpr int AST = H + 5;   // agg row: H message sums, 3 force sums, pad (odd stride)
+  static constexpr int AST = H + 3;   // agg row: H message sums, 3 force sums (odd stride)
   static constexpr bool BLOCKED = RB < NMAX;
   static constexpr int MAXP = RB * (NMAX - 1);
   static constexpr int PC = BLOCKED ? 512 : MAXP;                       // pair buffer entries
@@ -1338,7 +1338,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
                                 int a0, int n, int nf) {
   constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
   constexpr int ACT = H + 1;            // hidden activations staged in agg (free before layer 0)
-  static_assert(RB * (H + 5) >= RB * ACT, "agg too small for the ArgMax activations");
+  static_assert(Smem<H, NMAX, RB>::AST >= ACT, "agg too small for the ArgMax activations");
   float* const act = sm.agg;
   const AmLayout L = argmax_layout(H, nf);
   const int tid = threadIdx.x;
