@@ -11,18 +11,24 @@ OUT = os.path.join(HERE, "libenflow_hip.so")
 ARCH = os.environ.get("ENFLOW_OFFLOAD_ARCH", "gfx950")
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, out=OUT, defines=()):
+    """defines: extra -D flags (A/B and ablation variants built to another `out`)."""
     deps = SRCS + [os.path.join(CSRC, "flow_device.h"), os.path.join(ROOT, "include", "enflow_hip.h")]
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps):
-        return OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
+        return out
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), "-o", OUT + ".tmp"] + SRCS
+           "-I", os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines], "-o", out + ".tmp"] + SRCS
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+    # python -m enflow_amd.build [OUT.so [DEFINE ...]]
+    if len(sys.argv) > 1:
+        print(build(force=True, verbose=True, out=os.path.abspath(sys.argv[1]), defines=sys.argv[2:]))
+    else:
+        print(build(force=True, verbose=True))

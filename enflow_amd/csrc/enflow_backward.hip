@@ -23,6 +23,7 @@
 //   argmax_bwd_kernel (+ its two weight gradients).
 // All arithmetic is float32.
 
+#define ENFLOW_BACKWARD_TU   // -DENFLOW_STAMPS_BWD stamps this file's kernels only (tools/stamps_bwd.py)
 #include "flow_device.h"
 
 // ---------------------------------------------------------------------------
@@ -70,6 +71,34 @@ __global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int n
       const float w0 = q < K1 ? raw[R.We1 + k0 * K1 + q] * sc : 0.f;
       const float w1 = q < K1 ? raw[R.We1 + k1 * K1 + q] * sc : 0.f;
       v = __builtin_bit_cast(float, f16_split_bits(w0, w1, d >= 4));
+    } else if (idx >= L.wn2Tx && idx < L.wn1aTx + NT * (H / 16) * 512) {   // F16X3 node-backward fragments
+      int e, sidx;
+      if (idx < L.wvTx) { e = idx - L.wn2Tx; sidx = 0; }
+      else if (idx < L.wnhTx) { e = idx - L.wvTx; sidx = 1; }
+      else if (idx < L.wn1aTx) { e = idx - L.wnhTx; sidx = 2; }
+      else { e = idx - L.wn1aTx; sidx = 3; }
+      const int d = e & 7, lane = (e >> 3) & 63, blk = e >> 9;
+      const int m = lane & 31, kh = lane >> 5;
+      const float sc = out[L.scl + (sidx == 0 ? 10 : (sidx == 1 ? 6 : 8))];
+      float w2[2];
+      for (int q = 0; q < 2; ++q) {
+        const int jj = 2 * (d & 3) + q;
+        float w = 0.f;
+        if (sidx == 0) {                 // blk = tp; k index = aG feature
+          const int f = 8 * kh + jj;
+          if (f < nf) w = raw[R.Wn2 + f * H + 32 * blk + m];
+        } else if (sidx < 3) {           // blk = tp * 2 + s; rows f < nf
+          const int tp = blk >> 1, s2 = blk & 1;
+          const int k = 32 * tp + rho(8 * s2 + jj, kh);
+          if (m < nf) w = sidx == 1 ? raw[R.Wv1 + k * nf + m] : raw[R.Wn1 + k * (H + nf) + m];
+        } else {                         // blk = tp * (H / 16) + ks
+          const int tp = blk / (H / 16), ks = blk % (H / 16);
+          const int k = 16 * ks + 8 * kh + jj;
+          w = raw[R.Wn1 + k * (H + nf) + nf + 32 * tp + m];
+        }
+        w2[q] = w * sc;
+      }
+      v = __builtin_bit_cast(float, f16_split_bits(w2[0], w2[1], d >= 4));
     } else if (idx < L.wn1T) {              // wv1T[f][k]
       const int e = idx - L.wv1T, f = e / H, k = e % H;
       if (f < nf) v = raw[R.Wv1 + k * nf + f];
@@ -91,6 +120,10 @@ __global__ void __launch_bounds__(256) egcl_bwd_scale_kernel(const float* __rest
 }
 
 __device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float dsilu_f(float z) {   // d silu / dz
+  const float s = sigmoid_f(z);
+  return s * (1.f + z * (1.f - s));
+}
 
 // ---------------------------------------------------------------------------
 // per-layer backward
@@ -111,13 +144,15 @@ struct BwdArgs {
   float* apos;       // [A][3]
   float* avel;
   const int32_t* pair_off;   // this layer's [num_mols + 1] row offsets (32-aligned)
-  float* xin;        // pair rows [P][16]: h_i, h_j, radial        (X of edge_nn.0)
-  float* x1;         // [P][H] silu(edge_nn.0)                       (X of edge_nn.2)
-  float* e;          // [P][H] edge message                         (X of coord_nn.0)
-  float* sc;         // [P][H] silu(coord_nn.0)                      (X of coord_nn.2)
+  // pair rows, tile-blocked (trow).  The pre-activations are stored, not their
+  // SiLUs: outer_acc_kernel applies silu (X operands) and aphi * wc2 * silu'
+  // (coord_nn.0's DY) on load, and this kernel re-reads p0 / pe for silu'.
+  float* xin;        // [P][16] h_i, h_j, radial                     (X of edge_nn.0)
+  float* p0;         // [P][H] pre(edge_nn.0)           silu -> X of edge_nn.2
+  float* pe;         // [P][H] pre(edge_nn.2)           silu -> X of coord_nn.0 (the message)
+  float* pc;         // [P][H] pre(coord_nn.0)          silu -> X of coord_nn.2; DY of coord_nn.0
   float* dp0;        // [P][H] d pre(edge_nn.0)                      (DY of edge_nn.0)
   float* dpe;        // [P][H] d pre(edge_nn.2)                      (DY of edge_nn.2)
-  float* ac;         // [P][H] d pre(coord_nn.0)                     (DY of coord_nn.0)
   float* aphi;       // [P]    d phi                                 (DY of coord_nn.2)
   float* su;         // atom rows [A][H] silu(vel_scaling_nn.0)      (X of vel_scaling_nn.2)
   float* au;         // [A][H] d pre(vel_scaling_nn.0)               (DY of vel_scaling_nn.0)
@@ -128,13 +163,17 @@ struct BwdArgs {
   int32_t* err;
 };
 
+// <= 80 KB at (H, NMAX) = (128, 64): two workgroups per CU.  The node-MLP
+// adjoint rows go through LDS a chunk of Smem::NBCH atoms at a time, in the
+// union the pair build uses later.
 template <int H, int NMAX>
 struct BwdSmem {
-  Smem<H, NMAX> f;
+  using Img = Smem<H, NMAX, NMAX, true>;
+  Img f;
   float ah[NMAX * NFP], ag[NMAX * NFP], aG[NMAX * NFP];
   float apos[NMAX * 3], avel[NMAX * 3], aF[NMAX * 3];
   float aQ[NMAX];
-  float au[NMAX * (H + 1)], an[NMAX * (H + 1)];
+  uint32_t nmax[NMAX / 32];   // per atom tile: max |d pre(node_nn.0)| (float bits)
 };
 
 // Adjoint tiles span many decades (coord_nn.2 starts at gain 0.001), so before
@@ -163,17 +202,222 @@ __device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
 }
 
 
+// power of two putting m in [2^12, 2^13) (0 for m == 0 / non-finite)
+__device__ __forceinline__ int pow2_exp(float m) {
+  int ex = 0;
+  if (m > 0.f && isfinite(m)) {
+    frexpf(m, &ex);
+    ex = 13 - ex;
+    ex = ex > 100 ? 100 : (ex < -100 ? -100 : ex);
+  }
+  return ex;
+}
+
+// Node MLPs backward on F16X3 MFMA, atoms on the lanes (the forward's node
+// phase transposed): per item (32 hidden units tp, 32 atoms at) the
+// pre-activations of vel_scaling_nn.0 and node_nn.0 are recomputed, d pre of
+// both (rows su / au / sn / an for the weight gradients), then
+//   d h   += vel_scaling_nn.0.weight^T d u + node_nn.0.weight[:, :nf]^T d pre
+//            (per-item partials, fixed-order sum over tp),
+//   d agg  = node_nn.0.weight[:, nf:]^T d pre   (into sm.agg, over the message sums).
+// Adjoint operands carry power-of-two scales like the edge chain's.
+template <int H, int NMAX>
+__device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs& B, const EgclLayout& L,
+                                            const EgclBwdLayout& LB, int a0, int n, int nf, int tid) {
+  auto& sm = sb.f;
+  constexpr int NT = H / 32, NA = NMAX / 32, KS = H / 16, NI = NT * NA, IPW = (NI + WAVES - 1) / WAVES;
+  constexpr int AST = BwdSmem<H, NMAX>::Img::AST;
+  static_assert(NT * NFMAX * NMAX <= BwdSmem<H, NMAX>::Img::NBW, "dh partials do not fit sm.u.nb");
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5;
+  const rsrc_t W = weights_rsrc(B.Lp, L.total), WB = weights_rsrc(B.Bp, LB.total);
+  const int vo = lane * 32;
+  const float inv_v1 = B.Lp[L.scl + 7], inv_n1 = B.Lp[L.scl + 9], inv_n2 = B.Lp[L.scl + 11];
+  float* const gp = sm.u.nb;   // d h partials [tp][q][atom]
+  for (int k = tid; k < H; k += BLOCK) {
+    sm.bias[k] = B.Lp[L.bv1 + k];
+    sm.bias[H + k] = B.Lp[L.wv2 + k];
+    sm.bias[2 * H + k] = B.Lp[L.bn1 + k];
+  }
+  if (tid < NA) sb.nmax[tid] = 0u;
+  __syncthreads();
+  auto mm3 = [&](const rsrc_t& r, int off_floats, const f16x8& bh, const f16x8& bl, f32x16 acc) {
+    const f32x4 ah = bload4(r, vo, off_floats * 4), al = bload4(r, vo + 16, off_floats * 4);
+    acc = mfma_f16(ah, bh, acc);
+    acc = mfma_f16(ah, bl, acc);
+    return mfma_f16(al, bh, acc);
+  };
+  f32x16 keep[IPW];
+#pragma unroll
+  for (int ii = 0; ii < IPW; ++ii) {
+    const int item = w + WAVES * ii;
+    if (item >= NI) break;
+    const int tp = item % NT, at = item / NT;
+    const int a = at * 32 + j;
+    const bool va = a < n;
+    const int ac = va ? a : 0;
+    f32x16 hin = (f32x16)0.f, gin = (f32x16)0.f;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const bool on = va && hh == 0 && jj < nf;
+      hin[jj] = on ? sm.h[ac * NFP + jj] : 0.f;
+      gin[jj] = on ? sb.aG[ac * NFP + jj] : 0.f;
+    }
+    f16x8 bh, bl;
+    split_f16(hin, 0, bh, bl);
+    f32x16 zu = mm3(W, L.wv1x + tp * 512, bh, bl, (f32x16)0.f);
+    f32x16 zn = mm3(W, L.wn1hx + tp * 512, bh, bl, (f32x16)0.f);
+    const float* arow = &sm.agg[ac * AST];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      f32x16 av;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) av[jj] = va ? arow[16 * ks + 8 * hh + jj] : 0.f;
+      split_f16(av, 0, bh, bl);
+      zn = mm3(W, L.wn1ax + (tp * KS + ks) * 512, bh, bl, zn);
+    }
+    // d silu(node_nn.0) = node_nn.2.weight^T d G
+    f32x16 gs[1] = {gin};
+    const float ig = tile_pow2_scale(gs);
+    split_f16(gs[0], 0, bh, bl);
+    const f32x16 asn = mm3(WB, LB.wn2Tx + tp * 512, bh, bl, (f32x16)0.f);
+    const float ug = inv_n2 * ig;
+    const float aq = va ? sb.aQ[ac] : 0.f;
+    f32x16 au, an;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int f0 = 32 * tp + 8 * g4 + 4 * hh;
+      const f32x4 b1 = ld4(sm.bias + f0), w2 = ld4(sm.bias + H + f0), bn = ld4(sm.bias + 2 * H + f0);
+      f32x4 su4, au4, sn4, an4;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = 4 * g4 + u;
+        const float z1 = fmaf(zu[r], inv_v1, b1[u]), z2 = fmaf(zn[r], inv_n1, bn[u]);
+        const float s1 = sigmoid_f(z1), s2 = sigmoid_f(z2);
+        su4[u] = z1 * s1;
+        sn4[u] = z2 * s2;
+        au4[u] = aq * w2[u] * (s1 * (1.f + z1 * (1.f - s1)));
+        an4[u] = asn[r] * ug * (s2 * (1.f + z2 * (1.f - s2)));
+        au[r] = au4[u];
+        an[r] = an4[u];
+      }
+      if (va) {
+        const size_t row = (size_t)(a0 + a) * H + f0;
+        st4(B.su + row, su4);
+        st4(B.au + row, au4);
+        st4(B.sn + row, sn4);
+        st4(B.an + row, an4);
+      }
+    }
+    // d h partial over this item's hidden units (rows f = rho(r, hh) < nf: r < 4)
+    f32x16 tu[1] = {au}, tn[1] = {an};
+    const float iu = tile_pow2_scale(tu), in = tile_pow2_scale(tn);
+    f32x16 dv = (f32x16)0.f, dn = (f32x16)0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      split_f16(tu[0], s2, bh, bl);
+      dv = mm3(WB, LB.wvTx + (tp * 2 + s2) * 512, bh, bl, dv);
+      split_f16(tn[0], s2, bh, bl);
+      dn = mm3(WB, LB.wnhTx + (tp * 2 + s2) * 512, bh, bl, dn);
+    }
+    if (va) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int q = r + 4 * hh;
+        if (q < nf) gp[(tp * NFMAX + q) * NMAX + a] = dv[r] * (inv_v1 * iu) + dn[r] * (inv_n1 * in);
+      }
+    }
+    keep[ii] = an;
+    float mx = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fabsf(an[r]));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    if (lane == 0) atomicMax(&sb.nmax[at], __float_as_uint(mx));
+  }
+  __syncthreads();   // message-sum rows consumed; partials and tile maxima complete
+  // d pre(node_nn.0) rows into sm.agg, scaled per atom tile
+#pragma unroll
+  for (int ii = 0; ii < IPW; ++ii) {
+    const int item = w + WAVES * ii;
+    if (item >= NI) break;
+    const int tp = item % NT, at = item / NT, a = at * 32 + j;
+    const float s = ldexpf(1.f, pow2_exp(__uint_as_float(sb.nmax[at])));
+    if (a < n) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sm.agg[a * AST + 32 * tp + rho(r, hh)] = keep[ii][r] * s;
+    }
+  }
+  for (int e = tid; e < n * nf; e += BLOCK) {   // d h: fixed-order sum over the hidden tiles
+    const int a = e / nf, q = e - a * nf;
+    float acc = 0.f;
+#pragma unroll
+    for (int tp = 0; tp < NT; ++tp) acc += gp[(tp * NFMAX + q) * NMAX + a];
+    sb.ah[a * NFP + q] += acc;
+  }
+  __syncthreads();
+  // d agg = node_nn.0.weight[:, nf:]^T d pre
+#pragma unroll
+  for (int ii = 0; ii < IPW; ++ii) {
+    const int item = w + WAVES * ii;
+    if (item >= NI) break;
+    const int tp = item % NT, at = item / NT, a = at * 32 + j;
+    const bool va = a < n;
+    const float* arow = &sm.agg[(va ? a : 0) * AST];
+    f32x16 acc = (f32x16)0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      f32x16 av;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) av[jj] = va ? arow[16 * ks + 8 * hh + jj] : 0.f;
+      f16x8 bh, bl;
+      split_f16(av, 0, bh, bl);
+      acc = mm3(WB, LB.wn1aTx + (tp * KS + ks) * 512, bh, bl, acc);
+    }
+    keep[ii] = acc * (inv_n1 * ldexpf(1.f, -pow2_exp(__uint_as_float(sb.nmax[at]))));
+  }
+  __syncthreads();   // d pre rows consumed
+#pragma unroll
+  for (int ii = 0; ii < IPW; ++ii) {
+    const int item = w + WAVES * ii;
+    if (item >= NI) break;
+    const int tp = item % NT, at = item / NT, a = at * 32 + j;
+    if (a < n) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sm.agg[a * AST + 32 * tp + rho(r, hh)] = keep[ii][r];
+    }
+  }
+  __syncthreads();
+}
+
 #ifndef ENFLOW_BWD_PREC
 #define ENFLOW_BWD_PREC PREC_F16X3
 #endif
+// timing ablations (tools/ab_train.py; results are wrong): 1 = drop the pair-row
+// output stores, 2 = also drop the parked silu' rows
+#ifndef ENFLOW_BWD_ABLATE
+#define ENFLOW_BWD_ABLATE 0
+#endif
+#define ST_OUT(r, vo, so, v) do { if (!(ENFLOW_BWD_ABLATE & 1)) bstore(r, vo, so, v); } while (0)
+#define ST_PARK(r, vo, so, v) do { if (!(ENFLOW_BWD_ABLATE & 2)) bstore(r, vo, so, v); } while (0)
+
+// Pair rows are stored tile-blocked: the 32 rows of a tile are contiguous per
+// feature, element (row p, feature f) of a W-wide array at
+// ((p / 32) * W + f) * 32 + p % 32.  A wave's accumulator register (one
+// feature per half-wave, pairs on the lanes) is then two full 128-byte lines,
+// and outer_acc_kernel reads a tile as one contiguous W x 32 block.
+__device__ __forceinline__ size_t trow(size_t rtile, int W, int f, int j) {
+  return ((rtile * W + f) << 5) + j;
+}
 template <int H, int NMAX, int PREC = ENFLOW_BWD_PREC>
 __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   static_assert(PREC == PREC_F32 || PREC == PREC_F16X3, "backward: fp32-accurate precisions only");
   __shared__ BwdSmem<H, NMAX> sb;
-  Smem<H, NMAX>& sm = sb.f;
+  using Img = typename BwdSmem<H, NMAX>::Img;
+  Img& sm = sb.f;
   constexpr int NT = H / 32;
-  constexpr int AST = Smem<H, NMAX>::AST;
-  constexpr int HS = H + 1;
+  constexpr int AST = Img::AST;
+  constexpr int NBCH = Img::NBCH;
   const int m = blockIdx.x, tid = threadIdx.x;
   const int a0 = B.mol_ptr[m], n = B.mol_ptr[m + 1] - a0;
   if (n > NMAX || B.nf > NFMAX) {
@@ -190,6 +434,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   const float* Rp = B.Rp;
   const float* Bp = B.Bp;
 
+  STAMP_DECL
   // ---- layer-input state (tape), message sums, Q; adjoints of the layer output
   for (int e = tid; e < n * 3; e += BLOCK) {
     sm.pos[e] = B.tape[T.pos + la * 3 + e];
@@ -211,12 +456,6 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     sm.agg[a * AST + k] = B.tape[T.hx + (la + a) * T.ldhx + nf + k];
   }
   for (int a = tid; a < n; a += BLOCK) sm.Q[a] = B.tape[T.q + la + a];
-  for (int k = tid; k < H; k += BLOCK) {
-    sm.bias[k] = B.Lp[L.be1 + k];
-    sm.bias[H + k] = B.Lp[L.be2 + k];
-    sm.bias[2 * H + k] = B.Lp[L.bc1 + k];
-    sm.bias[3 * H + k] = B.Lp[L.wc2 + k];
-  }
   if (tid == 0) sm.err = 0;
   __syncthreads();
   MolRef M;
@@ -226,8 +465,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   M.bx = n > 0 ? sm.boxa[0] : 0.f;
   M.by = n > 0 ? sm.boxa[1] : 0.f;
   M.bz = n > 0 ? sm.boxa[2] : 0.f;
-  build_pairs(sm, M, tid);   // same positions as the forward -> same pairs
 
+  STAMP(0);
   // ---- leapfrog adjoint (dynamics.py:13-21 in reverse order)
   const float aldj = B.adj_ldj[0];
   for (int a = tid; a < n; a += BLOCK) {
@@ -248,61 +487,86 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   }
   __syncthreads();
 
-  // ---- node MLPs backward (egcl.py:26-30, 51-54, 90-92): threads = (hidden unit k, atom group)
+  STAMP(1);
+  // ---- node MLPs backward (egcl.py:26-30, 51-54, 90-92)
+  for (int a = tid; a < n; a += BLOCK) B.aq[a0 + a] = sb.aQ[a];
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    B.agr[(size_t)a0 * nf + e] = sb.aG[a * NFP + q];
+  }
+  if constexpr (PREC == PREC_F16X3) {
+    node_bwd_x3<H, NMAX>(sb, B, L, LB, a0, n, nf, tid);
+  } else {
+  // VALU form (fp32 mode), NBCH atoms at a time:
+  //      threads = (hidden unit k, atom group); adjoint rows staged in sm.u.nb
   {
     constexpr int NG = BLOCK / H;
     const int k = tid % H, grp = tid / H;
+    const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const float bv1 = Rp[R.bv1 + k], bn1 = Rp[R.bn1 + k], wv2 = Rp[R.Wv2 + k];
-    for (int a = grp; a < n; a += NG) {
-      float u = bv1, nn = bn1;
-      for (int f = 0; f < nf; ++f) {
-        const float hv = sm.h[a * NFP + f];
-        u = fmaf(Bp[LB.wv1T + f * H + k], hv, u);
-        nn = fmaf(Bp[LB.wn1T + f * H + k], hv, nn);
+    for (int c0 = 0; c0 < n; c0 += NBCH) {
+      const int c1 = min(n, c0 + NBCH);
+      for (int a = c0 + grp; a < c1; a += NG) {
+        float u = bv1, nn = bn1;
+        for (int f = 0; f < nf; ++f) {
+          const float hv = sm.h[a * NFP + f];
+          u = fmaf(Bp[LB.wv1T + f * H + k], hv, u);
+          nn = fmaf(Bp[LB.wn1T + f * H + k], hv, nn);
+        }
+        const float* arow = &sm.agg[a * AST];
+        const float* wcol = Bp + LB.wn1T + NFMAX * H + k;
+#pragma unroll 8
+        for (int f = 0; f < H; ++f) nn = fmaf(wcol[f * H], arow[f], nn);
+        const float s_u = sigmoid_f(u), s_n = sigmoid_f(nn);
+        const float du = s_u * (1.f + u * (1.f - s_u)), dn = s_n * (1.f + nn * (1.f - s_n));
+        const float au = sb.aQ[a] * wv2 * du;
+        float asn = 0.f;
+        for (int q = 0; q < nf; ++q) asn = fmaf(Rp[R.Wn2 + q * H + k], sb.aG[a * NFP + q], asn);
+        const float an = asn * dn;
+        const size_t row = (size_t)(a0 + a) * H + k;
+        B.su[row] = u * s_u;
+        B.au[row] = au;
+        B.sn[row] = nn * s_n;
+        B.an[row] = an;
+        sm.u.nb[(a - c0) * 2 * H + k] = au;
+        sm.u.nb[(a - c0) * 2 * H + H + k] = an;
       }
-      const float* arow = &sm.agg[a * AST];
-      const float* wcol = Bp + LB.wn1T + NFMAX * H + k;
+      __syncthreads();
+      // d agg = node_nn.0.weight[:, nf:]^T d pre  (overwrites the chunk's message sums)
+      for (int a = c0 + grp; a < c1; a += NG) {
+        const float* anr = &sm.u.nb[(a - c0) * 2 * H + H];
+        const float* wr = Rp + R.Wn1 + nf + k;
+        float s = 0.f;
 #pragma unroll 8
-      for (int f = 0; f < H; ++f) nn = fmaf(wcol[f * H], arow[f], nn);
-      const float s_u = sigmoid_f(u), s_n = sigmoid_f(nn);
-      const float du = s_u * (1.f + u * (1.f - s_u)), dn = s_n * (1.f + nn * (1.f - s_n));
-      const float au = sb.aQ[a] * wv2 * du;
-      float asn = 0.f;
-      for (int q = 0; q < nf; ++q) asn = fmaf(Rp[R.Wn2 + q * H + k], sb.aG[a * NFP + q], asn);
-      const float an = asn * dn;
-      const size_t row = (size_t)(a0 + a) * H + k;
-      B.su[row] = u * s_u;
-      B.au[row] = au;
-      B.sn[row] = nn * s_n;
-      B.an[row] = an;
-      sb.au[a * HS + k] = au;
-      sb.an[a * HS + k] = an;
+        for (int kk = 0; kk < H; ++kk) s = fmaf(wr[kk * (H + nf)], anr[kk], s);
+        sm.agg[a * AST + k] = s;
+      }
+      // d h += vel_scaling_nn.0.weight^T d u + node_nn.0.weight[:, :nf]^T d pre:
+      // one (atom, feature) per wave step, hidden units over the lanes
+      for (int e = w; e < (c1 - c0) * nf; e += WAVES) {
+        const int al = e / nf, f = e - al * nf;
+        const float* aur = &sm.u.nb[al * 2 * H];
+        float s = 0.f;
+        for (int kk = lane; kk < H; kk += 64)
+          s += Rp[R.Wv1 + kk * nf + f] * aur[kk] + Rp[R.Wn1 + kk * (H + nf) + f] * aur[H + kk];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (lane == 0) sb.ah[(c0 + al) * NFP + f] += s;
+      }
+      __syncthreads();
     }
-    for (int a = tid; a < n; a += BLOCK) B.aq[a0 + a] = sb.aQ[a];
-    for (int e = tid; e < n * nf; e += BLOCK) {
-      const int a = e / nf, q = e - a * nf;
-      B.agr[(size_t)a0 * nf + e] = sb.aG[a * NFP + q];
-    }
-    __syncthreads();
-    // d agg = node_nn.0.weight[:, nf:]^T d pre  (overwrites the message sums in LDS)
-    for (int a = grp; a < n; a += NG) {
-      float s = 0.f;
-      const float* wr = Rp + R.Wn1 + nf + k;
-#pragma unroll 8
-      for (int kk = 0; kk < H; ++kk) s = fmaf(wr[kk * (H + nf)], sb.an[a * HS + kk], s);
-      sm.agg[a * AST + k] = s;
-    }
-    // d h += vel_scaling_nn.0.weight^T d u + node_nn.0.weight[:, :nf]^T d pre
-    for (int e = tid; e < n * nf; e += BLOCK) {
-      const int a = e / nf, f = e - a * nf;
-      float s = 0.f;
-      for (int kk = 0; kk < H; ++kk)
-        s += Rp[R.Wv1 + kk * nf + f] * sb.au[a * HS + kk] + Rp[R.Wn1 + kk * (H + nf) + f] * sb.an[a * HS + kk];
-      sb.ah[a * NFP + f] += s;
-    }
-    __syncthreads();
   }
+  }
+  STAMP(2);
+  for (int k = tid; k < H; k += BLOCK) {   // edge-chain biases (the node phase used sm.bias)
+    sm.bias[k] = B.Lp[L.be1 + k];
+    sm.bias[H + k] = B.Lp[L.be2 + k];
+    sm.bias[2 * H + k] = B.Lp[L.bc1 + k];
+    sm.bias[3 * H + k] = B.Lp[L.wc2 + k];
+  }
+  build_pairs(sm, M, tid);   // same positions as the forward -> same pairs (reuses sm.u)
 
+  STAMP(3);
   // ---- edge chain backward, one 32-pair tile per wave step (egcl.py:57-74, 76-89)
   {
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
@@ -320,6 +584,14 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const float inv2 = x3 ? B.Lp[L.scl + 3] : 1.f;
     const float inv0 = x3 ? B.Lp[L.scl + 5] : 1.f;
     auto nofill = [](int) {};
+    // the molecule's tile-blocked rows (trow): buffer resources on its first
+    // row, per element a wave-uniform byte offset (tile, feature) + the lane's
+    const size_t nrow = (size_t)TT * 32;
+    const rsrc_t rp0 = rows_rsrc(B.p0 + prow0 * H, nrow * H), rpe = rows_rsrc(B.pe + prow0 * H, nrow * H);
+    const rsrc_t rpc = rows_rsrc(B.pc + prow0 * H, nrow * H);
+    const rsrc_t rdp0 = rows_rsrc(B.dp0 + prow0 * H, nrow * H), rdpe = rows_rsrc(B.dpe + prow0 * H, nrow * H);
+    const rsrc_t rxin = rows_rsrc(B.xin + prow0 * 16, nrow * 16);
+    const int lob = (hh * 128 + j) * 4;   // lane bytes: (feature 4hh, row j)
     for (int tile = t0; tile < t1; ++tile) {
       const int p = tile * 32 + j;
       const bool valid = p < P;
@@ -327,26 +599,21 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       const int i = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
       const float c = (float)(pr >> 16);       // multiplicity; 0 on padding lanes
       const size_t Rw = prow0 + (size_t)p;
+      const int tsb = tile * H * 128;   // tile byte offset in an H-wide array (16-wide: / (H / 16))
       const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
       const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
       const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], hbz);
       const float radial = dx * dx + dy * dy + dz * dz;
 
       // X row of edge_nn.0: [h_i, h_j, radial]
-      {
-        f32x4 v0, v1;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const int q = 8 * hh + u;
-          float v = 0.f;
-          if (q < nf) v = sm.h[i * NFP + q];
-          else if (q < 2 * nf) v = sm.h[jl * NFP + q - nf];
-          else if (q == 2 * nf) v = radial;
-          v = valid ? v : 0.f;
-          if (u < 4) v0[u] = v; else v1[u - 4] = v;
-        }
-        st4(B.xin + Rw * 16 + 8 * hh, v0);
-        st4(B.xin + Rw * 16 + 8 * hh + 4, v1);
+      for (int u = 0; u < 8; ++u) {
+        const int q = 8 * hh + u;
+        float v = 0.f;
+        if (q < nf) v = sm.h[i * NFP + q];
+        else if (q < 2 * nf) v = sm.h[jl * NFP + q - nf];
+        else if (q == 2 * nf) v = radial;
+        ST_OUT(rxin, (hh * 256 + j) * 4, tile * 2048 + u * 128, valid ? v : 0.f);
       }
 
       // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1
@@ -390,53 +657,50 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
             x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
         }
       }
-      // x1 = silu(pre0) (kept: B operand of GEMM1), silu'(pre0) parked in the dp0 row
+      STAMP(4);
+      // x1 = silu(pre0) (kept: B operand of GEMM1); pre0 stored
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
           const f32x4 b = ld4(sm.bias + f0);
-          f32x4 xv, dv;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float z = x0[t][4 * g4 + u] + b[u];
-            const float s = sigmoid_f(z);
-            xv[u] = z * s;
-            dv[u] = s * (1.f + z * (1.f - s));
-            x0[t][4 * g4 + u] = xv[u];
+            ST_PARK(rp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
+            x0[t][4 * g4 + u] = silu_f(z);
           }
-          st4(B.x1 + Rw * H + f0, xv);
-          st4(B.dp0 + Rw * H + f0, dv);
         }
-      // GEMM1 (recompute): e = silu(edge_nn.2 x1 + be2); silu' parked in the dpe row
+      __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
+      STAMP(5);
+      // GEMM1 (recompute): e = silu(edge_nn.2 x1 + be2); pre_e stored
       f32x16 ev[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) ev[t] = (f32x16)0.f;
       chain_prec_fill<PREC, NT, 1>(W, L.we2f, L.we2x, L.we2b, x0, ev, lane, nofill);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pre0 rows landed (drained by the chain anyway)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
           const f32x4 b = ld4(sm.bias + H + f0);
-          f32x4 xv, dv;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(ev[t][4 * g4 + u], inv1, b[u]);
-            const float s = sigmoid_f(z);
-            xv[u] = z * s;
-            dv[u] = s * (1.f + z * (1.f - s));
-            ev[t][4 * g4 + u] = xv[u];
+            ST_PARK(rpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
+            ev[t][4 * g4 + u] = silu_f(z);
           }
-          st4(B.e + Rw * H + f0, xv);
-          st4(B.dpe + Rw * H + f0, dv);
         }
+      __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
+      STAMP(6);
       // GEMM2 (recompute): phi = coord_nn.2 silu(coord_nn.0 e + bc1)
       f32x16 cv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) cv[t] = (f32x16)0.f;
       chain_prec_fill<PREC, NT, 1>(W, L.wc1f, L.wc1x, L.wc1b, ev, cv, lane, nofill);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pre_e rows landed
       float part = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -445,16 +709,14 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
           const f32x4 b = ld4(sm.bias + 2 * H + f0);
           const f32x4 w2 = ld4(sm.bias + 3 * H + f0);
-          f32x4 sv;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(cv[t][4 * g4 + u], inv2, b[u]);
             const float s = sigmoid_f(z);
-            sv[u] = z * s;
-            part = fmaf(w2[u], sv[u], part);
+            part = fmaf(w2[u], z * s, part);
+            ST_OUT(rpc, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
             cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
           }
-          st4(B.sc + Rw * H + f0, sv);
         }
       const float phi = part + __shfl_xor(part, 32, 64);
       // d phi from dF (egcl.py:71-74: mean over the row's edges, clamp, coords_weight)
@@ -463,71 +725,71 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       const float gy = fabsf(dy * phi) <= 100.f ? sb.aF[i * 3 + 1] * inv : 0.f;
       const float gz = fabsf(dz * phi) <= 100.f ? sb.aF[i * 3 + 2] * inv : 0.f;
       const float aph = c * (gx * dx + gy * dy + gz * dz);
-      if (hh == 0) B.aphi[Rw] = aph;
-      // d pre(coord_nn.0) = dphi * wc2 * silu'(c)
+      if (hh == 0 && !(ENFLOW_BWD_ABLATE & 1)) B.aphi[Rw] = aph;
+      // d pre(coord_nn.0) = dphi * wc2 * silu'(c)   (not stored: outer_acc rebuilds it from pc)
 #pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int f0 = 32 * t + 8 * g4 + 4 * hh;
-          f32x4 av;
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            av[u] = aph * cv[t][4 * g4 + u];
-            cv[t][4 * g4 + u] = av[u];
-          }
-          st4(B.ac + Rw * H + f0, av);
-        }
+      for (int t = 0; t < NT; ++t) cv[t] *= aph;
+      __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
+      STAMP(7);
       // GEMM3: d e = c * d agg[i] + coord_nn.0.weight^T d pre(coord_nn.0)
       f32x16 ae[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) ae[t] = (f32x16)0.f;
       float sc3 = 1.f;
       if constexpr (PREC == PREC_F16X3) sc3 = tile_pow2_scale(cv);   // cv already stored unscaled
-      chain_prec_fill<PREC, NT, 1>(WB, LB.wc1T, LB.wc1Tx, 0, cv, ae, lane, nofill);
+      // pre_e rows re-read during the chain, a quad per step, as the B operand tiles retire
+      f32x16 rl[NT];
+      chain_prec_fill<PREC, NT, 1>(WB, LB.wc1T, LB.wc1Tx, 0, cv, ae, lane, [&](int i) {
+        const int t = i >> 2, g4 = i & 3;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rl[t][4 * g4 + u] = bload(rpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7));
+      });
       const float u3 = inv2 * sc3;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) ae[t][r] = fmaf(ae[t][r], u3, c * sm.agg[i * AST + 32 * t + rho(r, hh)]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // parked silu' rows written by this lane
+      STAMP(8);
       // d pre(edge_nn.2) = d e * silu'(pre_e)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
-          const f32x4 dv = ld4(B.dpe + Rw * H + f0);
-          f32x4 av;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            av[u] = ae[t][4 * g4 + u] * dv[u];
-            ae[t][4 * g4 + u] = av[u];
+            ae[t][4 * g4 + u] *= dsilu_f(rl[t][4 * g4 + u]);
+            ST_OUT(rdpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7), ae[t][4 * g4 + u]);
           }
-          st4(B.dpe + Rw * H + f0, av);
         }
+      __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
+      STAMP(9);
       // GEMM4: d x1 = edge_nn.2.weight^T d pre(edge_nn.2);  d pre0 = d x1 * silu'(pre0)
       f32x16 ax[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) ax[t] = (f32x16)0.f;
       float sc4 = 1.f;
       if constexpr (PREC == PREC_F16X3) sc4 = tile_pow2_scale(ae);   // ae already stored unscaled
-      chain_prec_fill<PREC, NT, 1>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, nofill);
+      chain_prec_fill<PREC, NT, 1>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, [&](int i) {
+        const int t = i >> 2, g4 = i & 3;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) rl[t][4 * g4 + u] = bload(rp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7));
+      });
+      STAMP(10);
       const float u4 = inv1 * sc4;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
-          const f32x4 dv = ld4(B.dp0 + Rw * H + f0);
-          f32x4 av;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            av[u] = ax[t][4 * g4 + u] * u4 * dv[u];
-            ax[t][4 * g4 + u] = av[u];
+            ax[t][4 * g4 + u] = ax[t][4 * g4 + u] * u4 * dsilu_f(rl[t][4 * g4 + u]);
+            ST_OUT(rdp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), ax[t][4 * g4 + u]);
           }
-          st4(B.dp0 + Rw * H + f0, av);
         }
+      __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
+      STAMP(11);
       // GEMM5: d [h_i, h_j, radial] = edge_nn.0.weight^T d pre0   (rows q < 2nf+1)
       f32x16 ain = (f32x16)0.f;
       if constexpr (PREC == PREC_F16X3) {
@@ -555,6 +817,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
             for (int u = 0; u < 4; ++u) ain = mfma32(a4[u], ax[tp][4 * rg + u], ain);
           }
       }
+      STAMP(12);
       float arad = 0.f;
       if (valid) {
 #pragma unroll
@@ -582,6 +845,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   }
   __syncthreads();
 
+  STAMP(13);
   // ---- adjoints of the layer input
   for (int e = tid; e < n * 3; e += BLOCK) {
     B.apos[(size_t)a0 * 3 + e] = sb.apos[e];
@@ -592,6 +856,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     B.ah[(size_t)a0 * nf + e] = sb.ah[a * NFP + q];
     B.ag[(size_t)a0 * nf + e] = sb.ag[a * NFP + q];
   }
+  STAMP(14);
+  STAMP_FLUSH
   if (tid == 0 && sm.err) atomicOr(B.err, sm.err);
 }
 
@@ -634,6 +900,11 @@ struct OuterDesc {
   float* outW;               // [M][N] row-major (torch Linear weight layout)
   float* outB;               // [M] (bias) or NULL
   int ldd, M, ldx, N, rows_static, mb, nb, nch;
+  int tiled;                 // DY / X tile-blocked (trow layout; ldd / ldx = width) or row-major
+  int xf_x;                  // 1: X = silu(stored)
+  int xf_dy;                 // 1: DY[row][m] = rowv[row] * colv[m] * silu'(stored)
+  const float* rowv;
+  const float* colv;
 };
 #define OUTER_MAX 8
 struct OuterBatch {
@@ -659,6 +930,8 @@ __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
 // reduction and runs on VALU.  The bias column (sum of DY) is accumulated by
 // the n-block-0 workgroup from the same LDS image.
 #define OB_ROWS 32
+#define OB_LD 129   // LDS row stride: tile-blocked stages write down the columns
+template <bool TILED>
 __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
@@ -672,8 +945,8 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   const int NB = D.N + (D.outB ? 1 : 0);
   const int n0 = nbi * 128;
   const int M = D.M, N = D.N;
-  __shared__ float sd[2][OB_ROWS][128];
-  __shared__ float sx[2][OB_ROWS][128];
+  __shared__ float sd[2][OB_ROWS][OB_LD];
+  __shared__ float sx[2][OB_ROWS][OB_LD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j = lane & 31, hh = lane >> 5;
   const int mh = w & 1, nh = w >> 1;
   const bool do_bias = D.outB != nullptr && nbi == 0 && tid < M;
@@ -686,20 +959,52 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   float vacc = 0.f;   // M == 1 path: column n0 + tid (tid < 128)
   float rd[16], rx[16];
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
+  constexpr bool tiled = TILED;
+  // element q of this thread: (row r, column c) of the 32 x 128 stage; tile-blocked
+  // sources are read down the columns (contiguous), row-major ones along the rows
+  auto rc = [&](int q, int& r, int& c) {
+    const int e = q * 256 + tid;
+    if (tiled) { r = e & 31; c = e >> 5; } else { r = e >> 7; c = e & 127; }
+  };
+  // coord_nn.0's DY = aphi[row] * wc2[m] * silu'(pc): the row factor is applied
+  // on load (a thread's 16 elements of a tile-blocked stage share one row), the
+  // column factor wc2[m] to the finished sums
+  float ra = 0.f;
   auto gload = [&](int st) {
     const int rb = r0 + st * OB_ROWS;
+    const size_t rt = (size_t)(rb >> 5);
+    if (tiled && D.xf_dy) ra = rb + (tid & 31) < r1 ? D.rowv[rb + (tid & 31)] : 0.f;
+    const float* const dblk = D.DY + ((rt * D.ldd) << 5);            // wave-uniform tile blocks
+    const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int e = q * 256 + tid, r = e >> 7, c = e & 127, p = rb + r;
+      int r, c;
+      rc(q, r, c);
+      const int p = rb + r;
       const bool pv = p < r1;
-      rd[q] = (pv && c < M) ? D.DY[(size_t)p * D.ldd + c] : 0.f;
-      rx[q] = (pv && n0 + c < N) ? D.X[(size_t)p * D.ldx + n0 + c] : 0.f;
+      if (tiled) {
+        const unsigned e = (unsigned)(q * 256 + tid);                // = c * 32 + r
+        rd[q] = (pv && c < M) ? dblk[e] : 0.f;
+        rx[q] = (pv && n0 + c < N) ? xblk[e] : 0.f;
+      } else {
+        rd[q] = (pv && c < M) ? D.DY[(size_t)p * D.ldd + c] : 0.f;
+        rx[q] = (pv && n0 + c < N) ? D.X[(size_t)p * D.ldx + n0 + c] : 0.f;
+      }
     }
   };
   auto lstore = [&](int buf) {
+    if (tiled && D.xf_dy) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rd[q] = ra * dsilu_f(rd[q]);
+    }
+    if (tiled && D.xf_x) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rx[q] = silu_f(rx[q]);
+    }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      const int e = q * 256 + tid, r = e >> 7, c = e & 127;
+      int r, c;
+      rc(q, r, c);
       sd[buf][r][c] = rd[q];
       sx[buf][r][c] = rx[q];
     }
@@ -750,6 +1055,7 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
     __syncthreads();
   }
   float* out = D.part + (size_t)chunk * M * NB;
+  const bool colf = tiled && D.xf_dy;
   if (M > 1) {
 #pragma unroll
     for (int a = 0; a < 2; ++a)
@@ -758,12 +1064,12 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int mm = mh * 64 + a * 32 + rho(r, hh), nn = n0 + nh * 64 + b * 32 + j;
-          if (mm < M && nn < N) out[(size_t)mm * NB + nn] = acc[a][b][r];
+          if (mm < M && nn < N) out[(size_t)mm * NB + nn] = colf ? acc[a][b][r] * D.colv[mm] : acc[a][b][r];
         }
   } else if (tid < 128 && n0 + tid < N) {
     out[n0 + tid] = vacc;
   }
-  if (do_bias) out[(size_t)tid * NB + N] = bsum;
+  if (do_bias) out[(size_t)tid * NB + N] = colf ? bsum * D.colv[tid] : bsum;
 }
 
 __global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
@@ -917,7 +1223,7 @@ static inline size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 struct BwdWs {
-  size_t offs, xin, x1, e, sc, dp0, dpe, ac, aphi, su, au, sn, an, aq, agr, anet, part, total;  // floats
+  size_t offs, xin, p0, pe, pc, dp0, dpe, aphi, su, au, sn, an, aq, agr, anet, part, total;  // floats
   size_t part_floats;
 };
 
@@ -927,12 +1233,11 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   const size_t P = (size_t)prb, A = (size_t)num_atoms;
   W.offs = o; o += al64((size_t)n_layers * (num_mols + 1));
   W.xin = o; o += al64(P * 16);
-  W.x1 = o; o += al64(P * H);
-  W.e = o; o += al64(P * H);
-  W.sc = o; o += al64(P * H);
+  W.p0 = o; o += al64(P * H);
+  W.pe = o; o += al64(P * H);
+  W.pc = o; o += al64(P * H);
   W.dp0 = o; o += al64(P * H);
   W.dpe = o; o += al64(P * H);
-  W.ac = o; o += al64(P * H);
   W.aphi = o; o += al64(P);
   W.su = o; o += al64(A * H);
   W.au = o; o += al64(A * H);
@@ -954,8 +1259,13 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
 
 static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, const float* X, int ldx, int N,
                      const int32_t* rows_dev, int rows_static, int rows_bound, float*& part, float* outW,
-                     float* outB) {
+                     float* outB, int tiled = 0) {
   OuterDesc& D = ob.d[ob.nd];
+  D.tiled = tiled;
+  D.xf_x = 0;
+  D.xf_dy = 0;
+  D.rowv = nullptr;
+  D.colv = nullptr;
   D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
   D.rows_dev = rows_dev; D.rows_static = rows_static;
   D.outW = outW; D.outB = outB;
@@ -973,7 +1283,24 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
 }
 
 static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
-  if (wg > 0) hipLaunchKernelGGL(outer_acc_kernel, dim3(wg), dim3(256), 0, st, ob);
+  // one launch per layout (tile-blocked pair rows / row-major atom rows)
+  for (int tl = 0; tl < 2; ++tl) {
+    OuterBatch sub;
+    sub.nd = 0;
+    int swg = 0;
+    for (int k = 0; k < ob.nd; ++k) {
+      if (ob.d[k].tiled != tl) continue;
+      sub.d[sub.nd] = ob.d[k];
+      sub.start[sub.nd] = swg;
+      swg += ob.start[k + 1] - ob.start[k];
+      sub.start[++sub.nd] = swg;
+    }
+    if (swg > 0) {
+      if (tl) hipLaunchKernelGGL(outer_acc_kernel<true>, dim3(swg), dim3(256), 0, st, sub);
+      else hipLaunchKernelGGL(outer_acc_kernel<false>, dim3(swg), dim3(256), 0, st, sub);
+    }
+  }
+  (void)wg;
   // reducer: one workgroup per 256 outputs of each descriptor
   OuterBatch rb = ob;
   int rw = 0;
@@ -1001,6 +1328,18 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
   } while (0)
 
 extern "C" {
+
+#if defined(ENFLOW_STAMPS_BWD) && !defined(ENFLOW_STAMPS)
+int enflow_read_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(enflow_stamp_acc), sizeof(unsigned long long) * NSTAMP) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[NSTAMP] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enflow_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return NSTAMP;
+}
+#endif
 
 int64_t enflow_lf_tape_size(int num_atoms, int nf, int H, int n_layers) {
   if (num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || n_layers < 0) return -1;
@@ -1084,8 +1423,8 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
     A.pair_off = offs + (size_t)l * (num_mols + 1);
-    A.xin = ws + Wl.xin; A.x1 = ws + Wl.x1; A.e = ws + Wl.e; A.sc = ws + Wl.sc;
-    A.dp0 = ws + Wl.dp0; A.dpe = ws + Wl.dpe; A.ac = ws + Wl.ac; A.aphi = ws + Wl.aphi;
+    A.xin = ws + Wl.xin; A.p0 = ws + Wl.p0; A.pe = ws + Wl.pe; A.pc = ws + Wl.pc;
+    A.dp0 = ws + Wl.dp0; A.dpe = ws + Wl.dpe; A.aphi = ws + Wl.aphi;
     A.su = ws + Wl.su; A.au = ws + Wl.au; A.sn = ws + Wl.sn; A.an = ws + Wl.an;
     A.aq = ws + Wl.aq; A.agr = ws + Wl.agr; A.err = err_flag;
 #define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, A)
@@ -1100,10 +1439,17 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     ob.nd = 0;
     int wg = 0;
     float* part = ws + Wl.part;
-    add_desc(ob, wg, ws + Wl.dp0, H, H, ws + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1);
-    add_desc(ob, wg, ws + Wl.dpe, H, H, ws + Wl.x1, H, H, prow, 0, prb, part, G + R.We2, G + R.be2);
-    add_desc(ob, wg, ws + Wl.ac, H, H, ws + Wl.e, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1);
-    add_desc(ob, wg, ws + Wl.aphi, 1, 1, ws + Wl.sc, H, H, prow, 0, prb, part, G + R.wc2, nullptr);
+    add_desc(ob, wg, ws + Wl.dp0, H, H, ws + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, 1);
+    add_desc(ob, wg, ws + Wl.dpe, H, H, ws + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, 1);
+    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
+    add_desc(ob, wg, ws + Wl.pc, H, H, ws + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, 1);
+    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
+    ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
+    ob.d[ob.nd - 1].rowv = ws + Wl.aphi;
+    ob.d[ob.nd - 1].colv = A.Rp + R.wc2;
+    // aphi is one value per row: its "tile-blocked" layout is row-major with width 1
+    add_desc(ob, wg, ws + Wl.aphi, 1, 1, ws + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr, 1);
+    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
     add_desc(ob, wg, ws + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
     add_desc(ob, wg, ws + Wl.aq, 1, 1, ws + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
     add_desc(ob, wg, ws + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,

@@ -121,7 +121,7 @@ __host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
 // Backward-only packed EGCL section (floats): transposed fragments for the
 // adjoint GEMMs of the edge chain and k-contiguous node weights for the VALU
 // node backward (threads over hidden units k read coalesced rows).
-struct EgclBwdLayout { int we2T, wc1T, we1T, wv1T, wn1T, scl, we2Tx, wc1Tx, we1Tx, total; };
+struct EgclBwdLayout { int we2T, wc1T, we1T, wv1T, wn1T, scl, we2Tx, wc1Tx, we1Tx, wn2Tx, wvTx, wnhTx, wn1aTx, total; };
 __host__ __device__ inline EgclBwdLayout egcl_bwd_layout(int H) {
   const int NT = H / 32;
   EgclBwdLayout L;
@@ -136,6 +136,11 @@ __host__ __device__ inline EgclBwdLayout egcl_bwd_layout(int H) {
   L.we2Tx = o; o += H * H;            // F16X3 fragments of edge_nn.2.weight^T  (as we2x)
   L.wc1Tx = o; o += H * H;            // F16X3 fragments of coord_nn.0.weight^T (as wc1x)
   L.we1Tx = o; o += NT * 2 * 512;     // [tp][s][lane][hi|lo]: A[q][32 tp + rho(8 s + j, kh)] = We1[k][q]
+  // node-MLP backward (atoms on the lanes), F16X3 [..][lane][hi 8 | lo 8]:
+  L.wn2Tx = o; o += NT * 512;         // [tp]: A[m][q] = node_nn.2.weight[q][32 tp + m], q = 8 kh + j < nf
+  L.wvTx = o; o += NT * 2 * 512;      // [tp][s]: A[f][32 tp + rho(8 s + j, kh)] = vel_scaling_nn.0.weight[k][f]
+  L.wnhTx = o; o += NT * 2 * 512;     // [tp][s]: the same for node_nn.0.weight[k][f], f < nf
+  L.wn1aTx = o; o += NT * (H / 16) * 512;   // [tp][ks]: A[m][k] = node_nn.0.weight[k][nf + 32 tp + m], k = 16 ks + 8 kh + j
   o = (o + 63) & ~63;
   L.total = o;
   return L;
@@ -231,6 +236,16 @@ __device__ __forceinline__ float bload(rsrc_t r, int voff, int soff) {
 }
 __device__ __forceinline__ f32x4 bload4(rsrc_t r, int voff, int soff) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+
+#ifndef ENFLOW_STORE_AUX
+#define ENFLOW_STORE_AUX 0   // cache policy of streamed row stores (gfx950 CPol bits: sc0 1, nt 2, sc1 16)
+#endif
+__device__ __forceinline__ void bstore(rsrc_t r, int voff, int soff, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, voff, soff, ENFLOW_STORE_AUX);
+}
+__device__ __forceinline__ rsrc_t rows_rsrc(float* p, size_t nfloats) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)(nfloats * 4), 0x00020000);
 }
 
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
@@ -620,7 +635,7 @@ __device__ __forceinline__ void bias_silu(f32x16 (&X)[NT], const float* __restri
 // diagnostic phase stamps (compiled only with -DENFLOW_STAMPS; never in the
 // product library): per phase, the summed shader-clock cycles of wave 0 of
 // every workgroup, measured between the phase's enclosing barriers.
-#ifdef ENFLOW_STAMPS
+#if defined(ENFLOW_STAMPS) || (defined(ENFLOW_STAMPS_BWD) && defined(ENFLOW_BACKWARD_TU))
 #define NSTAMP 16
 __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 #define STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[NSTAMP] = {0};
@@ -657,27 +672,34 @@ __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 // multiplicity counts, a pair buffer of PC entries filled in as many
 // compaction passes as a block needs, ArgMax outputs per chunk of RB atoms,
 // per-atom boxes read from global memory.
-template <int H, int NMAX, int RB = NMAX>
+//
+// BWD = the training backward's image (enflow_backward.hip): no segment-sum
+// buffers, node-phase partials or ArgMax outputs; 16-bit counts; the union
+// instead holds a chunk of node-MLP adjoint rows (NBW floats).
+template <int H, int NMAX, int RB = NMAX, bool BWD = false>
 struct Smem {
   static constexpr int NT = H / 32;
   static constexpr int AST = H + 3;   // agg row: H message sums, 3 force sums (odd stride)
   static constexpr bool BLOCKED = RB < NMAX;
+  static constexpr bool PACKC = BLOCKED || BWD;                          // 2 x 16-bit counts per word
   static constexpr int MAXP = RB * (NMAX - 1);
   static constexpr int PC = BLOCKED ? 512 : MAXP;                       // pair buffer entries
-  static constexpr int CW = BLOCKED ? (RB * NMAX + 1) / 2 : RB * NMAX;  // count words (blocked: 2 x 16 bit)
-  static constexpr int NETA = BLOCKED ? RB : NMAX;                      // ArgMax output rows
+  static constexpr int CW = PACKC ? (RB * NMAX + 1) / 2 : RB * NMAX;    // count words
+  static constexpr int NETA = BWD ? 1 : (BLOCKED ? RB : NMAX);          // ArgMax output rows
+  static constexpr int NBCH = 8;                                        // BWD: atoms per node chunk
+  static constexpr int NBW = BWD ? NBCH * 2 * H : 1;
   float pos[NMAX * 3], vel[NMAX * 3], boxa[BLOCKED ? 3 : NMAX * 3];
-  float h[NMAX * NFP], g[NMAX * NFP], G[NMAX * NFP];
+  float h[NMAX * NFP], g[NMAX * NFP], G[BWD ? 1 : NMAX * NFP];
   float Q[NMAX];
   float F[BLOCKED ? NMAX * 3 : 1];    // forces of finished row blocks (blocked only)
   alignas(16) float bias[4 * H];      // be1, be2, bc1, wc2 of the current layer
   // F16X3 edge_nn.0 fragments of the current layer ([t][ks][hi lanes | lo lanes]
   // x 4 floats) for the <= 32-atom image (larger images read them from L2)
-  static constexpr bool W1X_LDS = !BLOCKED && NMAX <= 32;
+  static constexpr bool W1X_LDS = !BLOCKED && !BWD && NMAX <= 32;
   alignas(16) float w1x[W1X_LDS ? NT * 2 * 512 : 4];
   float agg[RB * AST];
-  float head[WAVES][H + 4];
-  float trash[WAVES][64];             // sink for the branch-free segment-sum stores
+  float head[BWD ? 1 : WAVES][BWD ? 1 : H + 4];
+  float trash[BWD ? 1 : WAVES][BWD ? 1 : 64];   // sink for the branch-free segment-sum stores
   uint32_t pairs[PC];
   uint32_t mask27[NMAX];
   int idmap[NMAX];
@@ -689,10 +711,12 @@ struct Smem {
   int ptotal;                         // pairs of the whole block
   int err;
   float red[WAVES];
+  static constexpr int NDT = BWD ? 1 : NT, NDR = BWD ? 1 : RB;
   union {
-    int C[CW];                                                  // pair build (block rows x atoms)
-    struct { float qp[NT][RB]; float gp[NT][NFMAX][RB]; } nd;   // node phase partials
-    float net[NETA * 2 * NFMAX];                                // ArgMax outputs
+    int C[CW];                                                    // pair build (block rows x atoms)
+    struct { float qp[NDT][NDR]; float gp[NDT][NFMAX][NDR]; } nd;   // node phase partials
+    float net[NETA * 2 * NFMAX];                                  // ArgMax outputs
+    float nb[NBW];                                                // BWD: node adjoint rows
   } u;
 };
 
@@ -700,12 +724,12 @@ struct Smem {
 // is at most 27 images x 27 repeated labels < 2^16)
 template <class S>
 __device__ __forceinline__ int c_get(const S& sm, int e) {
-  if constexpr (S::BLOCKED) return (sm.u.C[e >> 1] >> (16 * (e & 1))) & 0xffff;
+  if constexpr (S::PACKC) return (sm.u.C[e >> 1] >> (16 * (e & 1))) & 0xffff;
   else return sm.u.C[e];
 }
 template <class S>
 __device__ __forceinline__ void c_add(S& sm, int e, int v) {
-  if constexpr (S::BLOCKED) atomicAdd(&sm.u.C[e >> 1], v << (16 * (e & 1)));
+  if constexpr (S::PACKC) atomicAdd(&sm.u.C[e >> 1], v << (16 * (e & 1)));
   else atomicAdd(&sm.u.C[e], v);
 }
 
@@ -721,8 +745,8 @@ struct MolRef {
 __device__ __forceinline__ float shift_of(int idx, float b) { return idx == 0 ? -b : (idx == 1 ? b : 0.f); }
 
 // (a) image masks and (b) id_mapping for all atoms of the molecule (once per layer)
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ void build_images(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid) {
+template <class S>
+__device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
   const int n = M.n;
   const float rx = M.bx + M.rc, ry = M.by + M.rc, rz = M.bz + M.rc;   // helpers.py:20
   for (int a = tid; a < n; a += BLOCK) {
@@ -769,10 +793,10 @@ __device__ __forceinline__ void build_images(Smem<H, NMAX, RB>& sm, const MolRef
 //     of i within r_cut of atom q (base.py:133-139: both hit columns mapped through
 //     id_mapping, self pairs dropped), (d) compaction to (local row, col, mult)
 //     sorted by (row, col).
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ void block_counts(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid, int r0, int rb) {
+template <class S>
+__device__ __forceinline__ void block_counts(S& sm, const MolRef& M, int tid, int r0, int rb) {
   const int n = M.n;
-  const int words = Smem<H, NMAX, RB>::BLOCKED ? (rb * n + 1) / 2 : rb * n;
+  const int words = S::PACKC ? (rb * n + 1) / 2 : rb * n;
   for (int e = tid; e < words; e += BLOCK) sm.u.C[e] = 0;
   __syncthreads();
   const float r_sq = M.rc * M.rc;
@@ -805,9 +829,9 @@ __device__ __forceinline__ void block_counts(Smem<H, NMAX, RB>& sm, const MolRef
 // (d) compaction of the block's counts to (local row, col, mult) sorted by
 // (row, col): the pairs of rank p0 .. p0 + PC - 1 go to the pair buffer
 // (sm.npairs of them); returns the block's total (sm.ptotal).
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ int block_compact(Smem<H, NMAX, RB>& sm, int n, int tid, int rb, int p0) {
-  constexpr int PC = Smem<H, NMAX, RB>::PC;
+template <class S>
+__device__ __forceinline__ int block_compact(S& sm, int n, int tid, int rb, int p0) {
+  constexpr int PC = S::PC;
   const int NN = rb * n;
   const int per = (NN + BLOCK - 1) / BLOCK;
   const int e0 = tid * per, e1 = min(NN, e0 + per);
@@ -839,17 +863,17 @@ __device__ __forceinline__ int block_compact(Smem<H, NMAX, RB>& sm, int n, int t
   return sm.ptotal;
 }
 
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ void build_block_pairs(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid, int r0, int rb) {
-  static_assert(!Smem<H, NMAX, RB>::BLOCKED, "blocked images compact in passes (block_compact)");
+template <class S>
+__device__ __forceinline__ void build_block_pairs(S& sm, const MolRef& M, int tid, int r0, int rb) {
+  static_assert(!S::BLOCKED, "blocked images compact in passes (block_compact)");
   block_counts(sm, M, tid, r0, rb);
   block_compact(sm, M.n, tid, rb, 0);
 }
 
 // whole-molecule pair list (one block)
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ void build_pairs(Smem<H, NMAX, RB>& sm, const MolRef& M, int tid) {
-  static_assert(RB == NMAX, "build_pairs needs the unblocked image");
+template <class S>
+__device__ __forceinline__ void build_pairs(S& sm, const MolRef& M, int tid) {
+  static_assert(!S::BLOCKED, "build_pairs needs the unblocked image");
   build_images(sm, M, tid);
   build_block_pairs(sm, M, tid, 0, M.n);
 }

@@ -60,16 +60,19 @@ def test_training_gradients_match_reference(name):
     assert not bad, bad
 
 
-def test_training_gradients_bench_shape_vs_oracle():
-    """8 layers, hidden 128, 22-atom molecules (the bench's model) on a batch
-    the float64 gradient oracle finishes in seconds."""
+@pytest.mark.parametrize("sizes", [[22] * 12, [64, 33, 48]], ids=["22x12", "ragged33-64"])
+def test_training_gradients_bench_shape_vs_oracle(sizes):
+    """8 layers, hidden 128 (the bench's model): 22-atom molecules, and a
+    ragged batch of 33..64-atom molecules (the training config's 64-atom
+    kernels), on batches the float64 gradient oracle finishes in seconds."""
     from oracle import enflow_oracle_grad as OG
     from enflow_amd.data.synthetic import make_molecules, default_dt, default_kBT
     from enflow_amd.nn import EGCL, ArgMax
     from enflow_amd.flow import LFIntegrator
     from enflow_amd.data import Data
-    nf, hid, nl, M = 5, 128, 8, 12
-    b = make_molecules(M, 22, nf=nf, seed=77)
+    nf, hid, nl, M = 5, 128, 8, len(sizes)
+    radius = 4.0 * (max(sizes) / 22.0) ** (1.0 / 3.0)
+    b = make_molecules(M, sizes, nf=nf, seed=77, radius=radius)
     torch.manual_seed(5)
     model = LFIntegrator([EGCL(nf, nf, hid) for _ in range(nl)], ArgMax(nf, hid), dt=default_dt()).cuda()
     eps = np.random.default_rng(3).normal(size=b["h"].shape).astype(np.float32)

@@ -65,7 +65,7 @@ def test_backward_sizes_and_argument_errors():
     assert L.enflow_lf_tape_size(A, nf, H, nl) == nl * A * (nf + H + nf + 3 + 3 + 1)
     assert L.enflow_egcl_bwd_packed_size(H, nf) >= 2 * H * H
     assert L.enflow_egcl_bwd_packed_size(96, nf) == -1
-    assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480) > 4 * 480 * 6 * H * 4
+    assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480) > 4 * 480 * 5 * H * 4
     assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, -1) == -1
     # missing tape / buffers: rejected before any launch
     args = [M, A, 22, nf, H] + [None] * 8 + [nl, 1, None, None, None, 0.1, 1.0] + [None] * 7 + \
