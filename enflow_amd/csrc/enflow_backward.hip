@@ -900,11 +900,15 @@ struct OuterDesc {
   float* outW;               // [M][N] row-major (torch Linear weight layout)
   float* outB;               // [M] (bias) or NULL
   int ldd, M, ldx, N, rows_static, mb, nb, nch;
-  int tiled;                 // DY / X tile-blocked (trow layout; ldd / ldx = width) or row-major
+  int tiled;                 // 0 row-major; 1 tile-blocked (trow layout; ldd / ldx = width);
+                             // 2 tile-blocked on the F16X3 kernel (outer_x3_kernel);
+                             // 3 partials written by another descriptor's pass (part2)
   int xf_x;                  // 1: X = silu(stored)
   int xf_dy;                 // 1: DY[row][m] = rowv[row] * colv[m] * silu'(stored)
   const float* rowv;
   const float* colv;
+  int chunk;                 // rows per workgroup / partial
+  float* part2;              // outer_x3_kernel with xf_dy: partials of sum_rows rowv * silu(DY source)
 };
 #define OUTER_MAX 8
 struct OuterBatch {
@@ -912,7 +916,8 @@ struct OuterBatch {
   int nd;
   int start[OUTER_MAX + 1];   // first workgroup of each descriptor
 };
-#define OA_CHUNK 2048
+#define OA_CHUNK 2048        // pair rows per partial
+#define OA_CHUNK_ATOM 512    // atom rows per partial (a few hundred workgroups for 64k atoms)
 
 __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
   int k = 0;
@@ -930,6 +935,10 @@ __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
 // reduction and runs on VALU.  The bias column (sum of DY) is accumulated by
 // the n-block-0 workgroup from the same LDS image.
 #define OB_ROWS 32
+#ifndef ENFLOW_OUTER_X3
+#define ENFLOW_OUTER_X3 1    // pair-row weight gradients on F16X3 MFMA (0: fp32 MFMA)
+#endif
+#define PAIR_OUTER (ENFLOW_OUTER_X3 ? 2 : 1)
 #define OB_LD 129   // LDS row stride: tile-blocked stages write down the columns
 template <bool TILED>
 __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
@@ -939,9 +948,9 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   const int local = bid - ob.start[k];
   const int chunk = local / D.nb, nbi = local - chunk * D.nb;
   const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
-  const int r0 = chunk * OA_CHUNK;
+  const int r0 = chunk * D.chunk;
   if (r0 >= rows) return;
-  const int r1 = min(rows, r0 + OA_CHUNK);
+  const int r1 = min(rows, r0 + D.chunk);
   const int NB = D.N + (D.outB ? 1 : 0);
   const int n0 = nbi * 128;
   const int M = D.M, N = D.N;
@@ -1072,17 +1081,199 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   if (do_bias) out[(size_t)tid * NB + N] = colf ? bsum * D.colv[tid] : bsum;
 }
 
+// F16X3 form of outer_acc_kernel for the tile-blocked pair rows (M > 1): the
+// stage's DY / X tiles go to LDS column-major ([column][row], rows contiguous),
+// so an MFMA operand (8 consecutive rows of one column) is one ds_read_b128
+// pair.  Per stage and wave each operand block gets a power-of-two scale
+// (max |x| -> [2^12, 2^13), as the layer backward's adjoint tiles) before the
+// hi / lo split; the stage's three-product sums land in a scratch accumulator
+// that is added to the running one with the exact inverse scale.
+#define OX_LD 36   // LDS column stride (floats): 16-byte aligned operand reads
+__global__ void __launch_bounds__(256, 2) outer_x3_kernel(OuterBatch ob) {
+  const int bid = blockIdx.x;
+  const int k = find_desc(ob, bid);
+  const OuterDesc& D = ob.d[k];
+  const int local = bid - ob.start[k];
+  const int chunk = local / D.nb, nbi = local - chunk * D.nb;
+  const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
+  const int r0 = chunk * D.chunk;
+  if (r0 >= rows) return;
+  const int r1 = min(rows, r0 + D.chunk);
+  const int NB = D.N + (D.outB ? 1 : 0);
+  const int n0 = nbi * 128;
+  const int M = D.M, N = D.N;
+  __shared__ float sd[2][128][OX_LD];
+  __shared__ float sx[2][128][OX_LD];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5;
+  const int mh = w & 1, nh = w >> 1;
+  const bool do_bias = D.outB != nullptr && nbi == 0 && tid < M;
+  const bool xf_dy = D.xf_dy != 0, xf_x = D.xf_x != 0;
+  const bool fold = xf_dy && D.part2 != nullptr && nbi == 0;   // coord_nn.2's gradient rides along
+  float wacc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) wacc[q] = 0.f;
+  float bsum = 0.f;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
+  float rd[16], rx[16];
+  float ra = 0.f;
+  const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
+  // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
+  auto gload = [&](int st) {
+    const int rb = r0 + st * OB_ROWS;
+    const size_t rt = (size_t)(rb >> 5);
+    const float* const dblk = D.DY + ((rt * D.ldd) << 5);
+    const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
+    const bool pv = rb + (tid & 31) < r1;
+    if (xf_dy) ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = 8 * q + (tid >> 5);
+      const unsigned e = (unsigned)(q * 256 + tid);
+      rd[q] = (pv && c < M) ? dblk[e] : 0.f;
+      rx[q] = (pv && n0 + c < N) ? xblk[e] : 0.f;
+    }
+  };
+  auto lstore = [&](int buf) {
+    if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float z = rd[q], sg = sigmoid_f(z);
+        if (fold) wacc[q] = fmaf(ra, z * sg, wacc[q]);
+        rd[q] = ra * (sg * (1.f + z * (1.f - sg)));
+      }
+    }
+    if (xf_x) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rx[q] = silu_f(rx[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int c = 8 * q + (tid >> 5), r = tid & 31;
+      sd[buf][c][r] = rd[q];
+      sx[buf][c][r] = rx[q];
+    }
+  };
+  const bool use_m1 = mh * 64 + 32 < M, use_n0 = n0 + nh * 64 < N, use_n1 = n0 + nh * 64 + 32 < N;
+  const bool live = mh * 64 < M && use_n0;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) gload(st + 1);
+    if (live) {
+      // operands of both k-steps: A[a][ks] (DY columns), B[b][ks] (X columns)
+      f32x4 av[2][2][2], bv[2][2][2];   // [tile][ks][half]
+      float ma = 0.f, mb = 0.f;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int h2 = 0; h2 < 2; ++h2) {
+            const float* pa = &sd[buf][mh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2];
+            const float* pb = &sx[buf][nh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2];
+            av[a][ks][h2] = *reinterpret_cast<const f32x4*>(pa);
+            bv[a][ks][h2] = *reinterpret_cast<const f32x4*>(pb);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              ma = fmaxf(ma, fabsf(av[a][ks][h2][u]));
+              mb = fmaxf(mb, fabsf(bv[a][ks][h2][u]));
+            }
+          }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        ma = fmaxf(ma, __shfl_xor(ma, off, 64));
+        mb = fmaxf(mb, __shfl_xor(mb, off, 64));
+      }
+      const int ea = pow2_exp(ma), eb = pow2_exp(mb);
+      const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb), un = ldexpf(1.f, -(ea + eb));
+      f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const float xa = av[a][ks][jj >> 2][jj & 3] * sa, xb = bv[a][ks][jj >> 2][jj & 3] * sbs;
+            const _Float16 ha = (_Float16)xa, hb = (_Float16)xb;
+            ah[a][ks][jj] = ha;
+            al[a][ks][jj] = (_Float16)(xa - (float)ha);
+            bh[a][ks][jj] = hb;
+            bl[a][ks][jj] = (_Float16)(xb - (float)hb);
+          }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if ((a == 1 && !use_m1) || (b == 1 && !use_n1)) continue;
+          f32x16 t = (f32x16)0.f;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bh[b][ks], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bl[b][ks], t, 0, 0, 0);
+            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a][ks], bh[b][ks], t, 0, 0, 0);
+          }
+          acc[a][b] += t * un;
+        }
+    }
+    if (do_bias) {
+#pragma unroll 8
+      for (int r = 0; r < OB_ROWS; ++r) bsum += sd[buf][tid][r];
+    }
+    if (st + 1 < nst) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  float* out = D.part + (size_t)chunk * M * NB;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = mh * 64 + a * 32 + rho(r, hh), nn = n0 + nh * 64 + b * 32 + j;
+        if (mm < M && nn < N) out[(size_t)mm * NB + nn] = xf_dy ? acc[a][b][r] * D.colv[mm] : acc[a][b][r];
+      }
+  if (do_bias) out[(size_t)tid * NB + N] = xf_dy ? bsum * D.colv[tid] : bsum;
+  if (fold) {   // fixed-order sum over the 32 rows a half-wave holds
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float v = wacc[q];
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if ((tid & 31) == 0 && 8 * q + (tid >> 5) < M) D.part2[(size_t)chunk * M + 8 * q + (tid >> 5)] = v;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
   const OuterDesc& D = ob.d[k];
   const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
-  const int nch = (rows + OA_CHUNK - 1) / OA_CHUNK;
+  const int nch = (rows + D.chunk - 1) / D.chunk;
   const int NB = D.N + (D.outB ? 1 : 0);
   const int idx = (bid - ob.start[k]) * 256 + threadIdx.x;
   if (idx >= D.M * NB) return;
-  double s = 0.0;
-  for (int ch = 0; ch < nch; ++ch) s += (double)D.part[(size_t)ch * D.M * NB + idx];
+  // four interleaved fp64 sums (chunk mod 4), combined in a fixed order: the
+  // loads stream, the result does not depend on timing
+  const size_t cs = (size_t)D.M * NB;
+  const float* src = D.part + idx;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int ch = 0;
+  for (; ch + 3 < nch; ch += 4) {
+    s0 += (double)src[(size_t)ch * cs];
+    s1 += (double)src[(size_t)(ch + 1) * cs];
+    s2 += (double)src[(size_t)(ch + 2) * cs];
+    s3 += (double)src[(size_t)(ch + 3) * cs];
+  }
+  for (; ch < nch; ++ch) s0 += (double)src[(size_t)ch * cs];
+  const double s = (s0 + s1) + (s2 + s3);
   const int mm = idx / NB, nn = idx - mm * NB;
   if (nn < D.N) D.outW[(size_t)mm * D.N + nn] = (float)s;
   else D.outB[mm] = (float)s;
@@ -1246,7 +1437,7 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.aq = o; o += al64(A);
   W.agr = o; o += al64(A * nf);
   W.anet = o; o += al64(A * 2 * nf);
-  const size_t chp = (size_t)cdiv(prb, OA_CHUNK), cha = (size_t)cdiv(num_atoms, OA_CHUNK);
+  const size_t chp = (size_t)cdiv(prb, OA_CHUNK), cha = (size_t)cdiv(num_atoms, OA_CHUNK_ATOM);
   // partials of one layer's 8 gradients (all in flight together)
   W.part_floats = chp * ((size_t)H * (2 * nf + 2) + 2 * (size_t)H * (H + 1) + H) +
                   cha * ((size_t)H * (nf + 1) + (H + 1) + (size_t)H * (H + nf + 1) + (size_t)nf * (H + 1));
@@ -1266,6 +1457,8 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.xf_dy = 0;
   D.rowv = nullptr;
   D.colv = nullptr;
+  D.part2 = nullptr;
+  D.chunk = tiled ? OA_CHUNK : OA_CHUNK_ATOM;
   D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
   D.rows_dev = rows_dev; D.rows_static = rows_static;
   D.outW = outW; D.outB = outB;
@@ -1273,7 +1466,7 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.mb = 1;
   D.nb = cdiv(N, 128);
   (void)NB;
-  D.nch = rows_bound > 0 ? cdiv(rows_bound, OA_CHUNK) : 0;
+  D.nch = rows_bound > 0 ? cdiv(rows_bound, D.chunk) : 0;
   D.part = part;
   part += (size_t)D.nch * M * NB;
   ob.start[ob.nd] = wg;
@@ -1299,6 +1492,20 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
       if (tl) hipLaunchKernelGGL(outer_acc_kernel<true>, dim3(swg), dim3(256), 0, st, sub);
       else hipLaunchKernelGGL(outer_acc_kernel<false>, dim3(swg), dim3(256), 0, st, sub);
     }
+  }
+  // F16X3 MFMA: tile-blocked descriptors with M > 1
+  {
+    OuterBatch sub;
+    sub.nd = 0;
+    int swg = 0;
+    for (int k = 0; k < ob.nd; ++k) {
+      if (ob.d[k].tiled != 2) continue;
+      sub.d[sub.nd] = ob.d[k];
+      sub.start[sub.nd] = swg;
+      swg += ob.start[k + 1] - ob.start[k];
+      sub.start[++sub.nd] = swg;
+    }
+    if (swg > 0) hipLaunchKernelGGL(outer_x3_kernel, dim3(swg), dim3(256), 0, st, sub);
   }
   (void)wg;
   // reducer: one workgroup per 256 outputs of each descriptor
@@ -1354,7 +1561,7 @@ int64_t enflow_egcl_bwd_packed_size(int H, int nf) {
 int enflow_pack_egcl_bwd_f32(const float* raw, int H, int nf, float* packed, void* stream) {
   if (!hid_ok_b(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
   const int total = egcl_bwd_layout(H).total;
-  hipLaunchKernelGGL(egcl_bwd_scale_kernel, dim3(1), dim3(256), 0, SB(stream), raw, H, nf, packed);
+  hipLaunchKernelGGL(egcl_bwd_scale_kernel, dim3(6), dim3(256), 0, SB(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, SB(stream), raw, H, nf, packed);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
@@ -1439,17 +1646,20 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     ob.nd = 0;
     int wg = 0;
     float* part = ws + Wl.part;
-    add_desc(ob, wg, ws + Wl.dp0, H, H, ws + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, 1);
-    add_desc(ob, wg, ws + Wl.dpe, H, H, ws + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, 1);
+    add_desc(ob, wg, ws + Wl.dp0, H, H, ws + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, PAIR_OUTER);
+    add_desc(ob, wg, ws + Wl.dpe, H, H, ws + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
-    add_desc(ob, wg, ws + Wl.pc, H, H, ws + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, 1);
+    add_desc(ob, wg, ws + Wl.pc, H, H, ws + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
     ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
     ob.d[ob.nd - 1].rowv = ws + Wl.aphi;
     ob.d[ob.nd - 1].colv = A.Rp + R.wc2;
-    // aphi is one value per row: its "tile-blocked" layout is row-major with width 1
-    add_desc(ob, wg, ws + Wl.aphi, 1, 1, ws + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr, 1);
+    // coord_nn.2: d wc2 = sum_rows aphi silu(pc); aphi is one value per row (its "tile-blocked"
+    // layout is row-major with width 1)
+    add_desc(ob, wg, ws + Wl.aphi, 1, 1, ws + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr,
+             ENFLOW_OUTER_X3 ? 3 : 1);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
+    if (ENFLOW_OUTER_X3) ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;   // folded into coord_nn.0's pass
     add_desc(ob, wg, ws + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
     add_desc(ob, wg, ws + Wl.aq, 1, 1, ws + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
     add_desc(ob, wg, ws + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,

@@ -171,7 +171,7 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
   }
 }
 
-// Power-of-two scales of the F16X3 fragments (egcl_scales_block, flow_device.h). One block.
+// Power-of-two scales of the F16X3 fragments (egcl_scales_block, flow_device.h), one workgroup per matrix.
 __global__ void __launch_bounds__(256) egcl_scale_kernel(const float* __restrict__ raw, int H, int nf,
                                                          float* __restrict__ out) {
   egcl_scales_block(raw, H, nf, out + egcl_layout(H, nf).scl);
@@ -614,7 +614,7 @@ int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf) {
 int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {
   if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
   const int total = egcl_layout(H, nf).total;
-  hipLaunchKernelGGL(egcl_scale_kernel, dim3(1), dim3(256), 0, S(stream), raw, H, nf, packed);
+  hipLaunchKernelGGL(egcl_scale_kernel, dim3(6), dim3(256), 0, S(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -168,32 +168,41 @@ __host__ __device__ inline TapeLayout tape_layout(int num_atoms, int nf, int H, 
 // scl[0..11]): 2^s with max|W| 2^s in [2^13, 2^14), so hi parts stay far below
 // the fp16 maximum and lo parts of typical weights stay normal.  Run by one
 // 256-thread block.
+// Power-of-two scale of weight matrix k (We2, Wc1, We1, Wv1, Wn1, Wn2) for the
+// F16X3 fragments: one workgroup per matrix (launch with a grid of 6).
 __device__ __forceinline__ void egcl_scales_block(const float* __restrict__ raw, int H, int nf, float* __restrict__ scl) {
   const RawEgcl R = raw_egcl(H, nf);
+  const int k = blockIdx.x;
   const int off[6] = {R.We2, R.Wc1, R.We1, R.Wv1, R.Wn1, R.Wn2};
   const int cnt[6] = {H * H, H * H, H * (2 * nf + 1), H * nf, H * (H + nf), nf * H};
-  __shared__ float red[6][256];
-  for (int k = 0; k < 6; ++k) {
-    float mx = 0.f;
-    for (int i = threadIdx.x; i < cnt[k]; i += 256) mx = fmaxf(mx, fabsf(raw[off[k] + i]));
-    red[k][threadIdx.x] = mx;
+  __shared__ float red[256];
+  float m0 = 0.f, m1 = 0.f, m2 = 0.f, m3 = 0.f;
+  const float* src = raw + off[k];
+  const int c = cnt[k];
+  int i = threadIdx.x;
+  for (; i + 768 < c; i += 1024) {
+    m0 = fmaxf(m0, fabsf(src[i]));
+    m1 = fmaxf(m1, fabsf(src[i + 256]));
+    m2 = fmaxf(m2, fabsf(src[i + 512]));
+    m3 = fmaxf(m3, fabsf(src[i + 768]));
   }
+  for (; i < c; i += 256) m0 = fmaxf(m0, fabsf(src[i]));
+  red[threadIdx.x] = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o)
-      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + o]);
+    if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
     __syncthreads();
   }
-  if (threadIdx.x < 6) {
-    const float mx = red[threadIdx.x][0];
+  if (threadIdx.x == 0) {
+    const float mx = red[0];
     int ex = 0;
     if (mx > 0.f && isfinite(mx)) {
       frexpf(mx, &ex);              // mx = f 2^ex, f in [0.5, 1)
       ex = 14 - ex;                 // mx 2^(14 - ex) in [2^13, 2^14)
       ex = ex > 60 ? 60 : (ex < -60 ? -60 : ex);
     }
-    scl[2 * threadIdx.x] = ldexpf(1.f, ex);
-    scl[2 * threadIdx.x + 1] = ldexpf(1.f, -ex);
+    scl[2 * k] = ldexpf(1.f, ex);
+    scl[2 * k + 1] = ldexpf(1.f, -ex);
   }
 }
 
@@ -527,7 +536,11 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
 #pragma unroll
       for (int q = 0; q < TPG; ++q) {
         rh[d][q] = bload4(W, vo, foff(d, q));
+#ifdef ENFLOW_ABLATE_LOFRAG
+        rl[d][q] = rh[d][q];   // timing ablation: half the fragment traffic (wrong numerics)
+#else
         rl[d][q] = bload4(W, vo + 16, foff(d, q));
+#endif
       }
     }
   f16x8 bh, bl;
@@ -541,7 +554,11 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
 #pragma unroll
       for (int q = 0; q < TPG; ++q) {
         rh[sl][q] = bload4(W, vo, foff(step + D - 1, q));
+#ifdef ENFLOW_ABLATE_LOFRAG
+        rl[sl][q] = rh[sl][q];
+#else
         rl[sl][q] = bload4(W, vo + 16, foff(step + D - 1, q));
+#endif
       }
     }
     __builtin_amdgcn_sched_barrier(0);
