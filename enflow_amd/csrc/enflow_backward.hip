@@ -187,8 +187,7 @@ __device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(X[t][r]));
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+  m = wave_max(m);
   int ex = 0;
   if (m > 0.f && isfinite(m)) {
     frexpf(m, &ex);
@@ -331,8 +330,7 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
     float mx = 0.f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fabsf(an[r]));
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    mx = wave_max(mx);
     if (lane == 0) atomicMax(&sb.nmax[at], __float_as_uint(mx));
   }
   __syncthreads();   // message-sum rows consumed; partials and tile maxima complete
@@ -592,6 +590,13 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const rsrc_t rdp0 = rows_rsrc(B.dp0 + prow0 * H, nrow * H), rdpe = rows_rsrc(B.dpe + prow0 * H, nrow * H);
     const rsrc_t rxin = rows_rsrc(B.xin + prow0 * 16, nrow * 16);
     const int lob = (hh * 128 + j) * 4;   // lane bytes: (feature 4hh, row j)
+    // d h / d pos of the edge part: each wave adds into its own [atom][nf + 3]
+    // slab (one wave's LDS atomics apply in a fixed order), summed over the
+    // waves in wave order afterwards -> bitwise reproducible
+    const int EW = nf + 3;
+    float* const wacc = sm.u.nb + (size_t)w * n * EW;
+    for (int e = tid; e < WAVES * n * EW; e += BLOCK) sm.u.nb[e] = 0.f;
+    __syncthreads();
     for (int tile = t0; tile < t1; ++tile) {
       const int p = tile * 32 + j;
       const bool valid = p < P;
@@ -823,8 +828,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int q = rho(r, hh);
-          if (q < nf) atomicAdd(&sb.ah[i * NFP + q], ain[r]);
-          else if (q < 2 * nf) atomicAdd(&sb.ah[jl * NFP + q - nf], ain[r]);
+          if (q < nf) atomicAdd(&wacc[i * EW + q], ain[r]);
+          else if (q < 2 * nf) atomicAdd(&wacc[jl * EW + q - nf], ain[r]);
           else if (q == 2 * nf) arad = ain[r];
         }
       }
@@ -834,13 +839,22 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       const float ty = sF * gy + 2.f * dy * arad;
       const float tz = sF * gz + 2.f * dz * arad;
       if (valid && (tx != 0.f || ty != 0.f || tz != 0.f)) {
-        atomicAdd(&sb.apos[i * 3 + 0], tx);
-        atomicAdd(&sb.apos[i * 3 + 1], ty);
-        atomicAdd(&sb.apos[i * 3 + 2], tz);
-        atomicAdd(&sb.apos[jl * 3 + 0], -tx);
-        atomicAdd(&sb.apos[jl * 3 + 1], -ty);
-        atomicAdd(&sb.apos[jl * 3 + 2], -tz);
+        atomicAdd(&wacc[i * EW + nf + 0], tx);
+        atomicAdd(&wacc[i * EW + nf + 1], ty);
+        atomicAdd(&wacc[i * EW + nf + 2], tz);
+        atomicAdd(&wacc[jl * EW + nf + 0], -tx);
+        atomicAdd(&wacc[jl * EW + nf + 1], -ty);
+        atomicAdd(&wacc[jl * EW + nf + 2], -tz);
       }
+    }
+    __syncthreads();
+    for (int e = tid; e < n * EW; e += BLOCK) {
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) s += sm.u.nb[(size_t)ww * n * EW + e];
+      const int a = e / EW, q = e - a * EW;
+      if (q < nf) sb.ah[a * NFP + q] += s;
+      else sb.apos[a * 3 + q - nf] += s;
     }
   }
   __syncthreads();
@@ -1186,11 +1200,8 @@ __global__ void __launch_bounds__(256, 2) outer_x3_kernel(OuterBatch ob) {
               mb = fmaxf(mb, fabsf(bv[a][ks][h2][u]));
             }
           }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        ma = fmaxf(ma, __shfl_xor(ma, off, 64));
-        mb = fmaxf(mb, __shfl_xor(mb, off, 64));
-      }
+      ma = wave_max(ma);
+      mb = wave_max(mb);
       const int ea = pow2_exp(ma), eb = pow2_exp(mb);
       const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb), un = ldexpf(1.f, -(ea + eb));
       f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];

@@ -307,6 +307,21 @@ __device__ __forceinline__ float dpp_f(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xf, false));
 }
 
+// max over the wave's 64 lanes: DPP within each row of 16 (quad swaps, half-row
+// and row mirrors), then the four row maxima read into SGPRs; wave-uniform
+__device__ __forceinline__ float wave_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1, 0xf>(v));    // quad_perm [1, 0, 3, 2]
+  v = fmaxf(v, dpp_f<0x4E, 0xf>(v));    // quad_perm [2, 3, 0, 1]
+  v = fmaxf(v, dpp_f<0x141, 0xf>(v));   // row_half_mirror
+  v = fmaxf(v, dpp_f<0x140, 0xf>(v));   // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
 // Segmented inclusive scan over the 32 pair-lanes of each wave half, for
 // contiguous segments (pairs are sorted by row): lane j ends with the sum of
 // its segment's values at lanes <= j.  m1..m16: 1.0 where the lane d to the
@@ -704,7 +719,11 @@ struct Smem {
   static constexpr int CW = PACKC ? (RB * NMAX + 1) / 2 : RB * NMAX;    // count words
   static constexpr int NETA = BWD ? 1 : (BLOCKED ? RB : NMAX);          // ArgMax output rows
   static constexpr int NBCH = 8;                                        // BWD: atoms per node chunk
-  static constexpr int NBW = BWD ? NBCH * 2 * H : 1;
+  // BWD union member: node-chunk adjoint rows, then per-wave edge-adjoint sums
+  // ([wave][atom][nf + 3], summed over the waves in a fixed order)
+  static constexpr int NBW = BWD ? (NBCH * 2 * H > WAVES * NMAX * (NFMAX + 3) ? NBCH * 2 * H
+                                                                             : WAVES * NMAX * (NFMAX + 3))
+                                 : 1;
   float pos[NMAX * 3], vel[NMAX * 3], boxa[BLOCKED ? 3 : NMAX * 3];
   float h[NMAX * NFP], g[NMAX * NFP], G[BWD ? 1 : NMAX * NFP];
   float Q[NMAX];

@@ -138,3 +138,26 @@ def test_inference_forward_unchanged_by_training_path():
     for k in o1:
         assert torch.equal(o1[k], getattr(o2, k).detach()), k
     assert float(l1) == float(l2)
+
+
+def test_training_gradients_bitwise_reproducible():
+    """Two identical training steps give bitwise-identical gradients: the layer
+    backward sums d h / d pos per wave and then over the waves in a fixed
+    order, the weight gradients are reduced over fixed row chunks in fp64."""
+    from enflow_amd.data.synthetic import make_molecules, default_dt, default_kBT
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    nf, hid, nl = 5, 128, 4
+    sizes = [64, 40, 57, 22, 64, 33, 61, 48] * 4
+    b = make_molecules(len(sizes), sizes, nf=nf, seed=11, radius=5.7)
+    torch.manual_seed(9)
+    model = LFIntegrator([EGCL(nf, nf, hid) for _ in range(nl)], ArgMax(nf, hid), dt=default_dt()).cuda()
+    eps = torch.tensor(np.random.default_rng(4).normal(size=b["h"].shape).astype(np.float32), device="cuda")
+    grads = []
+    for _ in range(2):
+        data = Data.from_arrays(b, device="cuda")
+        _train_step(model, data, eps, default_kBT(), 0.1)
+        grads.append([p.grad.clone() for p in model.parameters()])
+    for g0, g1 in zip(*grads):
+        assert torch.equal(g0, g1)
