@@ -16,11 +16,24 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     deps = SRCS + [os.path.join(CSRC, "flow_device.h"), os.path.join(ROOT, "include", "enflow_hip.h")]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines], "-o", out + ".tmp"] + SRCS
+    # one hipcc per source, in parallel, then one link
+    base = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+            "-I", os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
+    objs = [out + "." + os.path.basename(src) + ".o" for src in SRCS]
+    procs = []
+    for src, obj in zip(SRCS, objs):
+        cmd = base + ["-c", src, "-o", obj]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append(subprocess.Popen(cmd))
+    if any(p.wait() != 0 for p in procs):
+        raise subprocess.CalledProcessError(1, "hipcc")
+    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
+    for obj in objs:
+        os.remove(obj)
     os.replace(out + ".tmp", out)
     return out
 

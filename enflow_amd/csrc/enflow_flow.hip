@@ -30,7 +30,8 @@
 // ---------------------------------------------------------------------------
 // packing kernels
 // ---------------------------------------------------------------------------
-__global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
+__global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out, int flags,
+                                 const float* __restrict__ att) {
   const EgclLayout L = egcl_layout(H, nf);
   const RawEgcl R = raw_egcl(H, nf);
   const int NT = H / 32;
@@ -86,7 +87,10 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
     else if (idx < L.wv2) v = raw[R.bv1 + idx - L.bv1];
     else if (idx < L.bn2) v = raw[R.Wv2 + idx - L.wv2];
     else if (idx < L.bv2) { int e = idx - L.bn2; if (e < nf) v = raw[R.bn2 + e]; }
-    else if (idx < L.scl) { if (idx == L.bv2) v = raw[R.bv2]; }
+    else if (idx < L.watt) { if (idx == L.bv2) v = raw[R.bv2]; }
+    else if (idx < L.batt) { if (att) v = att[idx - L.watt]; }
+    else if (idx < L.vfl) { if (idx == L.batt && att) v = att[H]; }
+    else if (idx < L.scl) { if (idx == L.vfl) v = (float)flags; }
     else if (idx < L.scl + 16) continue;     // written by egcl_scale_kernel
     else if (idx >= L.we1x && idx < L.wv1x) {  // F16X3 edge_nn.0: [t][ks][lane][hi 8 | lo 8], A[m][k]
       const int e = idx - L.we1x;
@@ -193,7 +197,7 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
 // ---------------------------------------------------------------------------
 // the fused flow kernel (forward or reverse)
 // ---------------------------------------------------------------------------
-template <int H, int NMAX, bool REV, int PREC, int RB>
+template <int H, int NMAX, bool REV, int PREC, int RB, bool VAR>
 __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(FlowArgs A) {
   __shared__ Smem<H, NMAX, RB> sm;
   constexpr bool BLOCKED = RB < NMAX;
@@ -263,12 +267,12 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
         atomicAdd(&A.stats[1], edges);
       }
       STAMP(3);
-      edge_tiles<H, NMAX, RB, PREC>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS);
+      edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS);
       if constexpr (BLOCKED) {   // blocks with more pairs than the buffer: further passes
         constexpr int PC = Smem<H, NMAX, RB>::PC;
         for (int p0 = PC; p0 < tot; p0 += PC) {
           block_compact(sm, n, tid_l, rb, p0);
-          edge_tiles<H, NMAX, RB, PREC>(sm, Lp, L, Ml, nf, tid_l, r0, rb, false STAMP_PASS);
+          edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, false STAMP_PASS);
         }
       }
       STAMP(4);
@@ -397,10 +401,10 @@ __global__ void __launch_bounds__(BLOCK, 2) egcl_forward_kernel(FlowArgs A, floa
     const int rb = min(RB, n - r0);
     block_counts(sm, M, tid, r0, rb);
     const int tot = block_compact(sm, n, tid, rb, 0);
-    edge_tiles(sm, A.layers, L, M, nf, tid, r0, rb, true STAMP_PASS);
+    edge_tiles<H, NMAX, RB, PREC_F32, true>(sm, A.layers, L, M, nf, tid, r0, rb, true STAMP_PASS);
     for (int p0 = PC; p0 < tot; p0 += PC) {   // blocks with more pairs than the buffer
       block_compact(sm, n, tid, rb, p0);
-      edge_tiles(sm, A.layers, L, M, nf, tid, r0, rb, false STAMP_PASS);
+      edge_tiles<H, NMAX, RB, PREC_F32, true>(sm, A.layers, L, M, nf, tid, r0, rb, false STAMP_PASS);
     }
     node_phase(sm, A.layers, L, n, nf, tid, r0, rb);
     for (int a = tid; a < rb; a += BLOCK) {
@@ -573,14 +577,21 @@ static const double kLog2Pi = 1.8378770664093453;
     }                                                         \
   } while (0)
 
+template <int HH, int NN, int RBB, bool REV, bool VAR>
+static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
+  if (prec == ENFLOW_PREC_F16X3)
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+  else if (prec == ENFLOW_PREC_BF16)
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+  else
+    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+}
+// gemm_precision may carry ENFLOW_EGCL_VARIANTS: layers packed with
+// enflow_pack_egcl_ex_f32 flags run on the variant-capable kernels
 template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
-  if (prec == ENFLOW_PREC_F16X3)
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB>), dim3(num_mols), dim3(BLOCK), 0, st, A);
-  else if (prec == ENFLOW_PREC_BF16)
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16, RBB>), dim3(num_mols), dim3(BLOCK), 0, st, A);
-  else
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32, RBB>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+  if (prec & ENFLOW_EGCL_VARIANTS) launch_flow_v<HH, NN, RBB, REV, true>(prec & 0xff, num_mols, st, A);
+  else launch_flow_v<HH, NN, RBB, REV, false>(prec, num_mols, st, A);
 }
 
 extern "C" {
@@ -611,12 +622,20 @@ int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf) {
   return argmax_layout(hidden_nf, node_nf).total;
 }
 
-int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {
+int enflow_pack_egcl_ex_f32(const float* raw, int H, int nf, int flags, const float* att, float* packed,
+                            void* stream) {
   if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
+  if (flags & ~(EGCL_ATTENTION | EGCL_NORM_DIFF | EGCL_TANH)) return -1;
+  if ((flags & EGCL_ATTENTION) && !att) return -1;
   const int total = egcl_layout(H, nf).total;
   hipLaunchKernelGGL(egcl_scale_kernel, dim3(6), dim3(256), 0, S(stream), raw, H, nf, packed);
-  hipLaunchKernelGGL(pack_egcl_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed);
+  hipLaunchKernelGGL(pack_egcl_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed,
+                     flags, (flags & EGCL_ATTENTION) ? att : nullptr);
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {
+  return enflow_pack_egcl_ex_f32(raw, H, nf, 0, nullptr, packed, stream);
 }
 
 int enflow_pack_argmax_f32(const float* raw, int H, int nf, float* packed, void* stream) {
@@ -643,7 +662,8 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           float* ldj_mol, float* ldj_total, int32_t* err_flag, uint64_t* pair_stats,
                           float* tape, int32_t* pair_counts, int gemm_precision, void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
-  if (gemm_precision < ENFLOW_PREC_F32 || gemm_precision > ENFLOW_PREC_BF16) return -1;
+  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
+      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
@@ -670,7 +690,8 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
                           void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
-  if (gemm_precision < ENFLOW_PREC_F32 || gemm_precision > ENFLOW_PREC_BF16) return -1;
+  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
+      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
   (void)num_atoms;

@@ -10,7 +10,7 @@
 
 #include "enflow_hip.h"
 
-#define ENFLOW_ABI 2
+#define ENFLOW_ABI 3
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8
@@ -38,9 +38,12 @@ __host__ __device__ constexpr int rho(int r, int hh) { return (r & 3) + 8 * (r >
 __host__ __device__ inline int node_ksteps(int H, int nf) { return (H + nf + 1) / 2; }
 
 struct EgclLayout {
-  int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, scl,
-      we1x, wv1x, wn1hx, wn1ax, wn2x, we2x, wc1x, we2b, wc1b, total;
+  int we1f, we2f, wc1f, wn1h, wn1a, wv1f, wn2f, be1, be2, bc1, wc2, bn1, bv1, wv2, bn2, bv2, watt, batt, vfl,
+      scl, we1x, wv1x, wn1hx, wn1ax, wn2x, we2x, wc1x, we2b, wc1b, total;
 };
+
+// EGCL constructor variants (enflow/nn/egcl.py:11-17), per packed layer (vfl)
+enum { EGCL_ATTENTION = 1, EGCL_NORM_DIFF = 2, EGCL_TANH = 4 };
 
 // GEMM precision of the two H x H edge GEMMs (edge_nn.2, coord_nn.0), the
 // flow's dominant work (include/enflow_hip.h ENFLOW_PREC_*):
@@ -76,6 +79,9 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   L.wv2 = o; o += H;
   L.bn2 = o; o += NFMAX;
   L.bv2 = o; o += 4;
+  L.watt = o; o += H;                      // att_nn.0.weight (attention layers; else zeros)
+  L.batt = o; o += 4;                      // att_nn.0.bias
+  L.vfl = o; o += 4;                       // EGCL_* flags of the layer (as a float)
   L.scl = o; o += 16;                      // (2^s, 2^-s) of edge_nn.2, coord_nn.0, edge_nn.0,
                                            // vel_scaling_nn.0, node_nn.0, node_nn.2 (F16X3)
   o = (o + 63) & ~63;
@@ -260,6 +266,7 @@ __device__ __forceinline__ rsrc_t rows_rsrc(float* p, size_t nfloats) {
 __device__ __forceinline__ void st4(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 
+__device__ __forceinline__ float sigm_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float silu_f(float x) {
 #if ENFLOW_ABLATE & 8
   return x;
@@ -917,7 +924,7 @@ __device__ __forceinline__ void build_pairs(S& sm, const MolRef& M, int tid) {
 // ---------------------------------------------------------------------------
 // EGCL edge part: per-pair MLP chain on MFMA + deterministic segment sums
 // ---------------------------------------------------------------------------
-template <int H, int NMAX, int RB, int PREC = PREC_F32>
+template <int H, int NMAX, int RB, int PREC = PREC_F32, bool VAR = false>
 __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                            const MolRef& M, int nf, int tid, int r0, int rb,
                                            bool zero_agg STAMP_ARGS) {
@@ -971,6 +978,11 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   // F16X3 accumulators carry the weight scale 2^s: unscale exactly in the bias fma
   const float inv1 = PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f;
   const float inv2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
+  // constructor variants of the layer (wave-uniform; compiled in only for VAR
+  // kernels, the default-flag kernels keep their registers)
+  const int vfl = VAR ? (int)Lp[L.vfl] : 0;
+  const bool v_att = (vfl & EGCL_ATTENTION) != 0, v_nd = (vfl & EGCL_NORM_DIFF) != 0,
+             v_tanh = (vfl & EGCL_TANH) != 0;
 
   STAMP(8);
   for (int tile = t0; tile < t1; ++tile) {
@@ -1084,6 +1096,28 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
       for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = silu_f(fmaf(e[0][4 * g4 + u], inv1, b[u]));
     }
+    if (v_att) {   // egcl.py:60-62: out *= sigmoid(att_nn(out)); every tile activated first
+#pragma unroll
+      for (int t = 1; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) e[t][4 * g4 + u] = silu_f(fmaf(e[t][4 * g4 + u], inv1, b[u]));
+        }
+      float d = 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 wa = ld4(Lp + L.watt + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) d = fmaf(wa[u], e[t][4 * g4 + u], d);
+        }
+      const float att = sigm_f(d + __shfl_xor(d, 32, 64) + Lp[L.batt]);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) e[t] *= att;
+    }
     STAMP(12);
     STAMP(13);
     // ---- GEMM2: coord_nn.0 (egcl.py:35-42), with fillers: activate e tile t+1
@@ -1119,7 +1153,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
         for (int u = 0; u < 4; ++u) dstm[(32 * t + 8 * g4 + 4 * hh + u) * fstride] += v[u];
 #endif
-        if (t + 1 < NT) {
+        if (t + 1 < NT && !v_att) {
           const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * (t + 1) + 8 * g4 + 4 * hh);
 #pragma unroll
           for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = silu_f(fmaf(e[t + 1][4 * g4 + u], inv1, b[u]));
@@ -1136,12 +1170,15 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
           for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(hc[tp][4 * g4 + u], inv2, b[u]));
         }
     }
-    const float phi = part + __shfl_xor(part, 32, 64);
+    float phi = part + __shfl_xor(part, 32, 64);
+    if (v_tanh) phi = tanhf(phi);                        // egcl.py:40-42
+    // norm_diff: coord_diff / (|coord_diff| + 1) (egcl.py:82-84; radial stays unnormalised)
+    const float nd = v_nd ? __builtin_amdgcn_rcpf(sqrtf(radial) + 1.f) : 1.f;
     // trans = clamp(coord_diff * phi, -100, 100) (egcl.py:71-72); segment sums
     // for the mean (egcl.py:73-74); lane half 0 stores
-    float tx = c * fminf(fmaxf(dx * phi, -100.f), 100.f);
-    float ty = c * fminf(fmaxf(dy * phi, -100.f), 100.f);
-    float tz = c * fminf(fmaxf(dz * phi, -100.f), 100.f);
+    float tx = c * fminf(fmaxf(dx * nd * phi, -100.f), 100.f);
+    float ty = c * fminf(fmaxf(dy * nd * phi, -100.f), 100.f);
+    float tz = c * fminf(fmaxf(dz * nd * phi, -100.f), 100.f);
 #if ENFLOW_SEGSCAN_ASM
     float tw = 0.f;
     seg_scan4(tx, ty, tz, tw, SM);

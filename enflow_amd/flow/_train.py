@@ -106,6 +106,10 @@ class _FlowFunction(torch.autograd.Function):
 
 def flow_forward_train(flow, data, noise, check_errors):
     """Differentiable LFIntegrator.forward (HIP forward with tape)."""
+    if any(n.variant_flags() for n in flow.networks):
+        raise NotImplementedError("the HIP training backward implements EGCL with the default flags "
+                                  "(attention=False, norm_diff=False, tanh=False); run the variants under "
+                                  "torch.no_grad() (forward / reverse)")
     s = flow._state(data)
     dev = s["dev"]
     kind = flow._dequant_kind()

@@ -32,9 +32,12 @@ class LFIntegrator(BaseFlow):
 
     def _prec(self):
         try:
-            return _lib.PRECISIONS[self.gemm_precision]
+            p = _lib.PRECISIONS[self.gemm_precision]
         except KeyError:
             raise ValueError(f"gemm_precision must be one of {sorted(_lib.PRECISIONS)}") from None
+        if any(isinstance(n, EGCL) and n.variant_flags() for n in self.networks):
+            p |= _lib.EGCL_VARIANTS      # attention / norm_diff / tanh layers: variant-capable kernels
+        return p
 
     def make_networks(self, network):
         return [network for _ in range(self.n_iter)]
@@ -88,8 +91,12 @@ class LFIntegrator(BaseFlow):
             return self._train_bufs
         hid, nf, _ = self._geometry()
         L = _lib.lib()
+        if any(n.variant_flags() for n in self.networks):
+            raise NotImplementedError("the HIP training backward implements EGCL with the default flags "
+                                      "(attention=False, norm_diff=False, tanh=False); the variants run "
+                                      "forward / reverse only")
         raw = torch.cat([torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
-                                    for _, p in n.named_parameters()]) for n in self.networks])
+                                    for p in n.raw_parameters()]) for n in self.networks])
         stride = L.enflow_egcl_bwd_packed_size(hid, nf)
         rstride = raw.numel() // max(len(self.networks), 1)
         bwd = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)

@@ -50,47 +50,67 @@ class EGCL(nn.Module):
 
     # ------------------------------------------------------------------
     def hip_supported(self):
-        """The HIP kernels implement the reference defaults used by main.py."""
+        """The HIP kernels implement every constructor flag of the reference
+        (attention, norm_diff, tanh; ``clamp`` is stored and unused there too)
+        with the SiLU activation, input_nf == output_nf <= 8, hidden_nf in
+        {32, 64, 128}."""
         L = _lib.lib()
-        return (not self.attention and not self.norm_diff and not self.tanh
-                and isinstance(self.act_fn, nn.SiLU) and self.input_nf == self.output_nf
+        return (isinstance(self.act_fn, nn.SiLU) and self.input_nf == self.output_nf
                 and 1 <= self.input_nf <= L.enflow_max_node_nf()
                 and bool(L.enflow_supports_hidden(self.hidden_nf)))
 
     def _check_supported(self):
         if not self.hip_supported():
             raise NotImplementedError(
-                "enflow_amd EGCL kernels implement attention=False, norm_diff=False, tanh=False, "
-                "SiLU, input_nf == output_nf <= 8 and hidden_nf in {32, 64, 128}")
+                "enflow_amd EGCL kernels implement the SiLU activation, input_nf == output_nf <= 8 "
+                "and hidden_nf in {32, 64, 128}")
+
+    def variant_flags(self):
+        """ENFLOW_EGCL_* flags of this layer's constructor variants (0 = defaults)."""
+        return ((_lib.EGCL_ATTENTION if self.attention else 0) | (_lib.EGCL_NORM_DIFF if self.norm_diff else 0)
+                | (_lib.EGCL_TANH if self.tanh else 0))
 
     def raw_parameters(self):
-        """Parameters in named_parameters() order, as the C ABI expects."""
-        return [p for _, p in self.named_parameters()]
+        """Parameters in the default-flag named_parameters() order the C ABI
+        expects (att_nn, present with attention=True, travels separately)."""
+        return [p for k, p in self.named_parameters() if not k.startswith("att_nn.")]
+
+    def _att_raw(self, device):
+        if not self.attention:
+            return None
+        lin = self.att_nn[0]
+        return torch.cat([lin.weight.detach().reshape(-1), lin.bias.detach().reshape(-1)]).to(
+            device=device, dtype=torch.float32)
+
+    def _pack(self, raw, dst, device):
+        L = _lib.lib()
+        att = self._att_raw(device)
+        _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.hidden_nf, self.input_nf, self.variant_flags(),
+                                             _lib.ptr(att), _lib.ptr(dst), _lib.stream_ptr(device)),
+                   "enflow_pack_egcl_ex_f32")
 
     def packed(self, device):
         """MFMA-fragment packed fp32 weights on `device` (cached, re-packed when
         any parameter changes)."""
-        params = self.raw_parameters()
+        params = [p for _, p in self.named_parameters()]
         key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is not None and self._packed_key == key:
             return self._packed
         L = _lib.lib()
-        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in params])
+        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
+                         for p in self.raw_parameters()])
         size = L.enflow_egcl_packed_size(self.hidden_nf, self.input_nf)
         out = torch.empty(size, dtype=torch.float32, device=device)
-        _lib.check(L.enflow_pack_egcl_f32(_lib.ptr(raw), self.hidden_nf, self.input_nf, _lib.ptr(out),
-                                          _lib.stream_ptr(device)), "enflow_pack_egcl_f32")
+        self._pack(raw, out, device)
         self._packed, self._packed_key = out, key
         return out
 
     def pack_into(self, dst):
         """Pack into a slice of a caller-owned buffer (used by the fused flow)."""
-        L = _lib.lib()
         device = dst.device
         raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
                          for p in self.raw_parameters()])
-        _lib.check(L.enflow_pack_egcl_f32(_lib.ptr(raw), self.hidden_nf, self.input_nf, _lib.ptr(dst),
-                                          _lib.stream_ptr(device)), "enflow_pack_egcl_f32")
+        self._pack(raw, dst, device)
 
     # ------------------------------------------------------------------
     def forward(self, h, edges):

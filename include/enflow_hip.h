@@ -73,6 +73,24 @@ int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf);
 int enflow_pack_egcl_f32(const float* raw, int hidden_nf, int node_nf,
                          float* packed, void* stream);
 
+/* EGCL constructor variants (enflow/nn/egcl.py:11-17, 40-49, 57-63, 80-84). */
+#define ENFLOW_EGCL_ATTENTION 1   /* edge messages *= sigmoid(att_nn(messages)) */
+#define ENFLOW_EGCL_NORM_DIFF 2   /* force uses coord_diff / (|coord_diff| + 1) */
+#define ENFLOW_EGCL_TANH      4   /* phi = tanh(coord_nn(...)) */
+/* OR into gemm_precision of enflow_lf_forward_f32 / enflow_lf_reverse_f32 when
+ * any layer carries ENFLOW_EGCL_* flags (selects the variant-capable kernels;
+ * without it the flags in the packed layers are ignored). */
+#define ENFLOW_EGCL_VARIANTS 0x100
+
+/* enflow_pack_egcl_f32 for a layer built with attention / norm_diff / tanh:
+ * `raw` in the same (default-flag) order as above, `flags` ENFLOW_EGCL_*,
+ * `att` = att_nn.0.weight [1][H] followed by att_nn.0.bias [1] (required with
+ * ENFLOW_EGCL_ATTENTION, else ignored).  The flow / EGCL forward and reverse
+ * kernels read the flags from the packed layer; the training backward
+ * supports only flags == 0 (the host refuses the others). */
+int enflow_pack_egcl_ex_f32(const float* raw, int hidden_nf, int node_nf, int flags,
+                            const float* att, float* packed, void* stream);
+
 /* Pack ArgMax.network (enflow/nn/argmax.py:6-10): network.0.weight [H][nf],
  * network.0.bias [H], network.2.weight [2nf][H], network.2.bias [2nf]. */
 int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,

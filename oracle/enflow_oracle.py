@@ -164,19 +164,31 @@ ARGMAX_PARAM_NAMES = ("network.0.weight", "network.0.bias",
                       "network.2.weight", "network.2.bias")
 
 
+def sigmoid(x):
+    return 1.0 / (1.0 + np.exp(-x))
+
+
 def egcl_forward(p, h, row, col, cdiff, coords_weight=1.0):
-    """EGCL.forward (enflow/nn/egcl.py:76-92) with the default flags
-    (attention=False, norm_diff=False, tanh=False).  ``p`` maps
-    EGCL_PARAM_NAMES to float64 arrays.  Returns (Q [n,1], F [n,3], G [n,nf])."""
+    """EGCL.forward (enflow/nn/egcl.py:76-92).  ``p`` maps EGCL_PARAM_NAMES to
+    float64 arrays; the constructor variants come from optional keys:
+    ``flags`` = (attention, norm_diff, tanh) and, with attention,
+    ``att_nn.0.weight`` / ``att_nn.0.bias``.  Returns (Q [n,1], F [n,3], G [n,nf])."""
+    attention, norm_diff, tanh = (bool(x) for x in p.get("flags", (0, 0, 0)))
     n = h.shape[0]
     radial = np.sum(cdiff ** 2, axis=1, keepdims=True)                 # egcl.py:79
+    if norm_diff:                                                        # egcl.py:82-84
+        cdiff = cdiff / (np.sqrt(radial) + 1.0)
     ein = np.concatenate([h[row], h[col], radial], axis=1)              # egcl.py:57
     e = silu(linear(silu(linear(ein, p["edge_nn.0.weight"], p["edge_nn.0.bias"])),
                     p["edge_nn.2.weight"], p["edge_nn.2.bias"]))         # egcl.py:20-24
+    if attention:                                                        # egcl.py:60-62
+        e = e * sigmoid(linear(e, p["att_nn.0.weight"], p["att_nn.0.bias"]))
     q = linear(silu(linear(h, p["vel_scaling_nn.0.weight"], p["vel_scaling_nn.0.bias"])),
                p["vel_scaling_nn.2.weight"], p["vel_scaling_nn.2.bias"])  # egcl.py:51-54
     phi = linear(silu(linear(e, p["coord_nn.0.weight"], p["coord_nn.0.bias"])),
                  p["coord_nn.2.weight"])                                  # egcl.py:35-42
+    if tanh:                                                             # egcl.py:40-42
+        phi = np.tanh(phi)
     trans = np.clip(cdiff * phi, -100.0, 100.0)                          # egcl.py:71-72
     f = segment_mean(trans, row, n) * coords_weight                      # egcl.py:73-74
     agg = segment_sum(e, row, n)                                          # egcl.py:65

@@ -91,7 +91,7 @@ def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partit
 
     Returns (loss, ldj, [layer grad dicts], dequant grad dict, output state)."""
     t = lambda a: torch.tensor(np.asarray(a, dtype=np.float64))  # noqa: E731
-    P = [{k: t(v).requires_grad_(True) for k, v in p.items()} for p in layers]
+    P = [{k: t(v).requires_grad_(True) for k, v in p.items() if k != "flags"} for p in layers]
     D = {k: t(v).requires_grad_(True) for k, v in dequant.items()}
     mol_ptr = np.asarray(state["mol_ptr"], dtype=np.int64)
     n = int(mol_ptr[-1])

@@ -13,6 +13,13 @@ EGCL_KEYS = (
     "vel_scaling_nn.2.weight", "vel_scaling_nn.2.bias",
 )
 ARGMAX_KEYS = ("network.0.weight", "network.0.bias", "network.2.weight", "network.2.bias")
+ATT_KEYS = ("att_nn.0.weight", "att_nn.0.bias")
+
+
+def layer_flags(inp, i):
+    """(attention, norm_diff, tanh) of fixture layer i (defaults when absent)."""
+    f = inp.get(f"p{i}.flags")
+    return tuple(bool(x) for x in f) if f is not None else (False, False, False)
 
 
 def load(name):
@@ -23,7 +30,23 @@ def load(name):
 
 
 def layer_params(inp, i, dtype=np.float64):
-    return {k: inp[f"p{i}.{k}"].astype(dtype) for k in EGCL_KEYS}
+    p = {k: inp[f"p{i}.{k}"].astype(dtype) for k in EGCL_KEYS}
+    flags = layer_flags(inp, i)
+    p["flags"] = flags
+    if flags[0]:
+        p.update({k: inp[f"p{i}.{k}"].astype(dtype) for k in ATT_KEYS})
+    return p
+
+
+def egcl_from_fixture(inp, i, nf, hid):
+    """enflow_amd EGCL with fixture layer i's constructor flags and weights."""
+    import torch
+    from enflow_amd.nn import EGCL
+    att, nd, th = layer_flags(inp, i)
+    net = EGCL(nf, nf, hid, attention=att, norm_diff=nd, tanh=th)
+    keys = EGCL_KEYS + (ATT_KEYS if att else ())
+    net.load_state_dict({k: torch.tensor(inp[f"p{i}.{k}"]) for k in keys})
+    return net
 
 
 def dequant_params(inp, dtype=np.float64):
@@ -55,11 +78,7 @@ def flow_from_fixture(inp, device="cuda"):
     from enflow_amd.data import Data
 
     hid, nf, nl = int(inp["hid"]), inp["h"].shape[1], int(inp["n_layers"])
-    nets = []
-    for i in range(nl):
-        net = EGCL(nf, nf, hid)
-        net.load_state_dict({k: torch.tensor(inp[f"p{i}.{k}"]) for k in EGCL_KEYS})
-        nets.append(net)
+    nets = [egcl_from_fixture(inp, i, nf, hid) for i in range(nl)]
     am = ArgMax(nf, hid)
     am.load_state_dict({k: torch.tensor(inp[f"dq.{k}"]) for k in ARGMAX_KEYS})
     model = LFIntegrator(nets, am, dt=float(inp["dt"])).to(device)

@@ -162,6 +162,21 @@ def case_egcl(hid, seed):
                                "G": g.detach().numpy()})
 
 
+def case_egcl_variant(hid, seed, flags, name):
+    """EGCL with the constructor variants (attention, norm_diff, tanh)."""
+    torch.manual_seed(seed)
+    nf = 5
+    att, nd, th = flags
+    net = EGCL(nf, nf, hid, attention=att, norm_diff=nd, tanh=th).double()
+    b = batch_inputs(4, [22, 9, 15, 3], nf, seed=seed, one_hot=False)
+    d = ref_data(b)
+    q, f, g = net(d.h, d.edges)
+    inp = dict(b)
+    inp.update(params_of(net, "p0."))
+    inp["p0.flags"] = np.array(flags, dtype=np.int32)
+    save(name, inp, {"Q": q.detach().numpy(), "F": f.detach().numpy(), "G": g.detach().numpy()})
+
+
 def case_argmax(hid, seed):
     torch.manual_seed(seed)
     nf = 5
@@ -179,11 +194,15 @@ def case_argmax(hid, seed):
                                  "reverse": rev.numpy()})
 
 
-def case_flow(hid, n_layers, sizes, seed, name):
+def case_flow(hid, n_layers, sizes, seed, name, flags=None):
+    """``flags``: per layer (attention, norm_diff, tanh), default flags when None."""
     torch.manual_seed(seed)
     nf = 5
     dt = default_dt()
-    nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+    if flags is None:
+        nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+    else:
+        nets = [EGCL(nf, nf, hid, attention=a, norm_diff=nd, tanh=th) for a, nd, th in flags]
     model = LFIntegrator(nets, ArgMax(nf, hid), dt=dt)   # BaseFlow casts to float64
     b = batch_inputs(len(sizes), sizes, nf, seed=seed)
     d = ref_data(b)
@@ -212,6 +231,8 @@ def case_flow(hid, n_layers, sizes, seed, name):
     inp["hid"] = np.array(hid)
     for i, net in enumerate(model.networks):
         inp.update(params_of(net, f"p{i}."))
+        if flags is not None:
+            inp[f"p{i}.flags"] = np.array(flags[i], dtype=np.int32)
     inp.update(params_of(model.dequantize, "dq."))
     fwd.update(rev)
     save(name, inp, fwd)
@@ -253,6 +274,14 @@ def case_train(hid, n_layers, sizes, seed, name, nf=5):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "variants":
+        case_egcl_variant(64, 31, (True, False, False), "egcl_h64_att")
+        case_egcl_variant(32, 32, (False, True, True), "egcl_h32_nd_tanh")
+        case_egcl_variant(128, 33, (True, True, True), "egcl_h128_all")
+        case_flow(64, 3, [22, 9, 15, 3], 34, "lf_var_h64_L3",
+                  flags=[(True, False, False), (False, True, True), (True, True, True)])
+        case_flow(128, 2, [22, 22, 30], 35, "lf_var_h128_L2", flags=[(False, True, False), (True, False, True)])
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "train":
         case_train(32, 3, [22, 9, 15, 3], 21, "train_h32_L3")
         case_train(128, 2, [22, 22], 22, "train_h128_L2")

@@ -10,7 +10,7 @@ import torch
 
 from oracle import enflow_oracle as O
 from _fixtures import (load, layer_params, dequant_params, state, n_layers, rel_err,
-                       flow_from_fixture, data_from_fixture, EGCL_KEYS, ARGMAX_KEYS)
+                       flow_from_fixture, data_from_fixture, egcl_from_fixture, EGCL_KEYS, ARGMAX_KEYS)
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -62,6 +62,20 @@ def test_egcl_matches_reference(hid):
     assert rel_err(g.cpu().numpy(), out["G"]) < TOL
 
 
+@pytest.mark.parametrize("name", ["egcl_h64_att", "egcl_h32_nd_tanh", "egcl_h128_all"])
+def test_egcl_variants_match_reference(name):
+    """EGCL(attention / norm_diff / tanh) against the reference module's outputs."""
+    inp, out = load(name)
+    net = egcl_from_fixture(inp, 0, 5, int(inp["p0.edge_nn.2.weight"].shape[0])).to(DEV)
+    assert net.variant_flags() != 0
+    d = data_from_fixture(inp, DEV)
+    with torch.no_grad():
+        q, f, g = net(d.h, d.edges)
+    assert rel_err(q.cpu().numpy(), out["Q"]) < TOL
+    assert rel_err(f.cpu().numpy(), out["F"]) < TOL
+    assert rel_err(g.cpu().numpy(), out["G"]) < TOL
+
+
 def test_argmax_matches_reference():
     from enflow_amd.nn import ArgMax
     inp, out = load("argmax_h32")
@@ -83,7 +97,7 @@ BF16_TOL = 1e-3              # configs[2] (bf16 generate path), normwise; measur
 
 
 @pytest.mark.parametrize("prec", PRECS)
-@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
+@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2", "lf_var_h64_L3", "lf_var_h128_L2"])
 def test_lf_forward_matches_reference(name, prec):
     from enflow_amd.flow import Alchemical_NLL
     inp, out = load(name)
@@ -99,7 +113,7 @@ def test_lf_forward_matches_reference(name, prec):
 
 
 @pytest.mark.parametrize("prec", PRECS)
-@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
+@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2", "lf_var_h64_L3", "lf_var_h128_L2"])
 def test_lf_reverse_matches_reference(name, prec):
     """generate direction: reverse of the reference's forward output."""
     inp, out = load(name)

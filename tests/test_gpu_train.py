@@ -161,3 +161,15 @@ def test_training_gradients_bitwise_reproducible():
         grads.append([p.grad.clone() for p in model.parameters()])
     for g0, g1 in zip(*grads):
         assert torch.equal(g0, g1)
+
+
+def test_training_through_egcl_variants_is_refused():
+    """The HIP backward implements the default EGCL flags only: a differentiable
+    forward through attention / norm_diff / tanh layers raises instead of
+    returning wrong gradients; under no_grad the variants run."""
+    inp, _ = load("lf_var_h64_L3")
+    model, data = flow_from_fixture(inp, "cuda")
+    with pytest.raises(NotImplementedError):
+        model(data, noise=torch.tensor(inp["eps"], device="cuda"))
+    with torch.no_grad():
+        model(data, noise=torch.tensor(inp["eps"], device="cuda"))

@@ -33,9 +33,10 @@ def test_edges_quirk_is_exercised():
     assert non_identity > 0
 
 
-@pytest.mark.parametrize("hid", [32, 128])
-def test_egcl_matches_reference(hid):
-    inp, out = load(f"egcl_h{hid}")
+@pytest.mark.parametrize("name", ["egcl_h32", "egcl_h128", "egcl_h64_att", "egcl_h32_nd_tanh", "egcl_h128_all"])
+def test_egcl_matches_reference(name):
+    """Default flags and the constructor variants (attention, norm_diff, tanh)."""
+    inp, out = load(name)
     s = state(inp)
     row, col, eb = O.batch_edges(s["pos"], s["box"], s["r_cut"], s["mol_ptr"])
     cd = O.coord_diff(s["pos"], row, col, eb)
@@ -54,7 +55,7 @@ def test_argmax_matches_reference():
     np.testing.assert_array_equal(O.argmax_reverse(z), out["reverse"])
 
 
-@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
+@pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2", "lf_var_h64_L3", "lf_var_h128_L2"])
 def test_lf_flow_matches_reference(name):
     inp, out = load(name)
     layers = [layer_params(inp, i) for i in range(n_layers(inp))]
