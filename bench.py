@@ -221,6 +221,97 @@ def run_train(args, world, rank, local, device, dist):
         print(json.dumps(line), flush=True)
 
 
+LJ_METRIC = "LJ-box generations/sec (reverse/generate path, example/generate.yaml: 2944-atom periodic box)"
+
+
+def run_lj(args, world, rank, device, dist):
+    """The reference's example/generate.yaml system: one periodic 2944-atom
+    Lennard-Jones box per GPU (batch 1), 8 coupling layers, hidden 128,
+    generated by LFIntegrator.reverse (main.py:263-278) through the
+    layer-by-layer large-system kernels (enflow_amd/csrc/enflow_large.hip).
+    Not a BASELINE.json config: reported for the large-system path."""
+    from enflow_amd.data.synthetic import make_lj_systems, default_dt
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    from enflow_amd.utils.helpers import mol_ptr_from_counts
+    from enflow_amd import _lib as L_
+    n = args.atoms or 2944
+    b = make_lj_systems([n], seed=3000 + rank, nf=NF)
+    b["pos"] = b["pos"] - np.round(b["pos"] / b["box"]) * b["box"]
+    torch.manual_seed(0)
+    model = LFIntegrator([EGCL(NF, NF, HID) for _ in range(LAYERS)], ArgMax(NF, HID), dt=default_dt()).to(device)
+    f = lambda k: torch.tensor(b[k], dtype=torch.float32, device=device).contiguous()  # noqa: E731
+    inp = {k: f(k) for k in ("h", "g", "pos", "vel", "box", "r_cut")}
+    inp["mol_ptr"] = mol_ptr_from_counts(torch.tensor(np.diff(b["mol_ptr"])), device=device)
+    work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
+    ldj_mol = torch.empty(1, dtype=torch.float32, device=device)
+    ldj = torch.empty(1, dtype=torch.float32, device=device)
+    err = torch.zeros(1, dtype=torch.int32, device=device)
+    idx = torch.empty(n, dtype=torch.int32, device=device)
+    mx = torch.zeros(1, dtype=torch.int32, device=device)
+    model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                          inp["mol_ptr"], n, torch.randn_like(work["h"]), ldj_mol, ldj, err)
+    gsrc = {k: work[k].clone() for k in work}
+    e = Data.from_arrays({**b, "pos": gsrc["pos"].double().cpu().numpy()}, device=device).edges
+    pairs = int(e._materialise()[0].numel()) * LAYERS          # unique pairs of the first layer x layers
+
+    def step():
+        for k in work:
+            work[k].copy_(gsrc[k])
+        model.reverse_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                              inp["mol_ptr"], n, idx, mx, err)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if int(err.item()) != 0:
+        raise RuntimeError(f"flow kernel error flag {int(err.item())}")
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    from enflow_amd.distributed import max_over_ranks
+    elapsed = max_over_ranks(time.perf_counter() - t0, device)
+    stream = torch.cuda.current_stream(device)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    for e0, e1 in evs:
+        for k in work:
+            work[k].copy_(gsrc[k])
+        e0.record(stream)
+        model.reverse_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
+                              inp["mol_ptr"], n, idx, mx, err)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if rank == 0:
+        flops = flops_per_launch(pairs, n, LAYERS, HID, NF) - n * (2 * HID * NF + 2 * HID * 2 * NF)
+        achieved = flops / (kern_ms * 1e-3) / 1e12
+        line = {
+            "metric": LJ_METRIC, "value": world * args.steps / elapsed, "unit": "box-generations/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": f"synthetic ({n}-atom LJ box, density 0.8, r_cut 2.5 sigma, random-init weights)",
+            "config": {"workload": f"lf_reverse_1x{n}lj_L{LAYERS}_H{HID}_nf{NF}_f32", "atoms": n,
+                       "coupling_layers": LAYERS, "hidden_nf": HID, "node_nf": NF,
+                       "parallelism": f"independent boxes x{world}", "unique_pairs_per_launch": pairs},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": PEAK_F32_MFMA_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": None,
+                         "kernel": "enflow_lf_reverse_large_f32 (per layer: images, id_mapping, pairs, "
+                                   "lg_layer_kernel<128,1,false>)",
+                         "kernel_ms": kern_ms, "flops_per_launch": flops, "gemm_precision": model.gemm_precision},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,10 +319,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=1536)
-    ap.add_argument("--mode", choices=("forward", "generate", "chain", "train"), default="forward",
+    ap.add_argument("--mode", choices=("forward", "generate", "chain", "train", "lj"), default="forward",
                     help="forward: the headline metric (configs[1]); generate: configs[2] (bf16 reverse); "
-                         "chain: configs[4] (256-atom chains, 16 layers); train: configs[3] per GPU")
-    ap.add_argument("--atoms", type=int, default=None, help="train mode: atoms per molecule (default 64)")
+                         "chain: configs[4] (256-atom chains, 16 layers); train: configs[3] per GPU; "
+                         "lj: example/generate.yaml's 2944-atom LJ box (large-system kernels)")
+    ap.add_argument("--atoms", type=int, default=None,
+                    help="train mode: atoms per molecule (default 64); lj mode: atoms per box (default 2944)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -244,8 +337,11 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
 
-    if args.mode == "train":
-        run_train(args, world, rank, local, device, dist)
+    if args.mode in ("train", "lj"):
+        if args.mode == "train":
+            run_train(args, world, rank, local, device, dist)
+        else:
+            run_lj(args, world, rank, device, dist)
         if dist:
             dist.barrier()
             dist.destroy_process_group()

@@ -37,6 +37,14 @@ SIGNATURES = {
                                    _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p, _p, _i, _p]),
     "enflow_lf_reverse_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                    _i, _f, _f, _p, _p, _p, _i, _p]),
+    "enflow_lf_large_workspace_size": (_i64, [_i, _i, _i, _i]),
+    "enflow_lf_forward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                         _i, _p, _p, _f, _f, _f, _p, _p, _p, _i, _p, _i64, _p]),
+    "enflow_lf_reverse_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                         _i, _f, _f, _p, _p, _p, _i, _p, _i64, _p]),
+    "enflow_egcl_forward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f,
+                                           _p, _p, _p, _p, _i, _p, _i64, _p]),
+    "enflow_neighbour_pairs_large_f32": (_i, [_i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "enflow_one_hot_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_egcl_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f,
                                      _p, _p, _p, _p, _p]),
@@ -97,6 +105,30 @@ def require_gpu(t):
     if not (isinstance(t, torch.Tensor) and t.is_cuda):
         raise HipPathError("the enflow_amd HIP path needs tensors on a ROCm GPU "
                            "(there is no CPU fallback)")
+
+
+LARGE_TRAIN_MSG = ("the HIP training backward handles molecules of <= 64 atoms; larger systems "
+                   "run forward / reverse / EGCL only")
+_large_ws = {}
+
+
+def is_large(max_mol_atoms):
+    """True if the batch needs the layer-by-layer large-system kernels."""
+    return int(max_mol_atoms) > lib().enflow_max_atoms()
+
+
+def large_workspace(num_mols, num_atoms, max_mol_atoms, nf, device):
+    """Device workspace of the large-system kernels (uint8, cached per device;
+    grown on demand, never shrunk)."""
+    need = lib().enflow_lf_large_workspace_size(num_mols, num_atoms, int(max_mol_atoms), nf)
+    if need < 0:
+        raise HipPathError("enflow_lf_large_workspace_size: bad arguments")
+    key = str(device)
+    ws = _large_ws.get(key)
+    if ws is None or ws.numel() < need:
+        ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
+        _large_ws[key] = ws
+    return ws
 
 
 def raise_on_err(err_flag):

@@ -5,7 +5,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-SRCS = [os.path.join(CSRC, f) for f in ("enflow_flow.hip", "enflow_backward.hip")
+SRCS = [os.path.join(CSRC, f) for f in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip")
         if os.path.exists(os.path.join(CSRC, f))]
 OUT = os.path.join(HERE, "libenflow_hip.so")
 ARCH = os.environ.get("ENFLOW_OFFLOAD_ARCH", "gfx950")
@@ -19,21 +19,30 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     # one hipcc per source, in parallel, then one link
     base = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
             "-I", os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
+    # objects are kept next to the library (git-ignored) and reused while they are
+    # newer than their source, the shared headers and this build's flags
     objs = [out + "." + os.path.basename(src) + ".o" for src in SRCS]
+    stamp = out + ".flags"
+    flags = " ".join(base)
+    same_flags = os.path.exists(stamp) and open(stamp).read() == flags
+    hdrs = [os.path.join(CSRC, "flow_device.h"), os.path.join(ROOT, "include", "enflow_hip.h")]
     procs = []
     for src, obj in zip(SRCS, objs):
+        if (not force and same_flags and os.path.exists(obj) and
+                all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in [src] + hdrs)):
+            continue
         cmd = base + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append(subprocess.Popen(cmd))
     if any(p.wait() != 0 for p in procs):
         raise subprocess.CalledProcessError(1, "hipcc")
+    with open(stamp, "w") as fh:
+        fh.write(flags)
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    for obj in objs:
-        os.remove(obj)
     os.replace(out + ".tmp", out)
     return out
 

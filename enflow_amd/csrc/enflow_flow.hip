@@ -470,15 +470,19 @@ __global__ void __launch_bounds__(BLOCK) neighbour_pairs_kernel(FlowArgs A, int 
 template <int NMAX>
 __global__ void __launch_bounds__(BLOCK) nll_mol_kernel(const int32_t* mol_ptr, int nf, const float* h, const float* g,
                                                       const float* pos, const float* vel, float softening, float* out) {
-  __shared__ float spos[NMAX * 3];
+  // NMAX == 0: molecules past the LDS image (large-system path) read pos from global memory
+  __shared__ float spos_l[NMAX > 0 ? NMAX * 3 : 1];
   __shared__ float red[4][WAVES];
   const int m = blockIdx.x, tid = threadIdx.x;
   const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
-  for (int e = tid; e < n * 3; e += BLOCK) spos[e] = pos[(size_t)a0 * 3 + e];
-  __syncthreads();
+  const float* spos = NMAX > 0 ? spos_l : pos + (size_t)a0 * 3;
+  if constexpr (NMAX > 0) {
+    for (int e = tid; e < n * 3; e += BLOCK) spos_l[e] = pos[(size_t)a0 * 3 + e];
+    __syncthreads();
+  }
   float lj = 0.f, v2 = 0.f, h2 = 0.f, g2 = 0.f;
-  for (int e = tid; e < n * n; e += BLOCK) {
-    const int i = e / n, k = e - i * n;
+  for (long long e = tid; e < (long long)n * n; e += BLOCK) {
+    const int i = (int)(e / n), k = (int)(e - (long long)i * n);
     if (k <= i) continue;
     const float dx = spos[i * 3] - spos[k * 3], dy = spos[i * 3 + 1] - spos[k * 3 + 1], dz = spos[i * 3 + 2] - spos[k * 3 + 2];
     const float d2 = dx * dx + dy * dy + dz * dz;
@@ -772,14 +776,16 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
                               const float* pos, const float* vel, const float* ldj_total,
                               float kBT, float softening, float partition_func,
                               float* nll_mol, float* loss, void* stream) {
-  if (num_mols < 0 || max_mol_atoms > MAX_ATOMS || nf < 1) return -1;
+  if (num_mols < 0 || max_mol_atoms < 0 || nf < 1) return -1;
   if (num_mols > 0) {
     if (max_mol_atoms <= 32)
       hipLaunchKernelGGL((nll_mol_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
     else if (max_mol_atoms <= 64)
       hipLaunchKernelGGL((nll_mol_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
-    else
+    else if (max_mol_atoms <= MAX_ATOMS)
       hipLaunchKernelGGL((nll_mol_kernel<256>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+    else
+      hipLaunchKernelGGL((nll_mol_kernel<0>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
   }
   hipLaunchKernelGGL(reduce_nll_kernel, dim3(1), dim3(BLOCK), 0, S(stream), nll_mol, num_mols, num_atoms, ldj_total,
                      kBT, partition_func, loss);

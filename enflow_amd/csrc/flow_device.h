@@ -10,7 +10,7 @@
 
 #include "enflow_hip.h"
 
-#define ENFLOW_ABI 3
+#define ENFLOW_ABI 4
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8
@@ -924,10 +924,19 @@ __device__ __forceinline__ void build_pairs(S& sm, const MolRef& M, int tid) {
 // ---------------------------------------------------------------------------
 // EGCL edge part: per-pair MLP chain on MFMA + deterministic segment sums
 // ---------------------------------------------------------------------------
-template <int H, int NMAX, int RB, int PREC = PREC_F32, bool VAR = false>
+//
+// BIG (large-system path, enflow_large.hip): the image holds only the block's
+// rows; pair words are (row | col << 5 | mult << 27) and the column atoms'
+// positions / features are read from global memory (cpos / ch, molecule-local
+// rows, L2-resident).
+template <bool BIG>
+__device__ __forceinline__ int pair_row(uint32_t pr) { return BIG ? (int)(pr & 31u) : (int)(pr & 0xffu); }
+
+template <int H, int NMAX, int RB, int PREC = PREC_F32, bool VAR = false, bool BIG = false>
 __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                            const MolRef& M, int nf, int tid, int r0, int rb,
-                                           bool zero_agg STAMP_ARGS) {
+                                           bool zero_agg STAMP_ARGS, const float* __restrict__ cpos = nullptr,
+                                           const float* __restrict__ ch = nullptr) {
   constexpr int NT = H / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
@@ -961,8 +970,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     int hr = -1, ih = 0;
     if (t0 < T) {
       const int p0 = t0 * 32;
-      hr = (int)(sm.pairs[p0] & 0xffu);
-      ih = (p0 > 0) && ((int)(sm.pairs[p0 - 1] & 0xffu) == hr);
+      hr = pair_row<BIG>(sm.pairs[p0]);
+      ih = (p0 > 0) && (pair_row<BIG>(sm.pairs[p0 - 1]) == hr);
     }
     sm.headrow[tid] = hr;
     sm.ishead[tid] = ih;
@@ -989,9 +998,19 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     const int p = tile * 32 + j;
     const bool valid = p < P;
     const uint32_t pr = valid ? sm.pairs[p] : 0u;
-    const int il = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
+    const int il = pair_row<BIG>(pr);
+    const int jl = BIG ? (int)((pr >> 5) & 0x3fffffu) : (int)((pr >> 8) & 0xffu);
     const int i = r0 + il;                 // atom of the row (il: row within the block)
-    const float c = (float)(pr >> 16);
+    const float c = (float)(BIG ? (pr >> 27) : (pr >> 16));
+    // column atom's coordinates / features: LDS image, or global (BIG)
+    auto cp = [&](int d) {
+      if constexpr (BIG) return cpos[(size_t)jl * 3 + d];
+      else return sm.pos[jl * 3 + d];
+    };
+    auto chf = [&](int k) {   // k < nf
+      if constexpr (BIG) return ch[(size_t)jl * nf + k];
+      else return sm.h[jl * NFP + k];
+    };
     // segments = runs of equal row; invalid lanes get unique rows of their own
     const int row = valid ? il : -1 - j;
     const SegMasks SM = seg_masks(row);
@@ -999,9 +1018,9 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     const bool seg_end = valid && (j == 31 || row_next != row);
     float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? il : 0) * AST];
     // Edges.coord_diff with the reference's half-box image (base.py:15-19)
-    const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
-    const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
-    const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], hbz);
+    const float dx = pbc1(sm.pos[i * 3 + 0] - cp(0), hbx);
+    const float dy = pbc1(sm.pos[i * 3 + 1] - cp(1), hby);
+    const float dz = pbc1(sm.pos[i * 3 + 2] - cp(2), hbz);
     const float radial = dx * dx + dy * dy + dz * dz;                 // egcl.py:79
 
     // ---- GEMM0: X0^T = edge_nn.0.weight . [h_i, h_j, radial]^T  (egcl.py:57-58)
@@ -1020,7 +1039,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
           const int k = 16 * ks + 8 * hh + jj;
           float v = 0.f;
           if (k < nf) v = sm.h[i * NFP + k];
-          else if (k < 2 * nf) v = sm.h[jl * NFP + k - nf];
+          else if (k < 2 * nf) v = chf(k - nf);
           else if (k == 2 * nf) v = radial;
           in[jj] = v;
         }
@@ -1055,8 +1074,14 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
           for (int t = 0; t < NT; ++t) nxt[t] = bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s + 1) * 64) * 4);
         }
-        const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh]
-                      : (s < NFMAX ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : (hh == 0 ? radial : 0.f));
+        float hj;
+        if constexpr (BIG) {   // global rows are not zero-padded past nf
+          const int kj = 2 * (s - NFMAX / 2) + hh;
+          hj = (s >= NFMAX / 2 && s < NFMAX && kj < nf) ? chf(kj) : 0.f;
+        } else {
+          hj = (s >= NFMAX / 2 && s < NFMAX) ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : 0.f;
+        }
+        const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh] : (s < NFMAX ? hj : (hh == 0 ? radial : 0.f));
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int t = 0; t < NT; ++t) x0[t] = mfma32(cur[t], b, x0[t]);

@@ -48,6 +48,36 @@ class Edges:
         return int(self.mol_ptr.numel() - 1)
 
     # ---- explicit list (materialised on demand)
+    def _materialise_large(self, L, dev, M, n):
+        """Systems past the fused kernels' LDS image: per-row (label, mult)
+        words from enflow_neighbour_pairs_large_f32, merged per (row, col)."""
+        A = self.pos.shape[0]
+        pos = self.pos.to(torch.float32).contiguous()
+        box = self.box.to(torch.float32).contiguous()
+        rc = torch.as_tensor(self.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous()
+        ptr = self.mol_ptr
+        npairs = torch.empty(max(A, 1), dtype=torch.int32, device=dev)
+        words = torch.empty((max(A, 1), n), dtype=torch.int32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        ws = _lib.large_workspace(M, A, n, 1, dev)
+        _lib.check(L.enflow_neighbour_pairs_large_f32(M, A, n, _lib.ptr(ptr), _lib.ptr(rc), _lib.ptr(box),
+                                                      _lib.ptr(pos), _lib.ptr(npairs), _lib.ptr(words),
+                                                      _lib.ptr(err), _lib.ptr(ws), ws.numel(),
+                                                      _lib.stream_ptr(dev)), "enflow_neighbour_pairs_large_f32")
+        _lib.raise_on_err(err)
+        cnt = npairs[:A].long()
+        valid = torch.arange(n, device=dev)[None, :] < cnt[:, None]
+        w = words[:A][valid].long() & 0xFFFFFFFF
+        row = torch.arange(A, device=dev).repeat_interleave(cnt)
+        mol = torch.searchsorted(ptr.long(), row, right=True) - 1
+        off = ptr[:-1].long()[mol]
+        col = ((w >> 5) & 0x3FFFFF) + off
+        key, inv = torch.unique(row * max(A, 1) + col, return_inverse=True)
+        mult = torch.zeros(key.numel(), dtype=torch.long, device=dev).index_add_(0, inv, w >> 27)
+        row, col = key // max(A, 1), key % max(A, 1)
+        mol = torch.searchsorted(ptr.long(), row, right=True) - 1
+        return row, col, mult, mol
+
     def _materialise(self):
         if self._pairs is not None:
             return self._pairs
@@ -56,6 +86,9 @@ class Edges:
         dev = self.pos.device
         M = self.num_mols
         n = self.max_mol_atoms
+        if _lib.is_large(n):
+            self._pairs = self._materialise_large(L, dev, M, n)
+            return self._pairs
         max_pairs = max(n * (n - 1), 1)
         pairs = torch.empty((M, max_pairs), dtype=torch.int32, device=dev)
         count = torch.empty(M, dtype=torch.int32, device=dev)

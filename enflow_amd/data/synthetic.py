@@ -102,6 +102,50 @@ def make_molecules(num_mols, n_atoms=22, nf=5, seed=0, r_cut_ang=3.0,
                 mol_ptr=mol_ptr)
 
 
+def arrange_points_on_grid(n, box, gap):
+    """n points on a regular grid inside [gap, box - gap] (the LJ dataset's
+    start configuration, enflow/data/lj.py:9-28)."""
+    num_z = int(np.ceil(n ** (1 / 3)))
+    num_y = int(np.ceil((n / num_z) ** 0.5))
+    num_x = int(np.ceil(n / (num_y * num_z)))
+    x = np.linspace(gap, box[0] - gap, num_x)
+    y = np.linspace(gap, box[1] - gap, num_y)
+    z = np.linspace(gap, box[2] - gap, num_z)
+    xv, yv, zv = np.meshgrid(x, y, z)
+    return np.stack((xv.flatten(), yv.flatten(), zv.flatten()), axis=-1)[:n]
+
+
+def make_lj_systems(n_atoms, num_systems=1, density=0.8, r_cut=2.5, nf=5, seed=0, kelvin=120.0,
+                    jitter=0.15):
+    """Periodic Lennard-Jones boxes shaped like the reference's LJ dataset
+    (enflow/data/lj.py + simulated.py:36-76; example/generate.yaml: one
+    2944-atom box), in LJ units: atoms on the start grid plus a random
+    displacement (a thermalised liquid instead of an OpenMM trajectory,
+    which needs openmm), wrapped into the box (apply_pbc) and centred;
+    h, g ~ N(0, 1/sqrt(kBT)) (simulated.py:56-58), Maxwell-Boltzmann
+    velocities.  ``n_atoms``: int or per-system sequence; box edge
+    (n / density)^(1/3)."""
+    rng = np.random.default_rng(seed)
+    sizes = [int(n_atoms)] * num_systems if np.isscalar(n_atoms) else [int(x) for x in n_atoms]
+    kBT = kelvin_to_lj(kelvin)
+    hs, gs, ps, vs, bs = [], [], [], [], []
+    for n in sizes:
+        L = (n / density) ** (1.0 / 3.0)
+        box = np.array([L, L, L])
+        pos = arrange_points_on_grid(n, box, 0.5) + rng.uniform(-jitter, jitter, size=(n, 3))
+        pos = pos - np.round(pos / box) * box                     # apply_pbc
+        pos = pos - pos.mean(axis=0, keepdims=True)               # Center
+        hs.append(rng.normal(0, 1 / np.sqrt(kBT), size=(n, nf)))
+        gs.append(rng.normal(0, 1 / np.sqrt(kBT), size=(n, nf)))
+        ps.append(pos)
+        vs.append(rng.normal(scale=np.sqrt(kBT), size=(n, 3)))
+        bs.append(np.repeat(box[None, :], n, axis=0))
+    mol_ptr = np.zeros(len(sizes) + 1, dtype=np.int64)
+    mol_ptr[1:] = np.cumsum(sizes)
+    return dict(h=np.concatenate(hs), g=np.concatenate(gs), pos=np.concatenate(ps), vel=np.concatenate(vs),
+                box=np.concatenate(bs), r_cut=np.full(len(sizes), float(r_cut)), mol_ptr=mol_ptr)
+
+
 def default_dt(ps=1.0):
     """dynamics.dt = 1 ps converted like main.py:113."""
     return time_to_lj(ps, 'pico')

@@ -4,7 +4,10 @@
 run the whole flow -- dequantisation, every layer's periodic neighbour list,
 EGCL and leapfrog update, and the log|detJ| sum -- as ONE HIP kernel launch
 (enflow_lf_forward_f32 / enflow_lf_reverse_f32): one workgroup per molecule,
-molecule state resident in LDS across layers.  Like the reference, ``data`` is
+molecule state resident in LDS across layers.  Systems larger than that LDS
+image (> enflow_max_atoms() atoms, e.g. the reference's 2944-atom LJ box in
+example/generate.yaml) run layer by layer through the large-system kernels
+(enflow_lf_forward_large_f32 / enflow_lf_reverse_large_f32).  Like the reference, ``data`` is
 updated (its tensors rebound) and returned.
 
 VVIntegrator (dynamics.py:39-86) is not provided: in the reference it cannot
@@ -121,13 +124,29 @@ class LFIntegrator(BaseFlow):
     def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
                         ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None):
         """In-place fused forward on preallocated fp32 device buffers (no
-        host sync, no allocation): the entry point the benchmark times."""
+        host sync, no allocation): the entry point the benchmark times.
+        Molecules past the fused kernel's LDS image (> enflow_max_atoms())
+        go through the layer-by-layer large-system kernels
+        (enflow_lf_forward_large_f32; needs a workspace, allocated once per
+        shape)."""
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         dev = h.device
         dq = self.dequantize.packed(dev) if kind == _lib.DEQUANT_ARGMAX else None
         scale = float(getattr(self.dequantize, "dequant_scale", 1.0)) if kind == _lib.DEQUANT_FLOOR else 0.0
         L = _lib.lib()
+        if _lib.is_large(max_mol_atoms):
+            if tape is not None:
+                raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
+            ws = _lib.large_workspace(mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, dev)
+            _lib.check(L.enflow_lf_forward_large_f32(
+                mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
+                _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
+                _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
+                _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
+                _lib.ptr(err), self._prec(), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)),
+                "enflow_lf_forward_large_f32")
+            return
         _lib.check(L.enflow_lf_forward_f32(
             mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
             _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
@@ -143,6 +162,15 @@ class LFIntegrator(BaseFlow):
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         L = _lib.lib()
+        if _lib.is_large(max_mol_atoms):
+            ws = _lib.large_workspace(mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, h.device)
+            _lib.check(L.enflow_lf_reverse_large_f32(
+                mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
+                _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
+                _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
+                _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), self._prec(), _lib.ptr(ws), ws.numel(),
+                _lib.stream_ptr(h.device)), "enflow_lf_reverse_large_f32")
+            return
         _lib.check(L.enflow_lf_reverse_f32(
             mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
             _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
@@ -205,12 +233,8 @@ class LFIntegrator(BaseFlow):
         mx = torch.zeros(1, dtype=torch.int32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         L = _lib.lib()
-        _lib.check(L.enflow_lf_reverse_f32(
-            s["mol_ptr"].numel() - 1, n, s["max_n"], nf, hid, _lib.ptr(s["mol_ptr"]), _lib.ptr(s["r_cut"]),
-            _lib.ptr(s["box"]), _lib.ptr(s["h"]), _lib.ptr(s["g"]), _lib.ptr(s["pos"]), _lib.ptr(s["vel"]),
-            _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, float(self.dt), cw,
-            _lib.ptr(idx), _lib.ptr(mx), _lib.ptr(err), self._prec(), _lib.stream_ptr(dev)),
-            "enflow_lf_reverse_f32")
+        self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"], s["max_n"],
+                             idx, mx, err)
         if check_errors:
             _lib.raise_on_err(err)
         dt = data.h.dtype

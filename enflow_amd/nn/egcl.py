@@ -133,6 +133,16 @@ class EGCL(nn.Module):
         F = torch.empty((n, 3), dtype=torch.float32, device=dev)
         G = torch.empty((n, nf), dtype=torch.float32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
+        if _lib.is_large(edges.max_mol_atoms):   # past the fused kernels' LDS image
+            ws = _lib.large_workspace(edges.num_mols, n, edges.max_mol_atoms, nf, dev)
+            prec = _lib.PREC_F32 | (_lib.EGCL_VARIANTS if self.variant_flags() else 0)
+            _lib.check(L.enflow_egcl_forward_large_f32(
+                edges.num_mols, n, edges.max_mol_atoms, nf, self.hidden_nf, _lib.ptr(edges.mol_ptr),
+                _lib.ptr(rc), _lib.ptr(box), _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),
+                float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F), _lib.ptr(G), _lib.ptr(err), prec,
+                _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)), "enflow_egcl_forward_large_f32")
+            _lib.raise_on_err(err)
+            return (Q.reshape(n, 1).to(h.dtype), F.to(h.dtype), G.to(h.dtype))
         _lib.check(L.enflow_egcl_forward_f32(edges.num_mols, n, edges.max_mol_atoms, nf, self.hidden_nf,
                                              _lib.ptr(edges.mol_ptr), _lib.ptr(rc), _lib.ptr(box),
                                              _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),

@@ -19,7 +19,8 @@
  *     images than atoms) are reported through err_flag (device int32, OR-ed
  *     ENFLOW_ERR_* bits) which the host reads after the stream syncs.
  *   - max_mol_atoms is the largest molecule in the batch (host-known from
- *     Data.N); it selects the kernel instantiation (<= 32 or <= 64 atoms);
+ *     Data.N); it selects the kernel instantiation (<= 32, <= 64 or <= 256
+ *     atoms; larger systems go through the *_large_* entry points);
  *   - all arithmetic is float32 (the reference computes in float64; parity is
  *     1e-5 relative).
  */
@@ -145,6 +146,54 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
                           int dequant_kind, float dt, float coords_weight,
                           int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
                           int gemm_precision, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Large systems: molecules / periodic boxes with more than enflow_max_atoms()
+ * atoms (e.g. the reference's example/generate.yaml, one 2944-atom LJ box).
+ * Same operators, arguments and results as enflow_lf_forward_f32 /
+ * enflow_lf_reverse_f32 / enflow_egcl_forward_f32 (LFIntegrator.forward /
+ * .reverse, enflow/flow/dynamics.py:10-37; EGCL.forward, enflow/nn/egcl.py:76-92;
+ * neighbour list enflow/data/base.py:122-144), any molecule size below 2^22
+ * atoms, without the training tape.  Each layer runs as grid-wide launches
+ * (image masks, id_mapping, pair words, one workgroup per 32-row block), so
+ * `workspace` (device, enflow_lf_large_workspace_size bytes, no
+ * initialisation needed) holds the per-layer neighbour list: 4 x max_mol_atoms
+ * bytes per atom plus O(atoms).  Returns -6 if workspace_bytes is too small.
+ * ---------------------------------------------------------------------- */
+int64_t enflow_lf_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int node_nf);
+
+int enflow_lf_forward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                                const int32_t* mol_ptr, const float* r_cut, const float* box,
+                                float* h, float* g, float* pos, float* vel,
+                                const float* layers, int n_layers,
+                                int dequant_kind, const float* dequant, const float* noise,
+                                float dequant_scale, float dt, float coords_weight,
+                                float* ldj_mol, float* ldj_total, int32_t* err_flag, int gemm_precision,
+                                void* workspace, int64_t workspace_bytes, void* stream);
+
+int enflow_lf_reverse_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                                const int32_t* mol_ptr, const float* r_cut, const float* box,
+                                float* h, float* g, float* pos, float* vel,
+                                const float* layers, int n_layers,
+                                int dequant_kind, float dt, float coords_weight,
+                                int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
+                                int gemm_precision, void* workspace, int64_t workspace_bytes, void* stream);
+
+int enflow_egcl_forward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                                  const int32_t* mol_ptr, const float* r_cut, const float* box,
+                                  const float* h, const float* pos, const float* layer,
+                                  float coords_weight, float* Q, float* F, float* G,
+                                  int32_t* err_flag, int gemm_precision,
+                                  void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Data.edges for large systems (base.py:122-144): per row atom a, npairs[a]
+ * words in pairs[a * max_mol_atoms ...], each (col << 5) | (multiplicity << 27)
+ * with col the molecule-local column label; one word per column atom q with a
+ * hit (a label can repeat within a row: sum the multiplicities per label). */
+int enflow_neighbour_pairs_large_f32(int num_mols, int num_atoms, int max_mol_atoms, const int32_t* mol_ptr,
+                                     const float* r_cut, const float* box, const float* pos,
+                                     int32_t* npairs, uint32_t* pairs, int32_t* err_flag,
+                                     void* workspace, int64_t workspace_bytes, void* stream);
 
 /* helpers.one_hot (enflow/utils/helpers.py:43-52): out[num_atoms][width]. */
 int enflow_one_hot_f32(const int32_t* idx, int num_atoms, int width, float* out,

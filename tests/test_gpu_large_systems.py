@@ -1,0 +1,173 @@
+"""GPU parity for systems past the fused kernels' LDS image (> 256 atoms):
+the layer-by-layer large-system kernels (enflow_amd/csrc/enflow_large.hip)
+against the CPU oracle, on periodic Lennard-Jones boxes shaped like the
+reference's LJ dataset (example/generate.yaml: one 2944-atom box, batch 1).
+
+Oracle comparisons at 300-700 atoms (the float64 oracle builds the
+reference's dense 27n x n distance matrix); at the example's 2944 atoms the
+size-independent properties: forward -> reverse round trip and bitwise
+determinism.  Tolerances as
+tests/test_gpu_parity.py: 1e-5 normwise, neighbour lists exact."""
+import collections
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import enflow_oracle as O
+from _fixtures import rel_err
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda:0"
+
+
+def _boxes(sizes, seed, nf=5, **kw):
+    from enflow_amd.data.synthetic import make_lj_systems
+    b = make_lj_systems(sizes, nf=nf, seed=seed, **kw)
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        b[k] = b[k].astype(np.float32).astype(np.float64)
+    return b
+
+
+def _model(hid, nf, n_layers, seed, **egcl_kw):
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data.synthetic import default_dt
+    torch.manual_seed(seed)
+    nets = [EGCL(nf, nf, hid, **egcl_kw) for _ in range(n_layers)]
+    return LFIntegrator(nets, ArgMax(nf, hid), dt=default_dt()).to(DEV)
+
+
+def _np_params(module):
+    return {k: v.detach().double().cpu().numpy() for k, v in module.state_dict().items()}
+
+
+def _layer_params(net):
+    p = _np_params(net)
+    p["flags"] = (bool(net.attention), bool(net.norm_diff), bool(net.tanh))
+    return p
+
+
+def test_large_pairs_exact():
+    """Data.edges of two LJ boxes (420 and 333 atoms): exact edge multiset."""
+    from enflow_amd.data import Data
+    b = _boxes([420, 333], 3)
+    e = Data.from_arrays(b, device=DEV).edges
+    got = collections.Counter(zip(e.row.cpu().tolist(), e.col.cpu().tolist()))
+    row, col, _ = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    assert got == collections.Counter(zip(row.tolist(), col.tolist()))
+    assert len(row) > 20000
+
+
+@pytest.mark.parametrize("hid,variants", [(128, {}), (64, dict(attention=True, norm_diff=True, tanh=True))])
+def test_large_egcl_vs_oracle(hid, variants):
+    from enflow_amd.nn import EGCL
+    from enflow_amd.data import Data
+    b = _boxes([700], 4)
+    torch.manual_seed(2)
+    net = EGCL(5, 5, hid, **variants).to(DEV)
+    d = Data.from_arrays(b, device=DEV)
+    with torch.no_grad():
+        q, f, g = net(d.h, d.edges)
+    row, col, eb = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    p = _layer_params(net)
+    rq, rf, rg = O.egcl_forward(p, b["h"], row, col, O.coord_diff(b["pos"], row, col, eb))
+    assert rel_err(q.cpu().numpy(), rq) < TOL
+    assert rel_err(f.cpu().numpy(), rf) < TOL
+    assert rel_err(g.cpu().numpy(), rg) < TOL
+
+
+@pytest.mark.parametrize("prec", ["f32", "f16x3"])
+def test_large_flow_vs_oracle(prec):
+    """Ragged batch (a 300-atom box, a 5-atom molecule, a 520-atom box): the
+    whole batch goes through the large-system kernels."""
+    from enflow_amd.data import Data
+    b = _boxes([300, 5, 520], 5)
+    model = _model(128, 5, 3, 6)
+    model.gemm_precision = prec
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(7))
+    with torch.no_grad():
+        o, ldj = model(d, noise=noise)
+    layers = [_layer_params(n) for n in model.networks]
+    ref, ref_ldj = O.lf_forward(layers, _np_params(model.dequantize), b, noise.cpu().double().numpy(), model.dt)
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
+    # reverse of the oracle's output vs the oracle's reverse
+    st = {k: ref[k].astype(np.float32).astype(np.float64) for k in ("h", "g", "pos", "vel")}
+    st.update(box=b["box"], r_cut=b["r_cut"], mol_ptr=b["mol_ptr"])
+    with torch.no_grad():
+        back = model.reverse(Data.from_arrays(st, device=DEV))
+    rback = O.lf_reverse(layers, st, model.dt)
+    np.testing.assert_array_equal(back.h.cpu().numpy(), rback["h"])
+    for k in ("g", "pos", "vel"):
+        assert rel_err(getattr(back, k).cpu().numpy(), rback[k]) < 1e-4, k
+
+
+def test_large_flow_variants_vs_oracle():
+    from enflow_amd.data import Data
+    b = _boxes([400], 11)
+    model = _model(64, 5, 2, 12, attention=True, norm_diff=True, tanh=True)
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(13))
+    with torch.no_grad():
+        o, ldj = model(d, noise=noise)
+    layers = [_layer_params(n) for n in model.networks]
+    ref, ref_ldj = O.lf_forward(layers, _np_params(model.dequantize), b, noise.cpu().double().numpy(), model.dt)
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
+
+
+def test_large_nll_vs_oracle():
+    from enflow_amd.data import Data
+    from enflow_amd.flow import Alchemical_NLL
+    b = _boxes([600], 14)
+    d = Data.from_arrays(b, device=DEV)
+    ldj = torch.tensor(3.25, device=DEV)
+    loss = Alchemical_NLL(kBT=1.0, softening=0.1)(d, ldj)
+    ref = O.alchemical_nll(b, 3.25, 1.0, softening=0.1)
+    assert abs(float(loss) - ref) <= 1e-5 * abs(ref)
+
+
+def test_generate_example_box_2944():
+    """example/generate.yaml's system: one 2944-atom LJ box, 8 layers, H=128.
+    Forward -> reverse returns the input (one-hot h exactly, vel / g per
+    atom), and two runs are bitwise identical."""
+    from enflow_amd.data import Data
+    b = _boxes([2944], 21, nf=5)
+    # wrapped into the pbc range: the dataset's Center transform runs after
+    # apply_pbc, and an atom outside [-L/2, L/2] comes back wrapped, which
+    # re-labels the reference's id_mapping (the float64 oracle shows the same)
+    b["pos"] = O.apply_pbc(b["pos"], b["box"]).astype(np.float32).astype(np.float64)
+    onehot = np.eye(5)[np.random.default_rng(0).integers(0, 5, 2944)]
+    b["h"] = onehot
+    model = _model(128, 5, 8, 22)
+    noise = torch.randn((2944, 5), device=DEV, generator=torch.Generator(DEV).manual_seed(23))
+    outs = []
+    for _ in range(2):
+        with torch.no_grad():
+            o, ldj = model(Data.from_arrays(b, device=DEV), noise=noise)
+        outs.append((o.pos.clone(), o.h.clone(), o.vel.clone(), float(ldj)))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert outs[0][3] == outs[1][3] and np.isfinite(outs[0][3])
+    with torch.no_grad():
+        back = model.reverse(o)
+    np.testing.assert_array_equal(back.h.cpu().numpy(), onehot)
+    # in fp32 a pair within ~1e-6 of r_cut can fall on the other side of the
+    # cut-off on the way back (~2 such pairs expected over 8 layers at 2944
+    # atoms); the atoms they touch are allowed to miss, nobody else
+    for k in ("vel", "g", "pos"):
+        got, want = getattr(back, k).cpu().numpy(), b[k]
+        bad = np.abs(got - want).max(axis=1) > 1e-4 * np.abs(want).max()
+        assert bad.mean() < 0.01, (k, int(bad.sum()))
+
+
+def test_large_training_is_rejected():
+    from enflow_amd.data import Data
+    b = _boxes([300], 8)
+    model = _model(32, 5, 1, 9)
+    with pytest.raises(NotImplementedError):
+        model(Data.from_arrays(b, device=DEV))

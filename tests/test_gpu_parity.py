@@ -219,15 +219,25 @@ def test_floor_dequant_vs_oracle():
     assert (got == want).mean() > 0.99, (len(bad), info)
 
 
-def test_too_large_molecule_raises():
+def test_molecule_past_fused_image_takes_large_path():
+    """257 atoms: one past the fused kernels' LDS image -> the layer-by-layer
+    large-system kernels (enflow_lf_forward_large_f32), same results."""
     from enflow_amd.data import Data
     from enflow_amd.data.synthetic import make_molecules
     from enflow_amd import _lib
-    model = _make_model(32, 5, 1, 0, 0.01)
-    d = Data.from_arrays(make_molecules(1, 257, seed=0, chain=True), device=DEV)
-    with pytest.raises(_lib.HipPathError):
-        with torch.no_grad():
-            model(d)
+    assert _lib.is_large(257) and not _lib.is_large(256)
+    b = _f32(make_molecules(1, 257, seed=0, chain=True))
+    model = _make_model(32, 5, 2, 0, 0.01)
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(1))
+    with torch.no_grad():
+        o, ldj = model(d, noise=noise)
+    layers = [{k: v.detach().double().cpu().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    dq = {k: v.detach().double().cpu().numpy() for k, v in model.dequantize.state_dict().items()}
+    ref, ref_ldj = O.lf_forward(layers, dq, b, noise.cpu().double().numpy(), model.dt)
+    for k in ("h", "g", "pos", "vel"):
+        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
 
 
 # ---------------------------------------------------------------------------
