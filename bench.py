@@ -29,6 +29,21 @@ sys.path.insert(0, ROOT)
 
 METRIC = "molecule-transforms/sec (fwd+log|detJ|), batch 1024×22 atoms, 1/2/4/8 GPU"
 PEAK_F32_MFMA_TFLOPS = 157.3      # MI355X_MICROARCH.md: dense f32 MFMA (= f32 vector) peak
+PEAK_F16_MFMA_TFLOPS = 2500.0     # MI355X_MICROARCH.md: dense BF16/F16 MFMA peak (spec, no sparsity)
+PRODUCTS = {"f32": 1, "f16x3": 3, "bf16": 1}   # MFMA products per fp32-equivalent GEMM FLOP
+
+
+def matrix_pipe(achieved, prec):
+    """What the matrix cores actually issue: f16x3 runs every fp32 GEMM FLOP as
+    3 split-fp16 products on the F16 pipe; bf16 as one BF16 product; f32 on the
+    F32 pipe.  Reported next to the fp32-equivalent roofline so neither hides
+    the other (upper bound: ignores the K padding of edge_nn.0 / node items)."""
+    if prec == "f32":
+        return {"dtype": "f32", "issued_tflops": achieved, "peak": PEAK_F32_MFMA_TFLOPS,
+                "frac": achieved / PEAK_F32_MFMA_TFLOPS}
+    issued = achieved * PRODUCTS[prec]
+    return {"dtype": "f16" if prec == "f16x3" else "bf16", "products_per_flop": PRODUCTS[prec],
+            "issued_tflops": issued, "peak": PEAK_F16_MFMA_TFLOPS, "frac": issued / PEAK_F16_MFMA_TFLOPS}
 MOLS_PER_GPU, ATOMS, LAYERS, HID, NF = 1024, 22, 8, 128, 5
 
 
@@ -306,7 +321,8 @@ def run_lj(args, world, rank, device, dist):
                          "frac": achieved / PEAK_F32_MFMA_TFLOPS, "traffic": None,
                          "kernel": "enflow_lf_reverse_large_f32 (per layer: images, id_mapping, pairs, "
                                    "lg_layer_kernel<128,1,false>)",
-                         "kernel_ms": kern_ms, "flops_per_launch": flops, "gemm_precision": model.gemm_precision},
+                         "kernel_ms": kern_ms, "flops_per_launch": flops, "gemm_precision": model.gemm_precision,
+                         "matrix_pipe": matrix_pipe(achieved, model.gemm_precision)},
             "cpu_baseline": None,
         }
         print(json.dumps(line), flush=True)
@@ -464,9 +480,11 @@ def main():
                          "kernel": f"lf_flow_kernel<128,{nmax},{str(c['reverse']).lower()},{prec_id}>",
                          "kernel_ms": kern_ms, "flops_per_launch": flops,
                          "gemm_precision": model.gemm_precision,
+                         "matrix_pipe": matrix_pipe(achieved, model.gemm_precision),
                          "note": "achieved = fp32-equivalent algorithmic FLOPs / event-timed launch; peak = dense "
                                  "f32 MFMA (the arithmetic the path delivers). f16x3 runs the GEMMs as 3 "
-                                 "split-fp16 products on the f16 MFMA pipe (see DESIGN.md)"},
+                                 "split-fp16 products on the f16 MFMA pipe: matrix_pipe is that pipe's "
+                                 "issued rate vs its dense peak (see DESIGN.md)"},
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline and args.mode == "forward":
