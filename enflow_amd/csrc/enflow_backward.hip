@@ -407,7 +407,10 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
 __device__ __forceinline__ size_t trow(size_t rtile, int W, int f, int j) {
   return ((rtile * W + f) << 5) + j;
 }
-template <int H, int NMAX, int PREC = ENFLOW_BWD_PREC>
+// VAR: layers may carry EGCL_NORM_DIFF / EGCL_TANH (read per layer from the
+// packed forward layer; a second instance so the default kernel keeps its
+// register allocation).  EGCL_ATTENTION is refused by the host.
+template <int H, int NMAX, bool VAR = false, int PREC = ENFLOW_BWD_PREC>
 __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   static_assert(PREC == PREC_F32 || PREC == PREC_F16X3, "backward: fp32-accurate precisions only");
   __shared__ BwdSmem<H, NMAX> sb;
@@ -582,6 +585,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const float inv2 = x3 ? B.Lp[L.scl + 3] : 1.f;
     const float inv0 = x3 ? B.Lp[L.scl + 5] : 1.f;
     auto nofill = [](int) {};
+    const int vfl = VAR ? (int)B.Lp[L.vfl] : 0;   // wave-uniform constructor variants
+    const bool v_nd = VAR && (vfl & EGCL_NORM_DIFF) != 0, v_tanh = VAR && (vfl & EGCL_TANH) != 0;
     // the molecule's tile-blocked rows (trow): buffer resources on its first
     // row, per element a wave-uniform byte offset (tile, feature) + the lane's
     const size_t nrow = (size_t)TT * 32;
@@ -723,13 +728,19 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
             cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
           }
         }
-      const float phi = part + __shfl_xor(part, 32, 64);
+      float phi = part + __shfl_xor(part, 32, 64);
+      if (v_tanh) phi = tanhf(phi);                             // egcl.py:40-42
+      // norm_diff: trans uses coord_diff / (|coord_diff| + 1) (egcl.py:82-84)
+      const float rr = v_nd ? sqrtf(radial) : 0.f;
+      const float nd = v_nd ? __builtin_amdgcn_rcpf(rr + 1.f) : 1.f;
+      const float dxn = dx * nd, dyn = dy * nd, dzn = dz * nd;
       // d phi from dF (egcl.py:71-74: mean over the row's edges, clamp, coords_weight)
       const float inv = B.cw / fmaxf((float)sm.cntrow[i], 1.f);
-      const float gx = fabsf(dx * phi) <= 100.f ? sb.aF[i * 3 + 0] * inv : 0.f;
-      const float gy = fabsf(dy * phi) <= 100.f ? sb.aF[i * 3 + 1] * inv : 0.f;
-      const float gz = fabsf(dz * phi) <= 100.f ? sb.aF[i * 3 + 2] * inv : 0.f;
-      const float aph = c * (gx * dx + gy * dy + gz * dz);
+      const float gx = fabsf(dxn * phi) <= 100.f ? sb.aF[i * 3 + 0] * inv : 0.f;
+      const float gy = fabsf(dyn * phi) <= 100.f ? sb.aF[i * 3 + 1] * inv : 0.f;
+      const float gz = fabsf(dzn * phi) <= 100.f ? sb.aF[i * 3 + 2] * inv : 0.f;
+      float aph = c * (gx * dxn + gy * dyn + gz * dzn);
+      if (v_tanh) aph *= 1.f - phi * phi;                       // d of coord_nn.2's output
       if (hh == 0 && !(ENFLOW_BWD_ABLATE & 1)) B.aphi[Rw] = aph;
       // d pre(coord_nn.0) = dphi * wc2 * silu'(c)   (not stored: outer_acc rebuilds it from pc)
 #pragma unroll
@@ -835,9 +846,16 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       }
       // d coord_diff (radial = |cd|^2, trans = cd * phi), d pos_i += ., d pos_j -= .
       const float sF = hh == 0 ? c * phi : 0.f;
-      const float tx = sF * gx + 2.f * dx * arad;
-      const float ty = sF * gy + 2.f * dy * arad;
-      const float tz = sF * gz + 2.f * dz * arad;
+      float ux = sF * gx, uy = sF * gy, uz = sF * gz;             // d (normalised) coord_diff
+      if (v_nd) {   // through cd / (|cd| + 1): nd u - nd^2 (u . cd) cd / |cd|
+        const float k2 = rr > 0.f ? nd * nd * (ux * dx + uy * dy + uz * dz) / rr : 0.f;
+        ux = nd * ux - k2 * dx;
+        uy = nd * uy - k2 * dy;
+        uz = nd * uz - k2 * dz;
+      }
+      const float tx = ux + 2.f * dx * arad;
+      const float ty = uy + 2.f * dy * arad;
+      const float tz = uz + 2.f * dz * arad;
       if (valid && (tx != 0.f || ty != 0.f || tz != 0.f)) {
         atomicAdd(&wacc[i * EW + nf + 0], tx);
         atomicAdd(&wacc[i * EW + nf + 1], ty);
@@ -1610,6 +1628,9 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
                            float* grad_layers, float* grad_dequant,
                            void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
                            int32_t* err_flag, void* stream) {
+  // dequant_kind may carry ENFLOW_EGCL_VARIANTS: layers with norm_diff / tanh flags
+  const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
+  dequant_kind &= 0xff;
   if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > NFMAX ||
       !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0 || pair_row_bound > 0x7fffffffLL)
     return -1;
@@ -1645,9 +1666,15 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     A.dp0 = ws + Wl.dp0; A.dpe = ws + Wl.dpe; A.aphi = ws + Wl.aphi;
     A.su = ws + Wl.su; A.au = ws + Wl.au; A.sn = ws + Wl.sn; A.an = ws + Wl.an;
     A.aq = ws + Wl.aq; A.agr = ws + Wl.agr; A.err = err_flag;
-#define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, A)
-    DISPATCH_HN_B(H, max_mol_atoms, CALL);
+    if (variants) {
+#define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, st, A)
+      DISPATCH_HN_B(H, max_mol_atoms, CALL);
 #undef CALL
+    } else {
+#define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, st, A)
+      DISPATCH_HN_B(H, max_mol_atoms, CALL);
+#undef CALL
+    }
     // the layer's weight gradients, straight into the torch parameter layout
     float* G = grad_layers + (size_t)l * R.total;
     const int32_t* prow = offs + (size_t)l * (num_mols + 1) + num_mols;

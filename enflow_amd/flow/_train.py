@@ -81,7 +81,7 @@ class _FlowFunction(torch.autograd.Function):
         _lib.check(L.enflow_lf_backward_f32(
             M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
             _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw),
-            n_layers, kind, _lib.ptr(dq_raw), _lib.ptr(h_in), _lib.ptr(meta["noise"]), float(flow.dt), cw,
+            n_layers, kind | (_lib.EGCL_VARIANTS if flow._has_variants() else 0), _lib.ptr(dq_raw), _lib.ptr(h_in), _lib.ptr(meta["noise"]), float(flow.dt), cw,
             _lib.ptr(ah), _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj),
             _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
             _lib.stream_ptr(dev)), "enflow_lf_backward_f32")
@@ -106,10 +106,7 @@ class _FlowFunction(torch.autograd.Function):
 
 def flow_forward_train(flow, data, noise, check_errors):
     """Differentiable LFIntegrator.forward (HIP forward with tape)."""
-    if any(n.variant_flags() for n in flow.networks):
-        raise NotImplementedError("the HIP training backward implements EGCL with the default flags "
-                                  "(attention=False, norm_diff=False, tanh=False); run the variants under "
-                                  "torch.no_grad() (forward / reverse)")
+    flow._check_trainable()
     s = flow._state(data)
     dev = s["dev"]
     kind = flow._dequant_kind()

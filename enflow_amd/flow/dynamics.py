@@ -94,10 +94,7 @@ class LFIntegrator(BaseFlow):
             return self._train_bufs
         hid, nf, _ = self._geometry()
         L = _lib.lib()
-        if any(n.variant_flags() for n in self.networks):
-            raise NotImplementedError("the HIP training backward implements EGCL with the default flags "
-                                      "(attention=False, norm_diff=False, tanh=False); the variants run "
-                                      "forward / reverse only")
+        self._check_trainable()
         raw = torch.cat([torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
                                     for p in n.raw_parameters()]) for n in self.networks])
         stride = L.enflow_egcl_bwd_packed_size(hid, nf)
@@ -110,6 +107,16 @@ class LFIntegrator(BaseFlow):
         self._train_bufs = (self.packed_layers(device), bwd, raw)
         self._train_key = key
         return self._train_bufs
+
+    def _has_variants(self):
+        return any(isinstance(n, EGCL) and n.variant_flags() for n in self.networks)
+
+    def _check_trainable(self):
+        """The HIP backward covers EGCL(norm_diff, tanh); attention layers run
+        forward / reverse only."""
+        if any(isinstance(n, EGCL) and (n.variant_flags() & _lib.EGCL_ATTENTION) for n in self.networks):
+            raise NotImplementedError("the HIP training backward does not implement EGCL(attention=True); "
+                                      "run attention layers under torch.no_grad() (forward / reverse)")
 
     def _needs_grad(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())

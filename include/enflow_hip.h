@@ -88,7 +88,7 @@ int enflow_pack_egcl_f32(const float* raw, int hidden_nf, int node_nf,
  * `att` = att_nn.0.weight [1][H] followed by att_nn.0.bias [1] (required with
  * ENFLOW_EGCL_ATTENTION, else ignored).  The flow / EGCL forward and reverse
  * kernels read the flags from the packed layer; the training backward
- * supports only flags == 0 (the host refuses the others). */
+ * supports NORM_DIFF and TANH (see enflow_lf_backward_f32), not ATTENTION. */
 int enflow_pack_egcl_ex_f32(const float* raw, int hidden_nf, int node_nf, int flags,
                             const float* att, float* packed, void* stream);
 
@@ -288,6 +288,10 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
  *   grad_layers       : out, [n_layers][EGCL parameter count] (named_parameters
  *                       order, torch layouts), grad_dequant: out, ArgMax layout
  *   workspace         : >= enflow_lf_backward_workspace_size bytes
+ *   dequant_kind      : ENFLOW_DEQUANT_*, OR-ed with ENFLOW_EGCL_VARIANTS when
+ *                       layers carry ENFLOW_EGCL_NORM_DIFF / ENFLOW_EGCL_TANH
+ *                       (the forward's layers; ENFLOW_EGCL_ATTENTION layers are
+ *                       not supported by the backward)
  */
 int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
                            const int32_t* mol_ptr, const float* r_cut, const float* box,

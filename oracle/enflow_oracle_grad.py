@@ -34,16 +34,24 @@ def _pbc(x, box):
     return x - torch.round(x / box) * box
 
 
-def _egcl(p, h, pos, row, col, eb, n, cw):
-    """EGCL.forward (enflow/nn/egcl.py:76-92), default flags."""
+def _egcl(p, h, pos, row, col, eb, n, cw, flags=(False, False, False)):
+    """EGCL.forward (enflow/nn/egcl.py:57-92); ``flags`` = the constructor's
+    (attention, norm_diff, tanh)."""
+    attention, norm_diff, tanh = (bool(x) for x in flags)
     cd = _pbc(pos[row] - pos[col], eb * 0.5)                                   # base.py:15-19
     radial = (cd ** 2).sum(1, keepdim=True)
+    if norm_diff:                                                              # egcl.py:82-84
+        cd = cd / (torch.sqrt(radial) + 1)
     x = torch.cat([h[row], h[col], radial], 1)
     e = _silu(F.linear(_silu(F.linear(x, p["edge_nn.0.weight"], p["edge_nn.0.bias"])),
                        p["edge_nn.2.weight"], p["edge_nn.2.bias"]))
+    if attention:                                                              # egcl.py:60-62
+        e = e * torch.sigmoid(F.linear(e, p["att_nn.0.weight"], p["att_nn.0.bias"]))
     q = F.linear(_silu(F.linear(h, p["vel_scaling_nn.0.weight"], p["vel_scaling_nn.0.bias"])),
                  p["vel_scaling_nn.2.weight"], p["vel_scaling_nn.2.bias"])
     phi = F.linear(_silu(F.linear(e, p["coord_nn.0.weight"], p["coord_nn.0.bias"])), p["coord_nn.2.weight"])
+    if tanh:                                                                   # egcl.py:40-42
+        phi = torch.tanh(phi)
     trans = torch.clamp(cd * phi, -100.0, 100.0)
     idx = row.unsqueeze(1).expand(-1, 3)
     fs = torch.zeros(n, 3, dtype=h.dtype).scatter_add(0, idx, trans)
@@ -98,10 +106,10 @@ def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partit
     box, r_cut = t(state["box"]), np.asarray(state["r_cut"], dtype=np.float64)
     h, ldj = _argmax(D, t(state["h"]), t(eps))
     g, pos, vel = t(state["g"]), t(state["pos"]), t(state["vel"])
-    for p in P:
+    for p, lp in zip(P, layers):
         row, col, eb = O.batch_edges(pos.detach().numpy(), state["box"], r_cut, mol_ptr)
         row_t, col_t = torch.as_tensor(row, dtype=torch.long), torch.as_tensor(col, dtype=torch.long)
-        q, f, gg = _egcl(p, h, pos, row_t, col_t, t(eb), n, coords_weight)
+        q, f, gg = _egcl(p, h, pos, row_t, col_t, t(eb), n, coords_weight, lp.get("flags", (0, 0, 0)))
         vel = torch.exp(q) * vel + f * dt
         g = g + gg * dt
         pos = _pbc(pos + vel * dt, box)

@@ -238,13 +238,17 @@ def case_flow(hid, n_layers, sizes, seed, name, flags=None):
     save(name, inp, fwd)
 
 
-def case_train(hid, n_layers, sizes, seed, name, nf=5):
+def case_train(hid, n_layers, sizes, seed, name, nf=5, flags=None):
     """One training step of the reference (enflow/main.py:217-221):
     out, ldj = model(data); loss = nll(out, ldj); loss.backward() -- the
-    parameter gradients of every EGCL layer and of the ArgMax dequantiser."""
+    parameter gradients of every EGCL layer and of the ArgMax dequantiser.
+    ``flags``: per layer (attention, norm_diff, tanh), default flags when None."""
     torch.manual_seed(seed)
     dt = default_dt()
-    nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+    if flags is None:
+        nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+    else:
+        nets = [EGCL(nf, nf, hid, attention=a, norm_diff=nd, tanh=th) for a, nd, th in flags]
     model = LFIntegrator(nets, ArgMax(nf, hid), dt=dt)   # BaseFlow casts to float64
     b = batch_inputs(len(sizes), sizes, nf, seed=seed)
     d = ref_data(b)
@@ -267,6 +271,8 @@ def case_train(hid, n_layers, sizes, seed, name, nf=5):
     for i, net in enumerate(model.networks):
         inp.update({f"p{i}.{k}": v.detach().numpy().astype(np.float32) for k, v in net.named_parameters()})
         res.update({f"grad_p{i}.{k}": v.grad.numpy() for k, v in net.named_parameters()})
+        if flags is not None:
+            inp[f"p{i}.flags"] = np.array(flags[i], dtype=np.int32)
     inp.update({f"dq.{k}": v.detach().numpy().astype(np.float32)
                 for k, v in model.dequantize.named_parameters()})
     res.update({f"grad_dq.{k}": v.grad.numpy() for k, v in model.dequantize.named_parameters()})
@@ -274,6 +280,11 @@ def case_train(hid, n_layers, sizes, seed, name, nf=5):
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "train_variants":
+        case_train(64, 2, [22, 40, 7], 41, "train_var_h64_L2", flags=[(False, True, True), (False, False, True)])
+        case_train(32, 3, [22, 9, 15, 3], 42, "train_var_h32_L3",
+                   flags=[(False, True, False), (False, True, True), (False, False, False)])
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "variants":
         case_egcl_variant(64, 31, (True, False, False), "egcl_h64_att")
         case_egcl_variant(32, 32, (False, True, True), "egcl_h32_nd_tanh")

@@ -40,7 +40,8 @@ def _train_step(model, data, eps, kBT, softening):
     return loss, ldj
 
 
-@pytest.mark.parametrize("name", ["train_h32_L3", "train_h128_L2", "train_h64_L2"])
+@pytest.mark.parametrize("name", ["train_h32_L3", "train_h128_L2", "train_h64_L2",
+                                  "train_var_h64_L2", "train_var_h32_L3"])   # var: EGCL(norm_diff, tanh)
 def test_training_gradients_match_reference(name):
     inp, ref = load(name)
     model, data = flow_from_fixture(inp, "cuda")
@@ -164,9 +165,9 @@ def test_training_gradients_bitwise_reproducible():
 
 
 def test_training_through_egcl_variants_is_refused():
-    """The HIP backward implements the default EGCL flags only: a differentiable
-    forward through attention / norm_diff / tanh layers raises instead of
-    returning wrong gradients; under no_grad the variants run."""
+    """The HIP backward covers norm_diff / tanh, not attention: a differentiable
+    forward through attention layers (this fixture has them) raises instead
+    of returning wrong gradients; under no_grad the variants run."""
     inp, _ = load("lf_var_h64_L3")
     model, data = flow_from_fixture(inp, "cuda")
     with pytest.raises(NotImplementedError):
