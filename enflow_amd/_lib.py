@@ -113,8 +113,12 @@ _large_ws = {}
 
 
 def is_large(max_mol_atoms):
-    """True if the batch needs the layer-by-layer large-system kernels."""
-    return int(max_mol_atoms) > lib().enflow_max_atoms()
+    """True if the batch goes through the layer-by-layer large-system kernels:
+    its largest molecule exceeds the fused kernels' LDS image, or the
+    ENFLOW_LARGE_MIN_ATOMS threshold (A/B runs)."""
+    thr = os.environ.get("ENFLOW_LARGE_MIN_ATOMS")
+    limit = lib().enflow_max_atoms() + 1 if not thr else int(thr)
+    return int(max_mol_atoms) >= limit
 
 
 def large_workspace(num_mols, num_atoms, max_mol_atoms, nf, device):

@@ -154,6 +154,8 @@ struct BwdArgs {
   float* dp0;        // [P][H] d pre(edge_nn.0)                      (DY of edge_nn.0)
   float* dpe;        // [P][H] d pre(edge_nn.2)                      (DY of edge_nn.2)
   float* aphi;       // [P]    d phi                                 (DY of coord_nn.2)
+  float* patt;       // [P]    att of the pair (VAR; 1 without attention): X of coord_nn.0 is e * att
+  float* dlogit;     // [P]    d att_nn logit (VAR; 0 without attention) (DY of att_nn.0)
   float* su;         // atom rows [A][H] silu(vel_scaling_nn.0)      (X of vel_scaling_nn.2)
   float* au;         // [A][H] d pre(vel_scaling_nn.0)               (DY of vel_scaling_nn.0)
   float* sn;         // [A][H] silu(node_nn.0)                       (X of node_nn.2)
@@ -587,6 +589,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     auto nofill = [](int) {};
     const int vfl = VAR ? (int)B.Lp[L.vfl] : 0;   // wave-uniform constructor variants
     const bool v_nd = VAR && (vfl & EGCL_NORM_DIFF) != 0, v_tanh = VAR && (vfl & EGCL_TANH) != 0;
+    const bool v_att = VAR && (vfl & EGCL_ATTENTION) != 0;
     // the molecule's tile-blocked rows (trow): buffer resources on its first
     // row, per element a wave-uniform byte offset (tile, feature) + the lane's
     const size_t nrow = (size_t)TT * 32;
@@ -703,6 +706,21 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
             ev[t][4 * g4 + u] = silu_f(z);
           }
         }
+      float att = 1.f;
+      if (v_att) {   // egcl.py:60-62: message = e * sigmoid(att_nn(e))
+        float d = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int g4 = 0; g4 < 4; ++g4) {
+            const f32x4 wa = ld4(B.Lp + L.watt + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) d = fmaf(wa[u], ev[t][4 * g4 + u], d);
+          }
+        att = sigm_f(d + __shfl_xor(d, 32, 64) + B.Lp[L.batt]);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) ev[t] *= att;
+      }
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(6);
       // GEMM2 (recompute): phi = coord_nn.2 silu(coord_nn.0 e + bc1)
@@ -742,6 +760,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       float aph = c * (gx * dxn + gy * dyn + gz * dzn);
       if (v_tanh) aph *= 1.f - phi * phi;                       // d of coord_nn.2's output
       if (hh == 0 && !(ENFLOW_BWD_ABLATE & 1)) B.aphi[Rw] = aph;
+      if (VAR && hh == 0) B.patt[Rw] = att;
       // d pre(coord_nn.0) = dphi * wc2 * silu'(c)   (not stored: outer_acc rebuilds it from pc)
 #pragma unroll
       for (int t = 0; t < NT; ++t) cv[t] *= aph;
@@ -765,6 +784,26 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) ae[t][r] = fmaf(ae[t][r], u3, c * sm.agg[i * AST + 32 * t + rho(r, hh)]);
+      if constexpr (VAR) {   // ae = d message; through message = e * att
+        float dl = 0.f;
+        if (v_att) {
+          float s = 0.f;
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s = fmaf(ae[t][r], silu_f(rl[t][r]), s);   // d message . e
+          dl = (s + __shfl_xor(s, 32, 64)) * att * (1.f - att);                      // d logit
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const f32x4 wa = ld4(B.Lp + L.watt + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+              for (int u = 0; u < 4; ++u) ae[t][4 * g4 + u] = fmaf(ae[t][4 * g4 + u], att, wa[u] * dl);
+            }
+        }
+        if (hh == 0) B.dlogit[Rw] = dl;
+      }
       STAMP(8);
       // d pre(edge_nn.2) = d e * silu'(pre_e)
 #pragma unroll
@@ -936,13 +975,14 @@ struct OuterDesc {
                              // 2 tile-blocked on the F16X3 kernel (outer_x3_kernel);
                              // 3 partials written by another descriptor's pass (part2)
   int xf_x;                  // 1: X = silu(stored)
+  const float* xrow;         // tile-blocked: X[row][n] *= xrow[row] after xf_x (or NULL)
   int xf_dy;                 // 1: DY[row][m] = rowv[row] * colv[m] * silu'(stored)
   const float* rowv;
   const float* colv;
   int chunk;                 // rows per workgroup / partial
   float* part2;              // outer_x3_kernel with xf_dy: partials of sum_rows rowv * silu(DY source)
 };
-#define OUTER_MAX 8
+#define OUTER_MAX 10
 struct OuterBatch {
   OuterDesc d[OUTER_MAX];
   int nd;
@@ -1010,11 +1050,12 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   // coord_nn.0's DY = aphi[row] * wc2[m] * silu'(pc): the row factor is applied
   // on load (a thread's 16 elements of a tile-blocked stage share one row), the
   // column factor wc2[m] to the finished sums
-  float ra = 0.f;
+  float ra = 0.f, xa = 1.f;
   auto gload = [&](int st) {
     const int rb = r0 + st * OB_ROWS;
     const size_t rt = (size_t)(rb >> 5);
     if (tiled && D.xf_dy) ra = rb + (tid & 31) < r1 ? D.rowv[rb + (tid & 31)] : 0.f;
+    if (tiled && D.xrow) xa = rb + (tid & 31) < r1 ? D.xrow[rb + (tid & 31)] : 0.f;
     const float* const dblk = D.DY + ((rt * D.ldd) << 5);            // wave-uniform tile blocks
     const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
 #pragma unroll
@@ -1041,6 +1082,10 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
     if (tiled && D.xf_x) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) rx[q] = silu_f(rx[q]);
+    }
+    if (tiled && D.xrow) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rx[q] *= xa;
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -1152,7 +1197,7 @@ __global__ void __launch_bounds__(256, 2) outer_x3_kernel(OuterBatch ob) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
   float rd[16], rx[16];
-  float ra = 0.f;
+  float ra = 0.f, xa = 1.f;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
   // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
   auto gload = [&](int st) {
@@ -1162,6 +1207,7 @@ __global__ void __launch_bounds__(256, 2) outer_x3_kernel(OuterBatch ob) {
     const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
     const bool pv = rb + (tid & 31) < r1;
     if (xf_dy) ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
+    if (D.xrow) xa = pv ? D.xrow[rb + (tid & 31)] : 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int c = 8 * q + (tid >> 5);
@@ -1182,6 +1228,10 @@ __global__ void __launch_bounds__(256, 2) outer_x3_kernel(OuterBatch ob) {
     if (xf_x) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) rx[q] = silu_f(rx[q]);
+    }
+    if (D.xrow) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) rx[q] *= xa;
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -1443,7 +1493,7 @@ static inline size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
 struct BwdWs {
-  size_t offs, xin, p0, pe, pc, dp0, dpe, aphi, su, au, sn, an, aq, agr, anet, part, total;  // floats
+  size_t offs, xin, p0, pe, pc, dp0, dpe, aphi, patt, dlogit, su, au, sn, an, aq, agr, anet, part, total;  // floats
   size_t part_floats;
 };
 
@@ -1459,6 +1509,8 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.dp0 = o; o += al64(P * H);
   W.dpe = o; o += al64(P * H);
   W.aphi = o; o += al64(P);
+  W.patt = o; o += al64(P);
+  W.dlogit = o; o += al64(P);
   W.su = o; o += al64(A * H);
   W.au = o; o += al64(A * H);
   W.sn = o; o += al64(A * H);
@@ -1468,7 +1520,7 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.anet = o; o += al64(A * 2 * nf);
   const size_t chp = (size_t)cdiv(prb, OA_CHUNK), cha = (size_t)cdiv(num_atoms, OA_CHUNK_ATOM);
   // partials of one layer's 8 gradients (all in flight together)
-  W.part_floats = chp * ((size_t)H * (2 * nf + 2) + 2 * (size_t)H * (H + 1) + H) +
+  W.part_floats = chp * ((size_t)H * (2 * nf + 2) + 2 * (size_t)H * (H + 1) + H + (H + 1)) +   // + att_nn
                   cha * ((size_t)H * (nf + 1) + (H + 1) + (size_t)H * (H + nf + 1) + (size_t)nf * (H + 1));
   const size_t am = cha * ((size_t)H * (nf + 1) + (size_t)2 * nf * (H + 1));
   if (am > W.part_floats) W.part_floats = am;
@@ -1483,6 +1535,7 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   OuterDesc& D = ob.d[ob.nd];
   D.tiled = tiled;
   D.xf_x = 0;
+  D.xrow = nullptr;
   D.xf_dy = 0;
   D.rowv = nullptr;
   D.colv = nullptr;
@@ -1658,12 +1711,13 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
     A.Lp = layers + (size_t)l * L.total;
     A.Bp = layers_bwd + (size_t)l * LB.total;
-    A.Rp = layers_raw + (size_t)l * R.total;
+    A.Rp = layers_raw + (size_t)l * R.total_bwd;
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
     A.pair_off = offs + (size_t)l * (num_mols + 1);
     A.xin = ws + Wl.xin; A.p0 = ws + Wl.p0; A.pe = ws + Wl.pe; A.pc = ws + Wl.pc;
     A.dp0 = ws + Wl.dp0; A.dpe = ws + Wl.dpe; A.aphi = ws + Wl.aphi;
+    A.patt = ws + Wl.patt; A.dlogit = ws + Wl.dlogit;
     A.su = ws + Wl.su; A.au = ws + Wl.au; A.sn = ws + Wl.sn; A.an = ws + Wl.an;
     A.aq = ws + Wl.aq; A.agr = ws + Wl.agr; A.err = err_flag;
     if (variants) {
@@ -1676,7 +1730,7 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
 #undef CALL
     }
     // the layer's weight gradients, straight into the torch parameter layout
-    float* G = grad_layers + (size_t)l * R.total;
+    float* G = grad_layers + (size_t)l * R.total_bwd;
     const int32_t* prow = offs + (size_t)l * (num_mols + 1) + num_mols;
     const float* hx = tape + tape_layout(num_atoms, nf, H, n_layers).hx +
                       (size_t)l * num_atoms * (nf + H);
@@ -1691,6 +1745,7 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
     ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
     ob.d[ob.nd - 1].rowv = ws + Wl.aphi;
+    if (variants) ob.d[ob.nd - 1].xrow = ws + Wl.patt;          // the message is e * att
     ob.d[ob.nd - 1].colv = A.Rp + R.wc2;
     // coord_nn.2: d wc2 = sum_rows aphi silu(pc); aphi is one value per row (its "tile-blocked"
     // layout is row-major with width 1)
@@ -1698,6 +1753,10 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
              ENFLOW_OUTER_X3 ? 3 : 1);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
     if (ENFLOW_OUTER_X3) ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;   // folded into coord_nn.0's pass
+    if (variants) {   // att_nn.0: d w = sum_rows dlogit e, d b = sum_rows dlogit (0 rows without attention)
+      add_desc(ob, wg, ws + Wl.dlogit, 1, 1, ws + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
+      ob.d[ob.nd - 1].xf_x = 1;                                 // X = silu(pre_e) = e
+    }
     add_desc(ob, wg, ws + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
     add_desc(ob, wg, ws + Wl.aq, 1, 1, ws + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
     add_desc(ob, wg, ws + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,

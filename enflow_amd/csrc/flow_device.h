@@ -10,7 +10,7 @@
 
 #include "enflow_hip.h"
 
-#define ENFLOW_ABI 4
+#define ENFLOW_ABI 5
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8
@@ -101,6 +101,9 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
 
 struct RawEgcl {  // offsets into the raw (torch) concatenation
   int We1, be1, We2, be2, Wn1, bn1, Wn2, bn2, Wc1, bc1, wc2, Wv1, bv1, Wv2, bv2, total;
+  // training backward (layers_raw / grad_layers): att_nn.0.weight, att_nn.0.bias
+  // appended to every layer (unused without attention); stride total_bwd
+  int watt, batt, total_bwd;
 };
 __host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
   RawEgcl R;
@@ -121,6 +124,9 @@ __host__ __device__ inline RawEgcl raw_egcl(int H, int nf) {
   R.Wv2 = o; o += H;
   R.bv2 = o; o += 1;
   R.total = o;
+  R.watt = o; o += H;
+  R.batt = o; o += 1;
+  R.total_bwd = o;
   return R;
 }
 

@@ -88,12 +88,23 @@ class _FlowFunction(torch.autograd.Function):
         if meta["check_errors"]:
             _lib.raise_on_err(err)
         # split the flat gradients into the parameters' shapes (inputs order)
+        # per layer: the default-flag parameters in raw order, then att_nn.0 (weight,
+        # bias) in the H + 1 slots every layer carries; emitted in named order
         grads = []
-        off = 0
-        for net in flow.networks:
-            for _, p in net.named_parameters():
-                grads.append(grad_layers[off:off + p.numel()].view(p.shape).to(p.dtype))
-                off += p.numel()
+        rstride = grad_layers.numel() // max(len(flow.networks), 1)
+        for li, net in enumerate(flow.networks):
+            off = li * rstride
+            slices = {}
+            for name, p in net.named_parameters():
+                if not name.startswith("att_nn."):
+                    slices[name] = grad_layers[off:off + p.numel()]
+                    off += p.numel()
+            for name, p in net.named_parameters():
+                if name.startswith("att_nn."):
+                    slices[name] = grad_layers[off:off + p.numel()]
+                    off += p.numel()
+            for name, p in net.named_parameters():
+                grads.append(slices[name].view(p.shape).to(p.dtype))
         if kind == _lib.DEQUANT_ARGMAX:
             off = 0
             for p in flow.dequantize.parameters():

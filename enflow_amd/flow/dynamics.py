@@ -95,8 +95,13 @@ class LFIntegrator(BaseFlow):
         hid, nf, _ = self._geometry()
         L = _lib.lib()
         self._check_trainable()
+        # per layer: the default-flag raw parameters, then att_nn.0 (weight, bias) or
+        # H + 1 zeros (enflow_lf_backward_f32's layers_raw stride)
         raw = torch.cat([torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
-                                    for p in n.raw_parameters()]) for n in self.networks])
+                                    for p in n.raw_parameters()] +
+                                   [n._att_raw(device) if n.attention else
+                                    torch.zeros(hid + 1, dtype=torch.float32, device=device)])
+                         for n in self.networks])
         stride = L.enflow_egcl_bwd_packed_size(hid, nf)
         rstride = raw.numel() // max(len(self.networks), 1)
         bwd = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)
@@ -112,11 +117,9 @@ class LFIntegrator(BaseFlow):
         return any(isinstance(n, EGCL) and n.variant_flags() for n in self.networks)
 
     def _check_trainable(self):
-        """The HIP backward covers EGCL(norm_diff, tanh); attention layers run
-        forward / reverse only."""
-        if any(isinstance(n, EGCL) and (n.variant_flags() & _lib.EGCL_ATTENTION) for n in self.networks):
-            raise NotImplementedError("the HIP training backward does not implement EGCL(attention=True); "
-                                      "run attention layers under torch.no_grad() (forward / reverse)")
+        """The HIP backward covers every EGCL constructor variant (attention,
+        norm_diff, tanh); only non-EGCL networks are refused (by _geometry)."""
+        self._geometry()
 
     def _needs_grad(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())

@@ -87,8 +87,8 @@ int enflow_pack_egcl_f32(const float* raw, int hidden_nf, int node_nf,
  * `raw` in the same (default-flag) order as above, `flags` ENFLOW_EGCL_*,
  * `att` = att_nn.0.weight [1][H] followed by att_nn.0.bias [1] (required with
  * ENFLOW_EGCL_ATTENTION, else ignored).  The flow / EGCL forward and reverse
- * kernels read the flags from the packed layer; the training backward
- * supports NORM_DIFF and TANH (see enflow_lf_backward_f32), not ATTENTION. */
+ * kernels read the flags from the packed layer, the training backward too
+ * (see enflow_lf_backward_f32). */
 int enflow_pack_egcl_ex_f32(const float* raw, int hidden_nf, int node_nf, int flags,
                             const float* att, float* packed, void* stream);
 
@@ -279,19 +279,23 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
  *   tape, pair_counts : written by enflow_lf_forward_f32 on the same inputs
  *   layers            : forward-packed layers (enflow_pack_egcl_f32)
  *   layers_bwd        : backward-packed layers (enflow_pack_egcl_bwd_f32)
- *   layers_raw        : raw torch-layout layers (stride = EGCL parameter count)
+ *   layers_raw        : raw torch-layout layers, per layer the default-flag
+ *                       parameters (named_parameters order without att_nn)
+ *                       followed by att_nn.0.weight [H] and att_nn.0.bias [1]
+ *                       (zeros for layers without attention); stride = that
+ *                       count + hidden_nf + 1
  *   dequant_raw       : raw ArgMax parameters; h_data the flow's input h
  *                       (before dequantisation) and noise its N(0,1) draw
  *   adj_h/g/pos/vel   : in: adjoints of the flow outputs; out: of the inputs
  *                       (adj_h: of the dequantised h)
  *   adj_ldj [1]       : adjoint of log|detJ|
- *   grad_layers       : out, [n_layers][EGCL parameter count] (named_parameters
- *                       order, torch layouts), grad_dequant: out, ArgMax layout
+ *   grad_layers       : out, same layout and stride as layers_raw (torch
+ *                       layouts; the att_nn slots of layers without attention
+ *                       are unspecified), grad_dequant: out, ArgMax layout
  *   workspace         : >= enflow_lf_backward_workspace_size bytes
  *   dequant_kind      : ENFLOW_DEQUANT_*, OR-ed with ENFLOW_EGCL_VARIANTS when
- *                       layers carry ENFLOW_EGCL_NORM_DIFF / ENFLOW_EGCL_TANH
- *                       (the forward's layers; ENFLOW_EGCL_ATTENTION layers are
- *                       not supported by the backward)
+ *                       any layer carries ENFLOW_EGCL_* flags (attention,
+ *                       norm_diff, tanh: all differentiated)
  */
 int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
                            const int32_t* mol_ptr, const float* r_cut, const float* box,

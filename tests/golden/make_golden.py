@@ -284,6 +284,9 @@ if __name__ == "__main__":
         case_train(64, 2, [22, 40, 7], 41, "train_var_h64_L2", flags=[(False, True, True), (False, False, True)])
         case_train(32, 3, [22, 9, 15, 3], 42, "train_var_h32_L3",
                    flags=[(False, True, False), (False, True, True), (False, False, False)])
+        case_train(64, 2, [22, 40, 7], 43, "train_att_h64_L2", flags=[(True, False, False), (True, True, True)])
+        case_train(32, 3, [22, 9, 15, 3], 44, "train_att_h32_L3",
+                   flags=[(True, False, False), (False, True, False), (True, False, True)])
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "variants":
         case_egcl_variant(64, 31, (True, False, False), "egcl_h64_att")

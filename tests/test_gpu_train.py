@@ -41,7 +41,8 @@ def _train_step(model, data, eps, kBT, softening):
 
 
 @pytest.mark.parametrize("name", ["train_h32_L3", "train_h128_L2", "train_h64_L2",
-                                  "train_var_h64_L2", "train_var_h32_L3"])   # var: EGCL(norm_diff, tanh)
+                                  "train_var_h64_L2", "train_var_h32_L3",    # var: EGCL(norm_diff, tanh)
+                                  "train_att_h64_L2", "train_att_h32_L3"])   # att: + attention
 def test_training_gradients_match_reference(name):
     inp, ref = load(name)
     model, data = flow_from_fixture(inp, "cuda")
@@ -164,13 +165,24 @@ def test_training_gradients_bitwise_reproducible():
         assert torch.equal(g0, g1)
 
 
-def test_training_through_egcl_variants_is_refused():
-    """The HIP backward covers norm_diff / tanh, not attention: a differentiable
-    forward through attention layers (this fixture has them) raises instead
-    of returning wrong gradients; under no_grad the variants run."""
+def test_training_through_all_egcl_variants_vs_oracle():
+    """Every constructor variant trains (lf_var_h64_L3: attention, norm_diff +
+    tanh, all three): HIP gradients vs the gradient oracle (pinned to the
+    reference's loss.backward() on train_att_* / train_var_*)."""
+    from oracle import enflow_oracle_grad as OG
+    from enflow_amd.data.synthetic import default_kBT
     inp, _ = load("lf_var_h64_L3")
     model, data = flow_from_fixture(inp, "cuda")
-    with pytest.raises(NotImplementedError):
-        model(data, noise=torch.tensor(inp["eps"], device="cuda"))
-    with torch.no_grad():
-        model(data, noise=torch.tensor(inp["eps"], device="cuda"))
+    kBT = default_kBT()
+    loss, _ = _train_step(model, data, torch.tensor(inp["eps"], device="cuda"), kBT, 0.1)
+    nl = n_layers(inp)
+    rloss, _, gl, gd, _ = OG.train_loss_and_grads([layer_params(inp, i) for i in range(nl)], dequant_params(inp),
+                                                  state(inp), inp["eps"].astype(np.float64), float(inp["dt"]),
+                                                  kBT, 0.1)
+    assert abs(float(loss) - rloss) <= LOSS_TOL * abs(rloss)
+    worst = {}
+    for i, net in enumerate(model.networks):
+        for k, p in net.named_parameters():
+            worst[f"p{i}.{k}"] = normwise(p.grad.cpu().numpy(), gl[i][k])
+    print("variants max normwise grad err", max(worst.values()))
+    assert max(worst.values()) <= GRAD_TOL, {k: v for k, v in worst.items() if v > GRAD_TOL}

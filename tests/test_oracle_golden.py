@@ -80,7 +80,8 @@ def test_multiplicity_roundtrip():
     assert np.all(pc >= 1)
 
 
-TRAIN_CASES = ["train_h32_L3", "train_h128_L2", "train_h64_L2", "train_var_h64_L2", "train_var_h32_L3"]
+TRAIN_CASES = ["train_h32_L3", "train_h128_L2", "train_h64_L2", "train_var_h64_L2", "train_var_h32_L3",
+               "train_att_h64_L2", "train_att_h32_L3"]
 
 
 @pytest.mark.parametrize("name", TRAIN_CASES)
