@@ -296,6 +296,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   M.bz = B.box[(size_t)M.a0 * 3 + 2];
   const int r0 = (b - B.blk_start[m]) * B.rbl, rb = min(B.rbl, M.n - r0);
   const int g0 = M.a0 + r0;   // first row atom (global)
+  STAMP_DECL   // diagnostic builds only (-DENFLOW_STAMPS)
   const int nf = B.nf;
   const EgclLayout L = egcl_layout(H, nf);
   for (int e = tid; e < rb * 3; e += BLOCK) sm.pos[e] = B.pos[(size_t)g0 * 3 + e];
@@ -327,7 +328,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
     }
     if (tid == 0) sm.npairs = max(cnt, 0);
     __syncthreads();
-    edge_tiles<H, 32, 32, PREC, VAR, true>(sm, B.layer, L, M, nf, tid, 0, rb, p0 == 0, cpos, ch);
+    edge_tiles<H, 32, 32, PREC, VAR, true>(sm, B.layer, L, M, nf, tid, 0, rb, p0 == 0 STAMP_PASS, cpos, ch);
     p0 += PC;
     if (p0 >= tot) break;
   }
