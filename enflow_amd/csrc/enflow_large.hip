@@ -60,6 +60,7 @@ struct LgArgs {
   uint32_t* pairs;      // [A][max_n]
   int max_n;
   int32_t* blk_start;   // [M + 1] first row block of molecule m
+  float* aabb;          // [M][6] bounding box of the molecule's positions (this layer)
   int rbl;              // rows per block (4 .. 32; the host picks it to fill the CUs)
   float* ldj_blk;       // [blocks] log|detJ| per row block
   float* Qo;            // EGCL mode outputs (else null)
@@ -155,18 +156,55 @@ __global__ void __launch_bounds__(IDB) lg_idmap_kernel(LgArgs B) {
   const int c0 = min(n, tid * per), c1 = min(n, c0 + per);
   const uint32_t* mk = n <= MK_LDS ? mk_l : B.mask + a0;
   int32_t* idm = B.idmap + a0;
+  __shared__ float red[6][IDW];
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
   for (int a = tid; a < n; a += IDB) {
     idm[a] = -1;
     if (n <= MK_LDS) mk_l[a] = B.mask[a0 + a];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      const float x = B.pos[(size_t)(a0 + a) * 3 + d];
+      lo[d] = fminf(lo[d], x);
+      hi[d] = fmaxf(hi[d], x);
+    }
+  }
+  // the molecule's bounding box (min / max: order-independent), for the pair
+  // search's image culling
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      lo[d] = fminf(lo[d], __shfl_xor(lo[d], o, 64));
+      hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], o, 64));
+    }
+    if (lane == 0) { red[d][w] = lo[d]; red[3 + d][w] = hi[d]; }
   }
   __syncthreads();
+  if (tid < 6) {
+    float v = red[tid][0];
+    for (int k = 1; k < IDW; ++k) v = tid < 3 ? fminf(v, red[tid][k]) : fmaxf(v, red[tid][k]);
+    B.aabb[(size_t)m * 6 + tid] = v;
+  }
+  // the thread's chunk of masks in registers (molecules up to IDB * MR atoms)
+  constexpr int MR = 16;
+  const bool regs = per <= MR;
+  uint32_t mr[MR];
+#pragma unroll
+  for (int k = 0; k < MR; ++k) mr[k] = (regs && c0 + k < c1) ? mk[c0 + k] : 0u;
   int cnt[27];
 #pragma unroll
   for (int s = 0; s < 27; ++s) cnt[s] = 0;
-  for (int a = c0; a < c1; ++a) {
-    const uint32_t v = mk[a];
+  if (regs) {
 #pragma unroll
-    for (int s = 0; s < 27; ++s) cnt[s] += (v >> s) & 1u;
+    for (int k = 0; k < MR; ++k)
+#pragma unroll
+      for (int s = 0; s < 27; ++s) cnt[s] += (mr[k] >> s) & 1u;
+  } else {
+    for (int a = c0; a < c1; ++a) {
+      const uint32_t v = mk[a];
+#pragma unroll
+      for (int s = 0; s < 27; ++s) cnt[s] += (v >> s) & 1u;
+    }
   }
   int base[27];
 #pragma unroll
@@ -191,9 +229,16 @@ __global__ void __launch_bounds__(IDB) lg_idmap_kernel(LgArgs B) {
 #pragma unroll
   for (int s = 0; s < 27; ++s) {   // unrolled: cnt / base stay in registers
     int o = base[s];
-    if (o < n)
-      for (int a = c0; a < c1 && o < n; ++a)
-        if ((mk[a] >> s) & 1u) idm[o++] = a;
+    if (o < n) {
+      if (regs) {
+#pragma unroll
+        for (int k = 0; k < MR; ++k)
+          if (((mr[k] >> s) & 1u) && o < n) idm[o++] = c0 + k;   // mr[k] = 0 past the chunk
+      } else {
+        for (int a = c0; a < c1 && o < n; ++a)
+          if ((mk[a] >> s) & 1u) idm[o++] = a;
+      }
+    }
   }
 }
 
@@ -214,6 +259,9 @@ __global__ void __launch_bounds__(BLOCK) lg_pairs_kernel(LgArgs B) {
   const float bx = B.box[(size_t)a0 * 3 + 0], by = B.box[(size_t)a0 * 3 + 1], bz = B.box[(size_t)a0 * 3 + 2];
   const float rc = B.r_cut[m], r_sq = rc * rc;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  float bb[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) bb[k] = B.aabb[(size_t)m * 6 + k];
   constexpr int RPW = 8;   // rows per wave (rbl <= 32)
   int np[RPW], edges[RPW];
 #pragma unroll
@@ -230,15 +278,28 @@ __global__ void __launch_bounds__(BLOCK) lg_pairs_kernel(LgArgs B) {
       if (il >= rb) break;   // wave-uniform
       const int a = a0 + r0 + il;
       const uint32_t mk = B.mask[a];
-      const int ni = __popc(mk);
-      if (lane < 27) {   // image list of the row, in image order (wave-private LDS)
+      // image list of the row (wave-private LDS): the surviving images that
+      // can reach the molecule's bounding box at all (farther than r_cut from
+      // it, with a 1e-4 relative margin over fp32 rounding, no atom can hit)
+      uint32_t cand = 0u;
+      float ix = 0.f, iy = 0.f, iz = 0.f;
+      if (lane < 27 && ((mk >> lane) & 1u)) {
         const int s = lane;
-        if ((mk >> s) & 1u) {
-          const int slot = __popc(mk & ((1u << s) - 1u));
-          img[w][slot * 3 + 0] = B.pos[(size_t)a * 3 + 0] + shift_of(s % 3, bx);
-          img[w][slot * 3 + 1] = B.pos[(size_t)a * 3 + 1] + shift_of((s / 3) % 3, by);
-          img[w][slot * 3 + 2] = B.pos[(size_t)a * 3 + 2] + shift_of(s / 9, bz);
-        }
+        ix = B.pos[(size_t)a * 3 + 0] + shift_of(s % 3, bx);
+        iy = B.pos[(size_t)a * 3 + 1] + shift_of((s / 3) % 3, by);
+        iz = B.pos[(size_t)a * 3 + 2] + shift_of(s / 9, bz);
+        const float ex = fmaxf(fmaxf(bb[0] - ix, ix - bb[3]), 0.f);
+        const float ey = fmaxf(fmaxf(bb[1] - iy, iy - bb[4]), 0.f);
+        const float ez = fmaxf(fmaxf(bb[2] - iz, iz - bb[5]), 0.f);
+        cand = (ex * ex + ey * ey + ez * ez) <= r_sq * 1.0001f ? 1u : 0u;
+      }
+      const uint64_t cb = __ballot(cand != 0u);
+      const int ni = __popcll(cb);
+      if (cand) {
+        const int slot = __popcll(cb & lt);
+        img[w][slot * 3 + 0] = ix;
+        img[w][slot * 3 + 1] = iy;
+        img[w][slot * 3 + 2] = iz;
       }
       wave_lds_sync();
       uint32_t* out = B.pairs + (size_t)a * B.max_n;
@@ -451,7 +512,7 @@ __global__ void __launch_bounds__(BLOCK) lg_ldj_kernel(LgArgs B, float* ldj_mol,
 static inline hipStream_t LS(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static const double kLog2PiL = 1.8378770664093453;
 
-struct LgWorkspace { size_t mask, idmap, npairs, cntrow, blk_start, ldj_blk, pos2, h2, pairs, total; };
+struct LgWorkspace { size_t mask, idmap, npairs, cntrow, blk_start, aabb, ldj_blk, pos2, h2, pairs, total; };
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 static LgWorkspace lg_workspace(int num_mols, int num_atoms, int max_n, int nf) {
   LgWorkspace W;
@@ -462,6 +523,7 @@ static LgWorkspace lg_workspace(int num_mols, int num_atoms, int max_n, int nf) 
   W.npairs = o; o = al256(o + A * 4);
   W.cntrow = o; o = al256(o + A * 4);
   W.blk_start = o; o = al256(o + ((size_t)num_mols + 1) * 4);
+  W.aabb = o; o = al256(o + (size_t)num_mols * 6 * 4);
   W.ldj_blk = o; o = al256(o + NB * 4);
   W.pos2 = o; o = al256(o + A * 3 * 4);
   W.h2 = o; o = al256(o + A * nf * 4);
@@ -541,6 +603,7 @@ static LgArgs lg_args(int num_mols, int num_atoms, int max_n, int nf, const int3
   B.pairs = reinterpret_cast<uint32_t*>(base + W.pairs);
   B.max_n = max_n;
   B.blk_start = reinterpret_cast<int32_t*>(base + W.blk_start);
+  B.aabb = reinterpret_cast<float*>(base + W.aabb);
   B.rbl = lg_rows(num_atoms);
   B.ldj_blk = reinterpret_cast<float*>(base + W.ldj_blk);
   B.err = err;
