@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(F
       }
       STAMP(4);
       if (!(ENFLOW_ABLATE & 2)) {
-        if constexpr (PREC == PREC_F16X3) node_phase_x3(sm, Lp, L, n, nf, tid_l, r0, rb);
+        if constexpr (PREC != PREC_F32) node_phase_x3(sm, Lp, L, n, nf, tid_l, r0, rb);   // fp32-accurate
         else node_phase(sm, Lp, L, n, nf, tid_l, r0, rb);
       }
       STAMP(5);

@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
     p0 += PC;
     if (p0 >= tot) break;
   }
-  if constexpr (PREC == PREC_F16X3) node_phase_x3(sm, B.layer, L, rb, nf, tid, 0, rb);
+  if constexpr (PREC != PREC_F32) node_phase_x3(sm, B.layer, L, rb, nf, tid, 0, rb);
   else node_phase(sm, B.layer, L, rb, nf, tid, 0, rb);
 
   float ldj = 0.f;

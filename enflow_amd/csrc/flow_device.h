@@ -961,7 +961,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     sm.bias[2 * H + k] = Lp[L.bc1 + k];
     sm.bias[3 * H + k] = Lp[L.wc2 + k];
   }
-  if constexpr (PREC == PREC_F16X3 && Smem<H, NMAX, RB>::W1X_LDS) {
+  if constexpr (PREC != PREC_F32 && Smem<H, NMAX, RB>::W1X_LDS) {   // GEMM0 is F16X3 in bf16 mode too
     // edge_nn.0 split fragments: one L2 pass per layer instead of one per tile
     const int ks_n = (2 * nf + 1 + 15) >> 4;
     for (int e = tid; e < NT * ks_n * 128; e += BLOCK) {   // 128 x 16 B per (t, ks)
@@ -1035,7 +1035,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     f32x16 x0[NT];
 #pragma unroll
     for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
-    if constexpr (PREC == PREC_F16X3) {
+    if constexpr (PREC != PREC_F32) {   // F16X3 (bf16 mode too: a 16-wide k-step on the matrix cores
+      // beats 9 f32 k-steps; only edge_nn.2 / coord_nn.0 run in bf16)
       // k = raw column of edge_nn.0: [h_i (nf), h_j (nf), radial], 16 per k-step
       const int ks_n = (2 * nf + 1 + 15) >> 4;
       for (int ks = 0; ks < ks_n; ++ks) {
