@@ -197,8 +197,12 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
 // ---------------------------------------------------------------------------
 // the fused flow kernel (forward or reverse)
 // ---------------------------------------------------------------------------
+#ifndef ENFLOW_BLOCKED_WPS
+#define ENFLOW_BLOCKED_WPS ENFLOW_WAVES_PER_SIMD   // row-blocked (> 64-atom) instances
+#endif
 template <int H, int NMAX, bool REV, int PREC, int RB, bool VAR>
-__global__ void __launch_bounds__(BLOCK, ENFLOW_WAVES_PER_SIMD) lf_flow_kernel(FlowArgs A) {
+__global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLOW_WAVES_PER_SIMD))
+    lf_flow_kernel(FlowArgs A) {
   __shared__ Smem<H, NMAX, RB> sm;
   constexpr bool BLOCKED = RB < NMAX;
   MolRef M;
