@@ -988,8 +988,13 @@ struct OuterBatch {
   int nd;
   int start[OUTER_MAX + 1];   // first workgroup of each descriptor
 };
+#ifndef OA_CHUNK
 #define OA_CHUNK 2048        // pair rows per partial
+#endif
+#ifndef OA_CHUNK_ATOM
 #define OA_CHUNK_ATOM 512    // atom rows per partial (a few hundred workgroups for 64k atoms)
+#endif
+static_assert(OA_CHUNK % 64 == 0 && OA_CHUNK_ATOM % 64 == 0, "partial chunks are whole row stages");
 
 __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
   int k = 0;
