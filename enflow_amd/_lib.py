@@ -135,9 +135,38 @@ def large_workspace(num_mols, num_atoms, max_mol_atoms, nf, device):
     return ws
 
 
+_pending = []
+
+
+def defer_err(err_flag):
+    """Queue a device error word for a later check instead of synchronising now:
+    a non-blocking copy into pinned host memory plus an event.  The training
+    backward uses this so the host-side tail of the step (gradient views, the
+    optimiser's launches) overlaps the backward kernels; the word is read by the
+    next raise_on_err / check_pending (normally the next step's forward check),
+    by which time the event has long completed."""
+    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(err_flag, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(err_flag.device))
+    _pending.append((ev, host))
+
+
+def check_pending():
+    """Raise for any deferred error word (waits only for the queued events)."""
+    while _pending:
+        ev, host = _pending.pop(0)
+        ev.synchronize()
+        _raise_code(int(host.item()))
+
+
 def raise_on_err(err_flag):
     """Read the device error word (synchronises) and raise like the reference."""
-    e = int(err_flag.item())
+    check_pending()
+    _raise_code(int(err_flag.item()))
+
+
+def _raise_code(e):
     if e & ERR_FEW_IMAGES:
         raise IndexError("fewer periodic images than atoms in a molecule: the reference "
                          "indexes id_mapping out of range here (enflow/data/base.py:137)")

@@ -86,7 +86,9 @@ class _FlowFunction(torch.autograd.Function):
             _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
             _lib.stream_ptr(dev)), "enflow_lf_backward_f32")
         if meta["check_errors"]:
-            _lib.raise_on_err(err)
+            # the forward already validated this batch's geometry; the backward's
+            # word is read at the next check instead of stalling the host here
+            _lib.defer_err(err)
         # split the flat gradients into the parameters' shapes (inputs order)
         # per layer: the default-flag parameters in raw order, then att_nn.0 (weight,
         # bias) in the H + 1 slots every layer carries; emitted in named order

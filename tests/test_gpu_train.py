@@ -186,3 +186,23 @@ def test_training_through_all_egcl_variants_vs_oracle():
             worst[f"p{i}.{k}"] = normwise(p.grad.cpu().numpy(), gl[i][k])
     print("variants max normwise grad err", max(worst.values()))
     assert max(worst.values()) <= GRAD_TOL, {k: v for k, v in worst.items() if v > GRAD_TOL}
+
+
+def test_backward_error_word_is_deferred_then_checked():
+    """The backward queues its device error word (pinned copy + event) instead
+    of synchronising; the next forward check, or _lib.check_pending(), reads
+    it.  A clean step leaves nothing pending afterwards and raises nothing; a
+    forced error code queued the same way raises at the next check."""
+    from enflow_amd import _lib
+    inp, _ = load("train_h32_L3")
+    model, data = flow_from_fixture(inp, "cuda")
+    eps = torch.tensor(inp["eps"], device="cuda")
+    _lib.check_pending()
+    _train_step(model, data, eps, float(inp["kBT"]), float(inp["softening"]))
+    assert len(_lib._pending) == 1
+    _lib.check_pending()
+    assert not _lib._pending
+    _lib.defer_err(torch.full((1,), _lib.ERR_FEW_IMAGES, dtype=torch.int32, device="cuda"))
+    with pytest.raises(IndexError):
+        _lib.check_pending()
+    assert not _lib._pending
