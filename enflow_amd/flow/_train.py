@@ -39,6 +39,14 @@ class _FlowFunction(torch.autograd.Function):
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"], meta["max_n"],
                              meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts)
+        # queue the backward's weight packing (cached on the parameters' versions,
+        # which cannot change before this graph's backward) and the dequantiser's
+        # flat parameters behind the forward kernel, ahead of the error check's sync
+        flow.training_layers(dev)
+        ctx.dq_raw = None
+        if kind == _lib.DEQUANT_ARGMAX:
+            ctx.dq_raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
+                                    for p in flow.dequantize.parameters()])
         if meta["check_errors"]:
             _lib.raise_on_err(err)
         ctx.flow, ctx.meta, ctx.kind = flow, meta, kind
@@ -69,8 +77,7 @@ class _FlowFunction(torch.autograd.Function):
         grad_layers = torch.empty_like(raw)
         dq_raw, grad_dq = None, None
         if kind == _lib.DEQUANT_ARGMAX:
-            dq_raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
-                                for p in flow.dequantize.parameters()])
+            dq_raw = ctx.dq_raw
             grad_dq = torch.empty_like(dq_raw)
         prb = meta["pair_row_bound"]
         wsb = L.enflow_lf_backward_workspace_size(M, A, nf, hid, n_layers, prb)
