@@ -1171,7 +1171,10 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 // hi / lo split; the stage's three-product sums land in a scratch accumulator
 // that is added to the running one with the exact inverse scale.
 #define OX_LD 36   // LDS column stride (floats): 16-byte aligned operand reads
-__global__ void __launch_bounds__(256, 2) outer_x3_kernel(OuterBatch ob) {
+#ifndef ENFLOW_OUTER_WPS
+#define ENFLOW_OUTER_WPS 2   // outer_x3_kernel occupancy hint (A/B knob)
+#endif
+__global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
   const OuterDesc& D = ob.d[k];
