@@ -97,11 +97,17 @@ class LFIntegrator(BaseFlow):
         self._check_trainable()
         # per layer: the default-flag raw parameters, then att_nn.0 (weight, bias) or
         # H + 1 zeros (enflow_lf_backward_f32's layers_raw stride)
-        raw = torch.cat([torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
-                                    for p in n.raw_parameters()] +
-                                   [n._att_raw(device) if n.attention else
-                                    torch.zeros(hid + 1, dtype=torch.float32, device=device)])
-                         for n in self.networks])
+        # (one flat cat launch; the zero pad is allocated once per device)
+        zkey = (str(device), hid)
+        if getattr(self, "_zpad_key", None) != zkey:
+            self._zpad = torch.zeros(hid + 1, dtype=torch.float32, device=device)
+            self._zpad_key = zkey
+        zpad = self._zpad
+        pieces = []
+        for n in self.networks:
+            pieces += [p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in n.raw_parameters()]
+            pieces.append(n._att_raw(device) if n.attention else zpad)
+        raw = torch.cat(pieces)
         stride = L.enflow_egcl_bwd_packed_size(hid, nf)
         rstride = raw.numel() // max(len(self.networks), 1)
         bwd = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)
