@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("ENFLOW_LIB") or os.path.join(os.path.dirname(os.path.
 ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2
 ERR_TOO_MANY_FEATURES = 4
+ERR_RANGE = 8
 DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
 PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
@@ -61,6 +62,11 @@ SIGNATURES = {
     "enflow_lf_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                     _i, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p,
                                     _p, _i64, _i64, _p, _p]),
+    "enflow_timing_enable": (_i, [_i]),
+    "enflow_timing_collect": (_i, []),
+    "enflow_timing_entry": (_i, [_i, ctypes.c_char_p, _i, ctypes.POINTER(ctypes.c_double),
+                                 ctypes.POINTER(ctypes.c_int64)]),
+    "enflow_timing_reset": (_i, []),
 }
 
 _lib = None
@@ -107,7 +113,8 @@ def require_gpu(t):
                            "(there is no CPU fallback)")
 
 
-LARGE_TRAIN_MSG = ("the HIP training backward handles molecules of <= 64 atoms; larger systems "
+TRAIN_MAX_ATOMS = 64      # the HIP backward keeps whole-molecule pair lists in LDS
+LARGE_TRAIN_MSG = (f"the HIP training backward handles molecules of <= {TRAIN_MAX_ATOMS} atoms; larger systems "
                    "run forward / reverse / EGCL only")
 _large_ws = {}
 
@@ -133,6 +140,40 @@ def large_workspace(num_mols, num_atoms, max_mol_atoms, nf, device):
         ws = torch.empty(max(need, 1), dtype=torch.uint8, device=device)
         _large_ws[key] = ws
     return ws
+
+
+class KernelTimer:
+    """Per-kernel HIP-event timing of this library's launches (enflow_timing_*):
+
+        with KernelTimer() as t:
+            ...launches...
+        t.ms_per_launch("lf_flow_kernel<fwd>")
+
+    Each launch is bracketed by an event pair on its own stream; exit waits for
+    the events and snapshots {name: (total_ms, launches)}."""
+
+    def __enter__(self):
+        L = lib()
+        L.enflow_timing_reset()
+        L.enflow_timing_enable(1)
+        self.stats = {}
+        return self
+
+    def __exit__(self, *exc):
+        L = lib()
+        L.enflow_timing_enable(0)
+        n = L.enflow_timing_collect()
+        buf = ctypes.create_string_buffer(128)
+        ms, cnt = ctypes.c_double(), ctypes.c_int64()
+        for i in range(n):
+            if L.enflow_timing_entry(i, buf, 128, ctypes.byref(ms), ctypes.byref(cnt)) == 0 and cnt.value:
+                self.stats[buf.value.decode()] = (ms.value, int(cnt.value))
+        L.enflow_timing_reset()
+        return False
+
+    def ms_per_launch(self, name):
+        tot, cnt = self.stats.get(name, (0.0, 0))
+        return tot / cnt if cnt else None
 
 
 _pending = []
@@ -174,3 +215,6 @@ def _raise_code(e):
         raise HipPathError(f"molecule larger than {lib().enflow_max_atoms()} atoms")
     if e & ERR_TOO_MANY_FEATURES:
         raise HipPathError(f"node_nf larger than {lib().enflow_max_node_nf()}")
+    if e & ERR_RANGE:
+        raise FloatingPointError("the split-precision (f16x3 / bf16) GEMMs produced a non-finite result: an "
+                                 "operand is past the fp16 / bf16 range; run with gemm_precision='f32'")

@@ -935,6 +935,19 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 // ---------------------------------------------------------------------------
 // per-layer 32-aligned pair row offsets (exclusive scan, one block per layer)
 // ---------------------------------------------------------------------------
+// A backward whose error word is set leaves NaN in every gradient it produced,
+// so an optimizer step that runs before the host reads the (deferred) word
+// cannot apply wrong-but-finite updates silently.
+__global__ void __launch_bounds__(256) poison_on_err_kernel(const int32_t* __restrict__ err, float* __restrict__ a,
+                                                            long long na, float* __restrict__ b, long long nb) {
+  if (__builtin_nontemporal_load(err) == 0) return;
+  const float nan = __builtin_nanf("");
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < na; i += stride) a[i] = nan;
+  if (b)
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride) b[i] = nan;
+}
+
 __global__ void __launch_bounds__(BLOCK) pair_offsets_kernel(const int32_t* counts, int num_mols, int32_t* offs) {
   __shared__ int wsum[WAVES];
   __shared__ int carry;
@@ -1579,8 +1592,8 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
       sub.start[++sub.nd] = swg;
     }
     if (swg > 0) {
-      if (tl) hipLaunchKernelGGL(outer_acc_kernel<true>, dim3(swg), dim3(256), 0, st, sub);
-      else hipLaunchKernelGGL(outer_acc_kernel<false>, dim3(swg), dim3(256), 0, st, sub);
+      if (tl) ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL(outer_acc_kernel<true>, dim3(swg), dim3(256), 0, st, sub));
+      else ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL(outer_acc_kernel<false>, dim3(swg), dim3(256), 0, st, sub));
     }
   }
   // F16X3 MFMA: tile-blocked descriptors with M > 1
@@ -1595,7 +1608,7 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
       swg += ob.start[k + 1] - ob.start[k];
       sub.start[++sub.nd] = swg;
     }
-    if (swg > 0) hipLaunchKernelGGL(outer_x3_kernel, dim3(swg), dim3(256), 0, st, sub);
+    if (swg > 0) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel, dim3(swg), dim3(256), 0, st, sub));
   }
   (void)wg;
   // reducer: one workgroup per 256 outputs of each descriptor
@@ -1607,7 +1620,7 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
     rw += cdiv((long long)ob.d[k].M * NB, 256);
   }
   rb.start[ob.nd] = rw;
-  if (rw > 0) hipLaunchKernelGGL(reduce_part_kernel, dim3(rw), dim3(256), 0, st, rb);
+  if (rw > 0) ENFLOW_TIMED("reduce_part_kernel", st, hipLaunchKernelGGL(reduce_part_kernel, dim3(rw), dim3(256), 0, st, rb));
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1670,12 +1683,14 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
                                        float* adj_vel, float* adj_ldj, void* stream) {
   (void)num_atoms;
   if (num_mols < 1 || max_mol_atoms > 64 || nf < 1 || !adj_ldj) return -1;
+  const int tm = enflow_tm_begin("nll_bwd_kernel", SB(stream));
   if (max_mol_atoms <= 32)
     hipLaunchKernelGGL((nll_bwd_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, SB(stream), mol_ptr, num_mols, nf, h, g,
                        pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos, adj_vel, adj_ldj);
   else
     hipLaunchKernelGGL((nll_bwd_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, SB(stream), mol_ptr, num_mols, nf, h, g,
                        pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos, adj_vel, adj_ldj);
+  enflow_tm_end(tm, SB(stream));
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -1729,11 +1744,11 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     A.su = ws + Wl.su; A.au = ws + Wl.au; A.sn = ws + Wl.sn; A.an = ws + Wl.an;
     A.aq = ws + Wl.aq; A.agr = ws + Wl.agr; A.err = err_flag;
     if (variants) {
-#define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, st, A)
+#define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);
 #undef CALL
     } else {
-#define CALL(HH, NN) hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, st, A)
+#define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, false>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);
 #undef CALL
     }
@@ -1796,6 +1811,9 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     const int rc = run_outer(ob, wg, st);
     if (rc) return rc;
   }
+  hipLaunchKernelGGL(poison_on_err_kernel, dim3(64), dim3(256), 0, st, err_flag, grad_layers,
+                     (long long)n_layers * R.total_bwd, dequant_kind == ENFLOW_DEQUANT_ARGMAX ? grad_dequant : nullptr,
+                     (long long)(H * nf + H + 2 * nf * H + 2 * nf));   // ArgMax.network: W1, b1, W2, b2
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

@@ -367,19 +367,31 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
     }
     __syncthreads();   // the write-back below maps threads to elements differently
   }
-  // write back
+  // write back.  Split-precision GEMMs (f16x3 / bf16) cannot represent operands
+  // past the fp16 / bf16 range: a non-finite output they produce is flagged
+  // (ENFLOW_ERR_RANGE) instead of returned silently; the f32 path returns
+  // whatever the arithmetic gives, as the reference does.
+  bool bad = false;
   for (int e = tid; e < n * 3; e += BLOCK) {
-    A.pos[(size_t)M.a0 * 3 + e] = sm.pos[e];
-    A.vel[(size_t)M.a0 * 3 + e] = sm.vel[e];
+    const float p = sm.pos[e], v = sm.vel[e];
+    A.pos[(size_t)M.a0 * 3 + e] = p;
+    A.vel[(size_t)M.a0 * 3 + e] = v;
+    bad |= !__builtin_isfinite(p) || !__builtin_isfinite(v);
   }
   for (int e = tid; e < n * nf; e += BLOCK) {
     const int a = e / nf, q = e - a * nf;
-    A.h[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
-    A.g[(size_t)M.a0 * nf + e] = sm.g[a * NFP + q];
+    const float hv = sm.h[a * NFP + q], gv = sm.g[a * NFP + q];
+    A.h[(size_t)M.a0 * nf + e] = hv;
+    A.g[(size_t)M.a0 * nf + e] = gv;
+    bad |= (!REV && !__builtin_isfinite(hv)) || !__builtin_isfinite(gv);
   }
   if (!REV) {
     const float s = block_sum(sm, ldj);
     if (tid == 0) A.ldj_mol[blockIdx.x] = s;
+    bad |= tid == 0 && !__builtin_isfinite(s);
+  }
+  if constexpr (PREC != PREC_F32) {
+    if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
   }
   if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
   STAMP(7);
@@ -588,11 +600,14 @@ static const double kLog2Pi = 1.8378770664093453;
 template <int HH, int NN, int RBB, bool REV, bool VAR>
 static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
   if (prec == ENFLOW_PREC_F16X3)
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    ENFLOW_TIMED(REV ? "lf_flow_kernel<rev>" : "lf_flow_kernel<fwd>", st,
+                 hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A));
   else if (prec == ENFLOW_PREC_BF16)
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    ENFLOW_TIMED(REV ? "lf_flow_kernel<rev>" : "lf_flow_kernel<fwd>", st,
+                 hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_BF16, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A));
   else
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    ENFLOW_TIMED(REV ? "lf_flow_kernel<rev>" : "lf_flow_kernel<fwd>", st,
+                 hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F32, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A));
 }
 // gemm_precision may carry ENFLOW_EGCL_VARIANTS: layers packed with
 // enflow_pack_egcl_ex_f32 flags run on the variant-capable kernels
@@ -677,6 +692,8 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
   // training tape: the backward handles molecules of <= 64 atoms (unblocked pair lists)
   if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr || max_mol_atoms > 64)) return -1;
+  // the tape feeds the fp32-accurate backward: it must come from an fp32-accurate forward
+  if (tape != nullptr && (gemm_precision & 0xff) == ENFLOW_PREC_BF16) return -1;
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
              dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
              reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
@@ -686,7 +703,8 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
 #undef CALL
   }
   const double cst = dequant_kind == ENFLOW_DEQUANT_ARGMAX ? -0.5 * kLog2Pi : 0.0;
-  hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total);
+  ENFLOW_TIMED("reduce_ldj_kernel", S(stream),
+               hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total));
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -781,6 +799,7 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
                               float kBT, float softening, float partition_func,
                               float* nll_mol, float* loss, void* stream) {
   if (num_mols < 0 || max_mol_atoms < 0 || nf < 1) return -1;
+  const int tm = enflow_tm_begin("nll_mol_kernel", S(stream));
   if (num_mols > 0) {
     if (max_mol_atoms <= 32)
       hipLaunchKernelGGL((nll_mol_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
@@ -793,6 +812,7 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
   }
   hipLaunchKernelGGL(reduce_nll_kernel, dim3(1), dim3(BLOCK), 0, S(stream), nll_mol, num_mols, num_atoms, ldj_total,
                      kBT, partition_func, loss);
+  enflow_tm_end(tm, S(stream));
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

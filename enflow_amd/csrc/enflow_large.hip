@@ -404,6 +404,12 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
     float F[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) F[d] = sm.agg[a * AST + H + d] * inv * B.cw;
+    if constexpr (PREC != PREC_F32) {   // split-precision GEMM out of range (ENFLOW_ERR_RANGE)
+      bool bad = !__builtin_isfinite(q) || !__builtin_isfinite(F[0]) || !__builtin_isfinite(F[1]) ||
+                 !__builtin_isfinite(F[2]);
+      for (int qf = 0; qf < nf; ++qf) bad |= !__builtin_isfinite(sm.G[a * NFP + qf]);
+      if (bad) atomicOr(B.err, ENFLOW_ERR_RANGE);
+    }
     if (mode == 2) {   // EGCL.forward outputs
       B.Qo[ga] = q;
       for (int d = 0; d < 3; ++d) B.Fo[ga * 3 + d] = F[d];
@@ -544,8 +550,8 @@ static int lg_check(int num_mols, int num_atoms, int max_n, int nf, int H, int p
 
 template <int HH, int PREC>
 static void lg_layer_launch(bool var, int grid, hipStream_t st, const LgArgs& B, int mode) {
-  if (var) hipLaunchKernelGGL((lg_layer_kernel<HH, PREC, true>), dim3(grid), dim3(BLOCK), 0, st, B, mode);
-  else hipLaunchKernelGGL((lg_layer_kernel<HH, PREC, false>), dim3(grid), dim3(BLOCK), 0, st, B, mode);
+  if (var) ENFLOW_TIMED("lg_layer_kernel", st, hipLaunchKernelGGL((lg_layer_kernel<HH, PREC, true>), dim3(grid), dim3(BLOCK), 0, st, B, mode));
+  else ENFLOW_TIMED("lg_layer_kernel", st, hipLaunchKernelGGL((lg_layer_kernel<HH, PREC, false>), dim3(grid), dim3(BLOCK), 0, st, B, mode));
 }
 template <int HH>
 static void lg_layer_prec(int prec, int grid, hipStream_t st, const LgArgs& B, int mode) {
@@ -565,10 +571,10 @@ static void lg_layer(int H, int prec, int grid, hipStream_t st, const LgArgs& B,
 // images -> id_mapping -> pair words -> layer, for one layer
 static void lg_one_layer(int H, int prec, hipStream_t st, LgArgs& B, int rev, int mode) {
   const int A = B.num_atoms;
-  hipLaunchKernelGGL(lg_images_kernel, dim3((A + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, B, rev);
-  hipLaunchKernelGGL(lg_idmap_kernel, dim3(B.num_mols), dim3(IDB), 0, st, B);
+  ENFLOW_TIMED("lg_images_kernel", st, hipLaunchKernelGGL(lg_images_kernel, dim3((A + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, B, rev));
+  ENFLOW_TIMED("lg_idmap_kernel", st, hipLaunchKernelGGL(lg_idmap_kernel, dim3(B.num_mols), dim3(IDB), 0, st, B));
   const int grid = A / B.rbl + B.num_mols + 1;   // >= the number of row blocks
-  hipLaunchKernelGGL(lg_pairs_kernel, dim3(grid), dim3(BLOCK), 0, st, B);
+  ENFLOW_TIMED("lg_pairs_kernel", st, hipLaunchKernelGGL(lg_pairs_kernel, dim3(grid), dim3(BLOCK), 0, st, B));
   lg_layer(H, prec, grid, st, B, mode);
 }
 

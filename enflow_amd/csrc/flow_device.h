@@ -9,8 +9,9 @@
 #include <math.h>
 
 #include "enflow_hip.h"
+#include "enflow_timing.h"
 
-#define ENFLOW_ABI 5
+#define ENFLOW_ABI 6
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8

@@ -37,8 +37,17 @@ class _FlowFunction(torch.autograd.Function):
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
+        prec = flow._prec()
+        if (prec & 0xff) == _lib.PREC_BF16:
+            # the tape feeds the fp32-accurate backward: record it from an fp32-accurate forward
+            prec = (prec & ~0xff) | _lib.PREC_F16X3
+            if not _warned_bf16:
+                _warned_bf16.append(True)
+                import warnings
+                warnings.warn("enflow_amd: gemm_precision='bf16' is a generate-path setting; the training "
+                              "forward runs f16x3", RuntimeWarning, stacklevel=2)
         flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"], meta["max_n"],
-                             meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts)
+                             meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts, prec=prec)
         # queue the backward's weight packing (cached on the parameters' versions,
         # which cannot change before this graph's backward) and the dequantiser's
         # flat parameters behind the forward kernel, ahead of the error check's sync
@@ -124,6 +133,35 @@ class _FlowFunction(torch.autograd.Function):
         return (None, None, gh_in, ag, apos, avel) + tuple(grads)
 
 
+def trainable_batch(data):
+    """True if the HIP backward covers the batch (every molecule <= the
+    backward's whole-molecule pair-list limit)."""
+    N = torch.as_tensor(data.N)
+    return (int(N.max()) if N.numel() else 0) <= _lib.TRAIN_MAX_ATOMS
+
+
+class _Untrainable(torch.autograd.Function):
+    """Identity on the flow outputs whose backward raises: the grad-enabled
+    forward of a batch the HIP backward does not cover."""
+
+    @staticmethod
+    def forward(ctx, h, g, pos, vel, ldj, *params):
+        return h.clone(), g.clone(), pos.clone(), vel.clone(), ldj.clone()
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
+
+
+def guard_untrainable(flow, data, ldj):
+    params = [p for p in flow.parameters() if p.requires_grad]
+    data.h, data.g, data.pos, data.vel, ldj = _Untrainable.apply(data.h, data.g, data.pos, data.vel, ldj, *params)
+    return data, ldj
+
+
+_warned_bf16 = []
+
+
 def flow_forward_train(flow, data, noise, check_errors):
     """Differentiable LFIntegrator.forward (HIP forward with tape)."""
     flow._check_trainable()
@@ -177,6 +215,8 @@ class _NLLFunction(torch.autograd.Function):
     def backward(ctx, gloss):
         h, g, pos, vel = ctx.saved_tensors
         nll, meta = ctx.nll, ctx.meta
+        if meta["max_n"] > _lib.TRAIN_MAX_ATOMS:
+            raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
         L = _lib.lib()
         dev = h.device
         M = meta["mol_ptr"].numel() - 1

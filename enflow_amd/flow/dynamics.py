@@ -138,7 +138,7 @@ class LFIntegrator(BaseFlow):
 
     # ------------------------------------------------------------------
     def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
-                        ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None):
+                        ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None, prec=None):
         """In-place fused forward on preallocated fp32 device buffers (no
         host sync, no allocation): the entry point the benchmark times.
         Molecules past the fused kernel's LDS image (> enflow_max_atoms())
@@ -148,6 +148,7 @@ class LFIntegrator(BaseFlow):
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         dev = h.device
+        prec = self._prec() if prec is None else prec
         dq = self.dequantize.packed(dev) if kind == _lib.DEQUANT_ARGMAX else None
         scale = float(getattr(self.dequantize, "dequant_scale", 1.0)) if kind == _lib.DEQUANT_FLOOR else 0.0
         L = _lib.lib()
@@ -160,7 +161,7 @@ class LFIntegrator(BaseFlow):
                 _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
                 _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
                 _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
-                _lib.ptr(err), self._prec(), _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)),
+                _lib.ptr(err), prec, _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)),
                 "enflow_lf_forward_large_f32")
             return
         _lib.check(L.enflow_lf_forward_f32(
@@ -168,7 +169,7 @@ class LFIntegrator(BaseFlow):
             _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
             _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
             _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
-            _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), self._prec(),
+            _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), prec,
             _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
 
     def reverse_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, argmax_idx, max_idx, err):
@@ -212,8 +213,17 @@ class LFIntegrator(BaseFlow):
         grad_fn whose backward is the HIP backward (enflow_lf_backward_f32),
         so the reference's ``loss.backward()`` / optimiser loop runs unchanged."""
         if self._needs_grad():
-            from ._train import flow_forward_train
-            return flow_forward_train(self, data, noise, check_errors)
+            from ._train import flow_forward_train, trainable_batch, guard_untrainable
+            if trainable_batch(data):
+                return flow_forward_train(self, data, noise, check_errors)
+            # past the HIP backward's molecule size: run the inference kernels (the
+            # reference's Main.generate calls model(out) with autograd on, main.py:275);
+            # only an actual loss.backward() through these outputs raises
+            warnings.warn("enflow_amd: " + _lib.LARGE_TRAIN_MSG + "; this forward is not differentiable "
+                          "(loss.backward() through it raises NotImplementedError)", RuntimeWarning, stacklevel=2)
+            with torch.no_grad():
+                out, ldj = self.forward(data, noise=noise, check_errors=check_errors)
+            return guard_untrainable(self, out, ldj)
         s = self._state(data)
         dev = s["dev"]
         kind = self._dequant_kind()

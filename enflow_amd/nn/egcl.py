@@ -119,8 +119,9 @@ class EGCL(nn.Module):
         self._check_supported()
         _lib.require_gpu(h)
         if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            warnings.warn("enflow_amd EGCL: HIP backward is not implemented yet; outputs are "
-                          "detached", RuntimeWarning, stacklevel=2)
+            warnings.warn("enflow_amd EGCL: a standalone EGCL.forward is not differentiable (the HIP "
+                          "backward runs fused inside LFIntegrator, which trains); outputs are detached",
+                          RuntimeWarning, stacklevel=2)
         L = _lib.lib()
         dev = h.device
         n = h.shape[0]

@@ -36,6 +36,9 @@ extern "C" {
 #define ENFLOW_ERR_TOO_MANY_ATOMS   1  /* molecule larger than the kernel's NMAX */
 #define ENFLOW_ERR_FEW_IMAGES       2  /* reference would IndexError (base.py:137) */
 #define ENFLOW_ERR_TOO_MANY_FEATURES 4
+#define ENFLOW_ERR_RANGE            8  /* f16x3 / bf16 GEMM path produced a non-finite output
+                                          (an operand past the fp16 / bf16 range): rerun
+                                          with ENFLOW_PREC_F32 */
 
 /* Precision of the flow's two H x H edge GEMMs (edge_nn.2, coord_nn.0); all
  * other arithmetic is fp32 in every mode.  See DESIGN.md for the error model. */
@@ -47,7 +50,8 @@ extern "C" {
 #define ENFLOW_DEQUANT_ARGMAX 1  /* enflow/nn/argmax.py */
 #define ENFLOW_DEQUANT_FLOOR  2  /* enflow/nn/floor.py  */
 
-/* ABI version of this header; bump on any signature change. */
+/* ABI version of this header; bump on any signature or error-semantics change (6: ENFLOW_ERR_RANGE,
+ * bf16 + tape rejected, NaN-poisoned gradients on a backward error, enflow_timing_*). */
 int enflow_abi_version(void);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept. */
@@ -307,6 +311,20 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
                            float* grad_layers, float* grad_dequant,
                            void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
                            int32_t* err_flag, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Per-kernel timing (measurement only; no reference counterpart).  When
+ * enabled, every kernel this library launches is bracketed by a hipEvent pair
+ * on its own launch stream; collect() waits for the recorded events and adds
+ * their elapsed times per kernel name.  Off by default (no events recorded).
+ * ---------------------------------------------------------------------- */
+int enflow_timing_enable(int on);
+/* Wait for and accumulate the recorded events; returns the number of names. */
+int enflow_timing_collect(void);
+/* Entry i: kernel name (NUL-terminated, truncated to name_len), total
+ * milliseconds and launch count since the last reset.  -1 if i is out of range. */
+int enflow_timing_entry(int i, char* name, int name_len, double* total_ms, int64_t* launches);
+int enflow_timing_reset(void);
 
 #ifdef __cplusplus
 }

@@ -277,7 +277,11 @@ def lf_reverse(layers, state, dt, coords_weight=1.0, dequant_kind="argmax"):
                          coords_weight)
         s["g"] = s["g"] - g * dt
         s["vel"] = (s["vel"] - f * dt) / np.exp(q)
-    s["h"] = argmax_reverse(s["h"]) if dequant_kind == "argmax" else floor_reverse(s["h"])
+    if dequant_kind == "argmax":
+        s["h"] = argmax_reverse(s["h"])
+    elif dequant_kind == "floor":
+        s["h"] = floor_reverse(s["h"])
+    # dequant_kind "none": the continuous h before the dequantiser's reverse (test checks)
     return s
 
 

@@ -102,8 +102,10 @@ def test_large_flow_vs_oracle(prec):
         back = model.reverse(Data.from_arrays(st, device=DEV))
     rback = O.lf_reverse(layers, st, model.dt)
     np.testing.assert_array_equal(back.h.cpu().numpy(), rback["h"])
-    for k in ("g", "pos", "vel"):
-        assert rel_err(getattr(back, k).cpu().numpy(), rback[k]) < 1e-4, k
+    errs = {k: rel_err(getattr(back, k).cpu().numpy(), rback[k]) for k in ("g", "pos", "vel")}
+    print(f"large flow {prec} reverse vs oracle (same fp32 inputs):",
+          {k: f"{v:.2e}" for k, v in errs.items()})
+    assert all(v < TOL for v in errs.values()), errs
 
 
 def test_large_flow_variants_vs_oracle():
@@ -165,12 +167,24 @@ def test_generate_example_box_2944():
         assert bad.mean() < 0.01, (k, int(bad.sum()))
 
 
-def test_large_training_is_rejected():
+def test_large_grad_enabled_forward_runs_and_backward_raises():
+    """The reference's Main.generate calls model(out) with autograd enabled
+    (main.py:275): past the HIP backward's size limit that forward must run
+    (same outputs as under no_grad, with a warning); only loss.backward()
+    through it raises NotImplementedError."""
     from enflow_amd.data import Data
+    from enflow_amd.flow import Alchemical_NLL
     b = _boxes([300], 8)
     model = _model(32, 5, 1, 9)
+    noise = torch.randn((300, 5), device=DEV, generator=torch.Generator(DEV).manual_seed(3))
+    with pytest.warns(RuntimeWarning):
+        o, ldj = model(Data.from_arrays(b, device=DEV), noise=noise)
+    with torch.no_grad():
+        o2, ldj2 = model(Data.from_arrays(b, device=DEV), noise=noise)
+    assert torch.equal(o.pos.detach(), o2.pos) and float(ldj) == float(ldj2)
+    loss = Alchemical_NLL(kBT=1.0, softening=0.1)(o, ldj)
     with pytest.raises(NotImplementedError):
-        model(Data.from_arrays(b, device=DEV))
+        loss.backward()
 
 
 def test_large_floor_dequant_vs_oracle():
@@ -194,5 +208,11 @@ def test_large_floor_dequant_vs_oracle():
         assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
     assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
     with torch.no_grad():
-        back = model.reverse(o)
-    assert (back.h.cpu().numpy() == b["h"]).mean() > 0.99
+        back = model.reverse(o.clone())
+    from test_gpu_parity import floor_reverse_check
+    st = {k: getattr(o, k).cpu().double().numpy() for k in ("h", "g", "pos", "vel")}
+    st.update(box=b["box"], r_cut=b["r_cut"], mol_ptr=b["mol_ptr"])
+    rc = O.lf_reverse(layers, st, model.dt, dequant_kind="none")
+    n_ex = floor_reverse_check(back.h.cpu().numpy(), rc["h"], want_exact=b["h"])
+    print(f"large floor reverse: exact except {n_ex} near-integer elements of {b['h'].size}")
+    assert n_ex <= 4

@@ -93,6 +93,10 @@ def test_argmax_matches_reference():
 # fused flow
 # ---------------------------------------------------------------------------
 PRECS = ["f32", "f16x3"]     # both meet the fp32 bar; bf16 has its own test below
+
+
+def fmt(errs):
+    return "{" + ", ".join(f"{k}: {v:.2e}" for k, v in errs.items()) + "}"
 BF16_TOL = 1e-3              # configs[2] (bf16 generate path), normwise; measured <= 1.3e-5
 
 
@@ -105,17 +109,29 @@ def test_lf_forward_matches_reference(name, prec):
     model.gemm_precision = prec
     with torch.no_grad():
         o, ldj = model(d, noise=torch.tensor(inp["eps"], device=DEV))
-    for k in ("h", "g", "pos", "vel"):
-        assert rel_err(getattr(o, k).cpu().numpy(), out[k]) < TOL, k
-    assert abs(float(ldj) - float(out["ldj"])) <= TOL * abs(float(out["ldj"]))
+    errs = {k: rel_err(getattr(o, k).cpu().numpy(), out[k]) for k in ("h", "g", "pos", "vel")}
+    errs["ldj"] = abs(float(ldj) - float(out["ldj"])) / abs(float(out["ldj"]))
     nll = Alchemical_NLL(kBT=float(inp["kBT"]), softening=float(inp["softening"]))(o, ldj)
-    assert abs(float(nll) - float(out["nll"])) <= TOL * abs(float(out["nll"]))
+    errs["nll"] = abs(float(nll) - float(out["nll"])) / abs(float(out["nll"]))
+    print(f"{name} {prec} forward vs reference golden:", fmt(errs))
+    assert all(v < TOL for v in errs.values()), errs
+
+
+def _fixture_layers(inp):
+    return [layer_params(inp, i) for i in range(n_layers(inp))]
 
 
 @pytest.mark.parametrize("prec", PRECS)
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2", "lf_var_h64_L3", "lf_var_h128_L2"])
 def test_lf_reverse_matches_reference(name, prec):
-    """generate direction: reverse of the reference's forward output."""
+    """generate direction (dynamics.py:26-37) on the reference's forward output.
+
+    The HIP path sees that output rounded to float32; the reference's golden
+    reverse started from the float64 output.  The kernel is therefore held to
+    1e-5 against the oracle reverse of the SAME float32 inputs (the oracle is
+    pinned to the reference by tests/test_oracle_golden.py), and the golden
+    itself is checked at 1e-4: the float32 rounding of the inputs, carried
+    through the layers, already accounts for up to ~1e-5 there."""
     inp, out = load(name)
     model, _ = flow_from_fixture(inp, DEV)
     model.gemm_precision = prec
@@ -124,9 +140,17 @@ def test_lf_reverse_matches_reference(name, prec):
         setattr(d, k, torch.tensor(out[k], dtype=torch.float32, device=DEV))
     with torch.no_grad():
         back = model.reverse(d)
+    st = state(inp)
+    for k in ("h", "g", "pos", "vel"):
+        st[k] = out[k].astype(np.float32).astype(np.float64)
+    ref = O.lf_reverse(_fixture_layers(inp), st, float(inp["dt"]))
     np.testing.assert_array_equal(back.h.cpu().numpy(), out["rev_h"])
-    for k in ("g", "pos", "vel"):
-        assert rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) < 1e-4, k
+    np.testing.assert_array_equal(back.h.cpu().numpy(), ref["h"])
+    errs = {k: rel_err(getattr(back, k).cpu().numpy(), ref[k]) for k in ("g", "pos", "vel")}
+    gold = {k: rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) for k in ("g", "pos", "vel")}
+    print(f"{name} {prec} reverse vs oracle(same fp32 inputs):", fmt(errs), "| vs golden:", fmt(gold))
+    assert all(v < TOL for v in errs.values()), errs
+    assert all(v < 1e-4 for v in gold.values()), gold
 
 
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
@@ -191,6 +215,24 @@ def test_ragged_and_edge_sizes_vs_oracle(sizes):
     assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
 
 
+def floor_reverse_check(got, h_cont, want_exact=None, near=1e-5):
+    """Floor.reverse (floor.py:13) after a float32 reverse: got must equal
+    floor(h_cont) (the oracle's continuous reverse of the same float32 inputs)
+    exactly, except elements whose h_cont lies within `near` (relative to
+    max|h|) of an integer -- there a float32 rounding legitimately picks the
+    other side.  Returns the number of such exempt elements."""
+    want = np.floor(h_cont)
+    dist = np.abs(h_cont - np.round(h_cont))
+    exempt = dist <= near * max(np.max(np.abs(h_cont)), 1.0)
+    bad = (got != want) & ~exempt
+    assert not bad.any(), [(tuple(ix), float(got[tuple(ix)]), float(h_cont[tuple(ix)]))
+                           for ix in np.argwhere(bad)[:8]]
+    if want_exact is not None:
+        ok = (got == want_exact) | exempt
+        assert ok.all(), int((~ok).sum())
+    return int(exempt.sum())
+
+
 def test_floor_dequant_vs_oracle():
     from enflow_amd.nn import EGCL, Floor
     from enflow_amd.flow import LFIntegrator
@@ -205,18 +247,19 @@ def test_floor_dequant_vs_oracle():
         o, ldj = model(d, noise=u)
     layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
     ref, ref_ldj = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
-    for k in ("h", "g", "pos", "vel"):
-        assert rel_err(getattr(o, k).cpu().numpy(), ref[k]) < TOL, k
+    errs = {k: rel_err(getattr(o, k).cpu().numpy(), ref[k]) for k in ("h", "g", "pos", "vel")}
+    print("floor forward vs oracle:", fmt(errs))
+    assert all(v < TOL for v in errs.values()), errs
     assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
     with torch.no_grad():
-        back = model.reverse(o)
-    # floor(h + u) after an fp32 round trip: an element whose pre-floor value
-    # lands a hair under an integer legitimately floors down
-    got, want = back.h.cpu().numpy(), np.floor(b["h"])
-    bad = np.argwhere(got != want)
-    info = [(tuple(ix), float(got[tuple(ix)]), float(want[tuple(ix)]), float(u[tuple(ix)]),
-             float(o.h[tuple(ix)])) for ix in bad[:8]]
-    assert (got == want).mean() > 0.99, (len(bad), info)
+        back = model.reverse(o.clone())
+    # the oracle's continuous reverse of the same float32 forward output
+    st = {k: getattr(o, k).cpu().double().numpy() for k in ("h", "g", "pos", "vel")}
+    st.update(box=b["box"], r_cut=b["r_cut"], mol_ptr=b["mol_ptr"])
+    rc = O.lf_reverse(layers, st, model.dt, dequant_kind="none")
+    n_ex = floor_reverse_check(back.h.cpu().numpy(), rc["h"], want_exact=np.floor(b["h"]))
+    print(f"floor reverse: exact except {n_ex} near-integer elements of {b['h'].size}")
+    assert n_ex <= 2
 
 
 def test_molecule_past_fused_image_takes_large_path():
@@ -264,18 +307,81 @@ def test_bench_config_deterministic(bench_run):
     assert torch.equal(l1, l2)
 
 
+SAMPLE = list(range(0, 1024, 32)) + [1023]      # 33 of the 1024 molecules
+
+
+def _sub(b, m):
+    a0, a1 = b["mol_ptr"][m], b["mol_ptr"][m + 1]
+    sub = {k: b[k][a0:a1] for k in ("h", "g", "pos", "vel", "box")}
+    sub["r_cut"] = b["r_cut"][m:m + 1]
+    sub["mol_ptr"] = np.array([0, a1 - a0])
+    return sub, a0, a1
+
+
 def test_bench_config_sampled_molecules_vs_oracle(bench_run):
     """Molecules are independent: check a sample of the 1024 against the oracle."""
     b, model, _, noise, (o1, _), _ = bench_run
-    ptr = b["mol_ptr"]
-    for m in (0, 1, 511, 1023):
-        a0, a1 = ptr[m], ptr[m + 1]
-        sub = {k: b[k][a0:a1] for k in ("h", "g", "pos", "vel", "box")}
-        sub["r_cut"] = b["r_cut"][m:m + 1]
-        sub["mol_ptr"] = np.array([0, a1 - a0])
+    worst = {k: 0.0 for k in ("h", "g", "pos", "vel")}
+    for m in SAMPLE:
+        sub, a0, a1 = _sub(b, m)
         ref, _ = _oracle_flow(model, sub, noise[a0:a1])
-        for k in ("h", "g", "pos", "vel"):
-            assert rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k]) < TOL, (m, k)
+        for k in worst:
+            worst[k] = max(worst[k], rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k]))
+    print(f"bench config forward, {len(SAMPLE)} molecules vs oracle:", fmt(worst))
+    assert all(v < TOL for v in worst.values()), worst
+
+
+def test_bench_config_reverse_vs_oracle(bench_run):
+    """configs[1] shape (1024 x 22 atoms, 8 layers, H=128), generate direction
+    in f16x3: HIP reverse of the whole batch vs the oracle reverse of the same
+    float32 states on sampled molecules."""
+    b, model, _, _, (o1, _), _ = bench_run
+    with torch.no_grad():
+        back = model.reverse(o1.clone())
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    worst = {k: 0.0 for k in ("g", "pos", "vel")}
+    for m in SAMPLE:
+        sub, a0, a1 = _sub(b, m)
+        st = {k: getattr(o1, k)[a0:a1].cpu().double().numpy() for k in ("h", "g", "pos", "vel")}
+        st.update(box=sub["box"], r_cut=sub["r_cut"], mol_ptr=sub["mol_ptr"])
+        ref = O.lf_reverse(layers, st, model.dt)
+        np.testing.assert_array_equal(np.argmax(back.h[a0:a1].cpu().numpy(), 1), np.argmax(ref["h"], 1))
+        for k in worst:
+            worst[k] = max(worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k]))
+    print(f"bench config reverse, {len(SAMPLE)} molecules vs oracle:", fmt(worst))
+    assert all(v < TOL for v in worst.values()), worst
+
+
+BF16_L8_TOL = 5e-3     # bf16 generate at 8 layers (configs[2]), normwise per tensor
+
+
+def test_bf16_generate_8_layers_vs_oracle():
+    """configs[2]: 1024 x 22-atom molecules, 8 layers, H=128, reverse with
+    bf16 edge GEMMs, against the float64 oracle reverse of the same float32
+    inputs on sampled molecules (bar BF16_L8_TOL; the one-hot h exact)."""
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(1024, 22, nf=5, seed=321))
+    model = _make_model(128, 5, 8, 11, default_dt())
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(12))
+    with torch.no_grad():
+        o, _ = model(d, noise=noise)                 # f16x3 forward: the states to generate from
+    model.gemm_precision = "bf16"
+    with torch.no_grad():
+        back = model.reverse(o.clone())
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    worst = {k: 0.0 for k in ("g", "pos", "vel")}
+    for m in SAMPLE[::2]:
+        sub, a0, a1 = _sub(b, m)
+        st = {k: getattr(o, k)[a0:a1].cpu().double().numpy() for k in ("h", "g", "pos", "vel")}
+        st.update(box=sub["box"], r_cut=sub["r_cut"], mol_ptr=sub["mol_ptr"])
+        ref = O.lf_reverse(layers, st, model.dt)
+        np.testing.assert_array_equal(np.argmax(back.h[a0:a1].cpu().numpy(), 1), np.argmax(ref["h"], 1))
+        for k in worst:
+            worst[k] = max(worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k]))
+    print(f"bf16 generate 8 layers, {len(SAMPLE[::2])} molecules vs oracle:", fmt(worst), f"(bar {BF16_L8_TOL:g})")
+    assert all(v < BF16_L8_TOL for v in worst.values()), worst
 
 
 def test_bench_config_roundtrip(bench_run):

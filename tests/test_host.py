@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 5
+    assert L.enflow_abi_version() == 6
     assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
@@ -123,3 +123,31 @@ def test_same_seed_same_init_as_reference():
     net = EGCL(5, 5, 32)
     for k in EGCL_KEYS:
         np.testing.assert_array_equal(net.state_dict()[k].numpy(), inp["p0." + k])
+
+
+def test_kernel_timer_without_launches():
+    """enflow_timing_*: enabling, collecting and reading back with nothing
+    launched (CPU-only: no events are recorded)."""
+    with _lib.KernelTimer() as t:
+        pass
+    assert t.stats == {}
+    assert t.ms_per_launch("lf_flow_kernel<fwd>") is None
+    L = _lib.lib()
+    assert L.enflow_timing_entry(10 ** 6, None, 0, None, None) == -1
+
+
+def test_bench_flop_accounting():
+    """bench.py's roofline: f16x3 issues 3 products per MFMA FLOP, bf16 one for
+    the two H x H edge GEMMs; frac = issued FLOPs / pipe peak."""
+    import bench
+    alg, iss = bench.flop_counts(1000, 100, 8, 128, 5, "f16x3")
+    parts = bench.gemm_parts(128, 5)
+    valu = 1000 * parts["pair"]["coord_nn.2"] + 800 * parts["atom_layer"]["vel_scaling_nn.2"] + \
+        100 * parts["atom"]["argmax.network"]
+    assert iss == 3 * (alg - valu)
+    alg_b, iss_b = bench.flop_counts(1000, 100, 8, 128, 5, "bf16")
+    assert alg_b == alg and iss_b == iss - 2 * 1000 * 2 * (2 * 128 * 128)
+    r = bench.roofline_mfma(alg, iss, 1.0, "f16x3", "k")
+    assert abs(r["frac"] - iss / 1e-3 / 1e12 / 2500.0) < 1e-12
+    assert abs(r["frac"] - r["matrix_pipe"]["frac"]) < 1e-12
+    assert bench.flops_per_launch(1000, 100, 8, 128, 5) == alg
