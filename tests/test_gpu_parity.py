@@ -97,7 +97,7 @@ PRECS = ["f32", "f16x3"]     # both meet the fp32 bar; bf16 has its own test bel
 
 def fmt(errs):
     return "{" + ", ".join(f"{k}: {v:.2e}" for k, v in errs.items()) + "}"
-BF16_TOL = 1e-3              # configs[2] (bf16 generate path), normwise; measured <= 1.3e-5
+BF16_TOL = 5e-5              # configs[2] (bf16 generate path), normwise; measured <= 1.21e-5 (r02a)
 
 
 @pytest.mark.parametrize("prec", PRECS)
@@ -127,11 +127,10 @@ def test_lf_reverse_matches_reference(name, prec):
     """generate direction (dynamics.py:26-37) on the reference's forward output.
 
     The HIP path sees that output rounded to float32; the reference's golden
-    reverse started from the float64 output.  The kernel is therefore held to
-    1e-5 against the oracle reverse of the SAME float32 inputs (the oracle is
-    pinned to the reference by tests/test_oracle_golden.py), and the golden
-    itself is checked at 1e-4: the float32 rounding of the inputs, carried
-    through the layers, already accounts for up to ~1e-5 there."""
+    reverse started from the float64 output.  The kernel is held to 1e-5
+    against both: the oracle reverse of the SAME float32 inputs (the oracle is
+    pinned to the reference by tests/test_oracle_golden.py) and the golden
+    (measured ~1e-7 for both, profiles/r02/r02a_gpu_tests.log)."""
     inp, out = load(name)
     model, _ = flow_from_fixture(inp, DEV)
     model.gemm_precision = prec
@@ -150,7 +149,7 @@ def test_lf_reverse_matches_reference(name, prec):
     gold = {k: rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) for k in ("g", "pos", "vel")}
     print(f"{name} {prec} reverse vs oracle(same fp32 inputs):", fmt(errs), "| vs golden:", fmt(gold))
     assert all(v < TOL for v in errs.values()), errs
-    assert all(v < 1e-4 for v in gold.values()), gold
+    assert all(v < TOL for v in gold.values()), gold
 
 
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
@@ -173,7 +172,7 @@ def test_lf_bf16_generate_and_forward(name):
         o, ldj = model2(d2, noise=torch.tensor(inp["eps"], device=DEV))
     errs.update({"fwd_" + k: rel_err(getattr(o, k).cpu().numpy(), out[k]) for k in ("h", "g", "pos", "vel")})
     errs["fwd_ldj"] = abs(float(ldj) - float(out["ldj"])) / abs(float(out["ldj"]))
-    print(name, "bf16 errors", errs)
+    print(f"{name} bf16 vs reference golden:", fmt(errs))
     assert all(v < BF16_TOL for v in errs.values()), errs
 
 
@@ -352,7 +351,7 @@ def test_bench_config_reverse_vs_oracle(bench_run):
     assert all(v < TOL for v in worst.values()), worst
 
 
-BF16_L8_TOL = 5e-3     # bf16 generate at 8 layers (configs[2]), normwise per tensor
+BF16_L8_TOL = 1e-4     # bf16 generate at 8 layers (configs[2]), normwise per tensor; measured 2.6e-5 (r02a)
 
 
 def test_bf16_generate_8_layers_vs_oracle():
