@@ -516,7 +516,35 @@ __device__ __forceinline__ f32x16 mfma_f16(f32x4 a, f16x8 b, f32x16 c) {
 __device__ __forceinline__ f32x16 mfma_bf16(f32x4 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
 }
+// x = hi + lo in fp16.  ENFLOW_SPLIT_MIX: lo = f16(x - hi) by v_fma_mix{lo,hi}_f16
+// reading hi straight from its packed fp16 register (x * 1 - hi in one fused
+// op, one rounding), 1.5 VALU per element instead of 3 (convert hi back to
+// fp32, subtract, convert).
+#ifndef ENFLOW_SPLIT_MIX
+#define ENFLOW_SPLIT_MIX 1
+#endif
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t split_lo2(float x0, float x1, uint32_t hi) {
+  uint32_t lo;
+  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(lo) : "v"(x0), "v"(x1), "v"(hi));
+  return lo;
+}
 __device__ __forceinline__ void split_f16(const f32x16& X, int s, f16x8& hi, f16x8& lo) {
+#if ENFLOW_SPLIT_MIX
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float x0 = X[8 * s + 2 * j], x1 = X[8 * s + 2 * j + 1];
+    const f16x2 hp = {(_Float16)x0, (_Float16)x1};          // v_cvt_pk_f16_f32 (RNE)
+    h[j] = __builtin_bit_cast(uint32_t, hp);
+    l[j] = split_lo2(x0, x1, h[j]);
+  }
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  hi = __builtin_bit_cast(f16x8, (u32x4){h[0], h[1], h[2], h[3]});
+  lo = __builtin_bit_cast(f16x8, (u32x4){l[0], l[1], l[2], l[3]});
+#else
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const float x = X[8 * s + j];
@@ -524,6 +552,7 @@ __device__ __forceinline__ void split_f16(const f32x16& X, int s, f16x8& hi, f16
     hi[j] = h;
     lo[j] = (_Float16)(x - (float)h);
   }
+#endif
 }
 __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
   bf16x8 b;
@@ -725,7 +754,11 @@ __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 template <int H, int NMAX, int RB = NMAX, bool BWD = false>
 struct Smem {
   static constexpr int NT = H / 32;
-  static constexpr int AST = H + 3;   // agg row: H message sums, 3 force sums (odd stride)
+  // agg row: H message sums, 3 force sums.  Forward images: H + 4 floats, rows
+  // 16-B aligned so a segment end adds 4 features with one ds_read_b128 /
+  // ds_write_b128 at a constant offset (ds_read_b128 banks 4 a + c mod 64: conflict-
+  // free over 16 rows); the backward's atom-lane b32 stores keep the odd stride.
+  static constexpr int AST = BWD ? H + 3 : H + 4;
   static constexpr bool BLOCKED = RB < NMAX;
   static constexpr bool PACKC = BLOCKED || BWD;                          // 2 x 16-bit counts per word
   static constexpr int MAXP = RB * (NMAX - 1);
@@ -747,9 +780,8 @@ struct Smem {
   // x 4 floats) for the <= 32-atom image (larger images read them from L2)
   static constexpr bool W1X_LDS = !BLOCKED && !BWD && NMAX <= 32;
   alignas(16) float w1x[W1X_LDS ? NT * 2 * 512 : 4];
-  float agg[RB * AST];
-  float head[BWD ? 1 : WAVES][BWD ? 1 : H + 4];
-  float trash[BWD ? 1 : WAVES][BWD ? 1 : 64];   // sink for the branch-free segment-sum stores
+  alignas(16) float agg[RB * AST];
+  alignas(16) float head[BWD ? 1 : WAVES][BWD ? 1 : H + 4];
   uint32_t pairs[PC];
   uint32_t mask27[NMAX];
   int idmap[NMAX];
@@ -992,6 +1024,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const rsrc_t W = weights_rsrc(Lp, L.total);
   const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
   // F16X3 accumulators carry the weight scale 2^s: unscale exactly in the bias fma
+  const float inv0 = PREC != PREC_F32 ? Lp[L.scl + 5] : 1.f;   // edge_nn.0 runs F16X3 in bf16 mode too
   const float inv1 = PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f;
   const float inv2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
   // constructor variants of the layer (wave-uniform; compiled in only for VAR
@@ -1069,9 +1102,6 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
           x0[t] = mfma_f16(al, bh, x0[t]);
         }
       }
-      const float inv0 = Lp[L.scl + 5];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) x0[t] *= inv0;
     } else {
       float cur[NT], nxt[NT];
 #pragma unroll
@@ -1102,11 +1132,12 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     }
     STAMP(9);
     // x0 tile 0 activated now, tiles 1.. as fillers of GEMM1's steps on tile t-1
+    // (split-precision GEMM0 accumulators carry edge_nn.0's 2^s: unscaled in the bias fma)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 8 * g4 + 4 * hh);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = silu_f(x0[0][4 * g4 + u] + b[u]);
+      for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = silu_f(fmaf(x0[0][4 * g4 + u], inv0, b[u]));
     }
     STAMP(10);
 
@@ -1119,7 +1150,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
       if (t < NT) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 32 * t + 8 * g4 + 4 * hh);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = silu_f(x0[t][4 * g4 + u] + b[u]);
+        for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = silu_f(fmaf(x0[t][4 * g4 + u], inv0, b[u]));
       }
     });
     STAMP(11);
@@ -1155,11 +1186,11 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     STAMP(13);
     // ---- GEMM2: coord_nn.0 (egcl.py:35-42), with fillers: activate e tile t+1
     //      and segment-sum the messages of tile t (egcl.py:64-65, multiplicity-
-    //      weighted, DPP segmented scan; the row's last lane adds to LDS, other
-    //      lanes add into a private trash slot -- branch-free)
-    float* const trash = &sm.trash[w][lane];
-    float* const dstm = seg_end ? dst_row : trash;
-    const int fstride = seg_end ? 1 : 0;
+    //      weighted, DPP segmented scan; the row's last lane adds its 4 features
+    //      into the row with one ds_read_b128 / ds_write_b128 at a constant offset:
+    //      the read is issued before the scan (every lane reads its own row, only
+    //      segment ends write), one adder per (row, feature) and tile)
+    float* const rowp = dst_row + 4 * hh;
     float part = 0.f;
     {
       f32x16 hc[NT];
@@ -1172,6 +1203,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
       chain_prec_fill<PREC, NT, 6>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
         const int t = step >> 2, g4 = step & 3;
 #if !(ENFLOW_ABLATE & 4)
+        f32x4* const slot = reinterpret_cast<f32x4*>(rowp + 32 * t + 8 * g4);
+        const f32x4 old = *slot;
         float v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = c * e[t][4 * g4 + u];
@@ -1181,10 +1214,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = seg_scan(v[u], SM);
 #endif
-        // one adder per (row, feature) and tile (rows shared with another wave go
-        // to its head buffer); plain read-modify-write: ds_add_f32 measured 1.7x slower
-#pragma unroll
-        for (int u = 0; u < 4; ++u) dstm[(32 * t + 8 * g4 + 4 * hh + u) * fstride] += v[u];
+        if (seg_end) *slot = old + (f32x4){v[0], v[1], v[2], v[3]};
 #endif
         if (t + 1 < NT && !v_att) {
           const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * (t + 1) + 8 * g4 + 4 * hh);
@@ -1209,22 +1239,20 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     const float nd = v_nd ? __builtin_amdgcn_rcpf(sqrtf(radial) + 1.f) : 1.f;
     // trans = clamp(coord_diff * phi, -100, 100) (egcl.py:71-72); segment sums
     // for the mean (egcl.py:73-74); lane half 0 stores
+    f32x4* const fslot = reinterpret_cast<f32x4*>(dst_row + H);   // H + 3 is padding (tw = 0)
+    const f32x4 fold = *fslot;
     float tx = c * fminf(fmaxf(dx * nd * phi, -100.f), 100.f);
     float ty = c * fminf(fmaxf(dy * nd * phi, -100.f), 100.f);
     float tz = c * fminf(fmaxf(dz * nd * phi, -100.f), 100.f);
-#if ENFLOW_SEGSCAN_ASM
     float tw = 0.f;
+#if ENFLOW_SEGSCAN_ASM
     seg_scan4(tx, ty, tz, tw, SM);
 #else
     tx = seg_scan(tx, SM);
     ty = seg_scan(ty, SM);
     tz = seg_scan(tz, SM);
 #endif
-    float* const dstf = (seg_end && hh == 0) ? dst_row : trash;
-    const int fs = (seg_end && hh == 0) ? 1 : 0;
-    dstf[(H + 0) * fs] += tx;
-    dstf[(H + 1) * fs] += ty;
-    dstf[(H + 2) * fs] += tz;
+    if (seg_end && hh == 0) *fslot = fold + (f32x4){tx, ty, tz, tw};
     STAMP(14);
   }
   __syncthreads();

@@ -19,7 +19,9 @@ def main():
     libs = sys.argv[1:]
     dev = torch.device("cuda", 0)
     c = bench.MODES[os.environ.get("AB_MODE", "forward")]
-    b, model, inp = bench.build_workload(0, dev, c["mols"], c["atoms"], c["layers"], c["chain"])
+    from enflow_amd.data.synthetic import make_molecules
+    model = bench.build_model(dev, c["layers"])
+    inp = bench.batch_tensors(make_molecules(c["mols"], c["atoms"], nf=bench.NF, seed=1000, chain=c["chain"]), dev)
     model.gemm_precision = c["prec"]
     mols, atoms = c["mols"], c["atoms"]
     work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
@@ -57,8 +59,10 @@ def main():
     base = outs[libs[0]]
     for p in libs:
         same = torch.equal(outs[p][0], base[0])
+        rel = float((outs[p][0] - base[0]).abs().max() / base[0].abs().max())
         print(f"{os.path.basename(p):40s} median {statistics.median(res[p]):.4f} ms  min {min(res[p]):.4f} ms"
-              f"  mol/s {mols / statistics.median(res[p]) * 1e3:.0f}  bitwise-equal-to-first {same}")
+              f"  mol/s {mols / statistics.median(res[p]) * 1e3:.0f}  bitwise-equal-to-first {same} "
+              f"pos-rel-diff {rel:.2e}", flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,29 @@
+"""Build an A/B variant of libenflow_hip.so: enflow_flow.hip recompiled with
+extra -D defines / hipcc flags, linked with the product build's other objects.
+
+    python tools/build_variant.py NAME [-DFOO=1 | -fflag ...]   ->  enflow_amd/var/libenflow_NAME.so
+"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "enflow_amd", "libenflow_hip.so")
+
+
+def main():
+    name, flags = sys.argv[1], sys.argv[2:]
+    out_dir = os.path.join(ROOT, "enflow_amd", "var")
+    os.makedirs(out_dir, exist_ok=True)
+    obj = os.path.join(out_dir, f"flow_{name}.o")
+    base = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include")]
+    subprocess.run(base + flags + ["-c", os.path.join(ROOT, "enflow_amd", "csrc", "enflow_flow.hip"), "-o", obj],
+                   check=True)
+    others = [LIB + "." + s + ".o" for s in ("enflow_backward.hip", "enflow_large.hip", "enflow_timing.hip")]
+    so = os.path.join(out_dir, f"libenflow_{name}.so")
+    subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, obj] + others, check=True)
+    print(so)
+
+
+if __name__ == "__main__":
+    main()

@@ -16,11 +16,15 @@ PHASES = ["load", "dequant", "pairs", "-", "edge_tiles(all)", "node", "update", 
 
 
 def main():
-    if not os.path.exists(SO):
-        subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                        "-DENFLOW_STAMPS", "-I", os.path.join(ROOT, "include"), "-o", SO,
-                        os.path.join(ROOT, "enflow_amd", "csrc", "enflow_flow.hip"),
-                        os.path.join(ROOT, "enflow_amd", "csrc", "enflow_backward.hip")], check=True)
+    global SO
+    if len(sys.argv) > 1 and sys.argv[1].endswith(".so"):
+        SO = os.path.abspath(sys.argv[1])
+    if not os.path.exists(SO):          # build here (CPU container) and ship: the box only runs it
+        sys.path.insert(0, ROOT)
+        from enflow_amd.build import build
+        build(force=True, out=SO, defines=["ENFLOW_STAMPS"])
+    if len(sys.argv) > 1 and sys.argv[1] == "build":
+        return
     os.environ["ENFLOW_LIB"] = SO
     sys.path.insert(0, ROOT)
     import torch
@@ -30,7 +34,9 @@ def main():
     L.enflow_read_stamps.restype = ctypes.c_int
     L.enflow_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
     dev = torch.device("cuda", 0)
-    b, model, inp = bench.build_workload(0, dev)
+    from enflow_amd.data.synthetic import make_molecules
+    model = bench.build_model(dev, bench.LAYERS)
+    inp = bench.batch_tensors(make_molecules(bench.MOLS_PER_GPU, bench.ATOMS, nf=bench.NF, seed=1000), dev)
     work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
     noise = torch.randn_like(inp["h"])
     ldj_mol = torch.empty(bench.MOLS_PER_GPU, device=dev)
