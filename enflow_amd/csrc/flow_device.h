@@ -294,13 +294,21 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// DPP moves (VALU, no LDS): row_shr:n = 0x110 + n, row_bcast:15 = 0x142, row_bcast:31 = 0x143.
+// Lanes whose source is outside the 16-lane row (or rows not in ROWMASK) get `old`.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xf, false);
+}
+
+// inclusive prefix sum over the wave's 64 lanes, DPP only (no LDS round trips)
 __device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    int t = __shfl_up(v, off, 64);
-    if (lane >= off) v += t;
-  }
+  v += dpp_i<0x111, 0xf>(0, v);
+  v += dpp_i<0x112, 0xf>(0, v);
+  v += dpp_i<0x114, 0xf>(0, v);
+  v += dpp_i<0x118, 0xf>(0, v);
+  v += dpp_i<0x142, 0xa>(0, v);
+  v += dpp_i<0x143, 0xc>(0, v);
   return v;
 }
 
@@ -310,12 +318,6 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// DPP moves (VALU, no LDS): row_shr:n = 0x110 + n, row_bcast:15 = 0x142.
-// Lanes whose source is outside the 16-lane row (or rows not in ROWMASK) get `old`.
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ int dpp_i(int old, int v) {
-  return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xf, false);
-}
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ float dpp_f(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWMASK, 0xf, false));
@@ -853,17 +855,30 @@ __device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
     const int lane = tid;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int prefix = 0;
-    for (int s = 0; s < 27 && prefix < n; ++s) {
-      for (int ch = 0; ch < n; ch += 64) {
-        const int a = ch + lane;
-        const uint32_t mk = a < n ? sm.mask27[a] : 0u;
+    if (n <= 64) {   // one chunk: the lane's mask loaded once, 27 ballots on registers
+      const uint32_t mk = lane < n ? sm.mask27[lane] : 0u;
+      for (int s = 0; s < 27 && prefix < n; ++s) {
         const bool bit = (mk >> s) & 1u;
         const uint64_t bal = __ballot(bit);
         if (bit) {
           const int posF = prefix + __popcll(bal & lt);
-          if (posF < n) sm.idmap[posF] = a;
+          if (posF < n) sm.idmap[posF] = lane;
         }
         prefix += __popcll(bal);
+      }
+    } else {
+      for (int s = 0; s < 27 && prefix < n; ++s) {
+        for (int ch = 0; ch < n; ch += 64) {
+          const int a = ch + lane;
+          const uint32_t mk = a < n ? sm.mask27[a] : 0u;
+          const bool bit = (mk >> s) & 1u;
+          const uint64_t bal = __ballot(bit);
+          if (bit) {
+            const int posF = prefix + __popcll(bal & lt);
+            if (posF < n) sm.idmap[posF] = a;
+          }
+          prefix += __popcll(bal);
+        }
       }
     }
     if (lane == 0 && prefix < n) sm.err |= ENFLOW_ERR_FEW_IMAGES;
@@ -1452,8 +1467,15 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
         al[(ks + 2) % 3] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + ks + 2) * 512) * 4);
       }
       f32x16 av;
+      {   // two ds_read_b128 (rows 16-B aligned, AST % 4 == 0); invalid atoms read row 0, zeroed
+        static_assert(AST % 4 == 0, "node phase reads agg rows as float4");
+        const f32x4 a0 = ld4(arow + 16 * ks + 8 * hh), a1 = ld4(arow + 16 * ks + 8 * hh + 4);
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) av[jj] = va ? arow[16 * ks + 8 * hh + jj] : 0.f;
+        for (int jj = 0; jj < 4; ++jj) {
+          av[jj] = va ? a0[jj] : 0.f;
+          av[4 + jj] = va ? a1[jj] : 0.f;
+        }
+      }
       f16x8 bh, bl;
       split_f16(av, 0, bh, bl);
       acc = mfma_f16(ah[ks % 3], bh, acc);
