@@ -471,8 +471,7 @@ def run_train(args, world, rank, local, device, dist):
         torch.randn(noise.shape, generator=gen, out=noise)
         out, ldj = net(base._replace(), noise=noise)
         loss = nll(out, ldj)
-        loss.backward()
-        L_.check_pending()                  # the backward's error word, before the update
+        loss.backward()                     # a backward error NaN-poisons the grads; raised at the next check
         opt.step()
         return loss
 

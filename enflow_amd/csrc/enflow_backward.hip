@@ -1513,8 +1513,15 @@ static inline int hid_ok_b(int H) { return H == 32 || H == 64 || H == 128; }
 static inline size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Workspace: the per-layer pair-row / atom-row / partial sections are double
+// buffered (BWD_NBUF copies, `span` floats apart): layer l's weight-gradient pass
+// (outer kernels, on an auxiliary stream) reads buffer l & 1 while layer l-1's
+// backward writes the other one.
+#define BWD_NBUF 2
 struct BwdWs {
-  size_t offs, xin, p0, pe, pc, dp0, dpe, aphi, patt, dlogit, su, au, sn, an, aq, agr, anet, part, total;  // floats
+  size_t offs, buf0, span;   // shared offsets section; first buffer; buffer stride
+  // offsets within a buffer (floats)
+  size_t xin, p0, pe, pc, dp0, dpe, aphi, patt, dlogit, su, au, sn, an, aq, agr, anet, part, total;
   size_t part_floats;
 };
 
@@ -1522,7 +1529,8 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   BwdWs W;
   size_t o = 0;
   const size_t P = (size_t)prb, A = (size_t)num_atoms;
-  W.offs = o; o += al64((size_t)n_layers * (num_mols + 1));
+  W.offs = 0;
+  W.buf0 = al64((size_t)n_layers * (num_mols + 1));
   W.xin = o; o += al64(P * 16);
   W.p0 = o; o += al64(P * H);
   W.pe = o; o += al64(P * H);
@@ -1546,9 +1554,43 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   const size_t am = cha * ((size_t)H * (nf + 1) + (size_t)2 * nf * (H + 1));
   if (am > W.part_floats) W.part_floats = am;
   W.part = o; o += al64(W.part_floats);
-  W.total = o;
+  W.span = o;
+  W.total = W.buf0 + BWD_NBUF * W.span;
   return W;
 }
+
+// Auxiliary stream (per device) for the weight-gradient passes, and a pool of
+// sync events.  Host-side state only; guarded by a mutex (one backward's launch
+// sequence at a time per process).
+#include <mutex>
+#include <vector>
+namespace {
+struct AuxDev {
+  hipStream_t s = nullptr;
+  std::vector<hipEvent_t> ev;
+};
+std::mutex g_aux_mu;
+AuxDev g_aux[64];
+hipStream_t aux_stream(int dev) {
+  if (!g_aux[dev].s) {   // created on `dev` (the caller's stream's device)
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    if (hipStreamCreateWithFlags(&g_aux[dev].s, hipStreamNonBlocking) != hipSuccess) g_aux[dev].s = nullptr;
+    if (cur != dev) (void)hipSetDevice(cur);
+  }
+  return g_aux[dev].s;
+}
+hipEvent_t aux_event(int dev, size_t i) {
+  auto& v = g_aux[dev].ev;
+  while (v.size() <= i) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    v.push_back(e);
+  }
+  return v[i];
+}
+}  // namespace
 
 static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, const float* X, int ldx, int N,
                      const int32_t* rows_dev, int rows_static, int rows_bound, float*& part, float* outW,
@@ -1724,11 +1766,25 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
   const EgclBwdLayout LB = egcl_bwd_layout(H);
   const RawEgcl R = raw_egcl(H, nf);
   const int prb = (int)pair_row_bound;
+  // weight-gradient passes of layer l run on an auxiliary stream, overlapping the
+  // layer backward of l - 1 (double-buffered rows); the caller's stream joins it
+  // before the dequantiser's gradients and before returning
+  int dev = 0;
+  if ((st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev)) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  std::lock_guard<std::mutex> aux_lock(g_aux_mu);
+  hipStream_t st2 = aux_stream(dev);
+  if (!st2) return -2;
+  auto ev = [&](int i) { return aux_event(dev, (size_t)i); };   // 2 l: backward of l done, 2 l + 1: outer of l done
+  for (int i = 0; i < 2 * n_layers + 1; ++i)
+    if (!ev(i)) return -2;
 
   if (n_layers > 0)
     hipLaunchKernelGGL(pair_offsets_kernel, dim3(n_layers), dim3(BLOCK), 0, st, pair_counts, num_mols, offs);
 
   for (int l = n_layers - 1; l >= 0; --l) {
+    float* const wb = ws + Wl.buf0 + (size_t)(l & 1) * Wl.span;   // this layer's buffer
+    // the buffer was last read by layer l + 2's weight-gradient pass
+    if (l + 2 < n_layers && hipStreamWaitEvent(st, ev(2 * (l + 2) + 1), 0) != hipSuccess) return -2;
     BwdArgs A;
     A.mol_ptr = mol_ptr; A.r_cut = r_cut; A.box = box; A.tape = tape;
     A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
@@ -1738,11 +1794,11 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
     A.pair_off = offs + (size_t)l * (num_mols + 1);
-    A.xin = ws + Wl.xin; A.p0 = ws + Wl.p0; A.pe = ws + Wl.pe; A.pc = ws + Wl.pc;
-    A.dp0 = ws + Wl.dp0; A.dpe = ws + Wl.dpe; A.aphi = ws + Wl.aphi;
-    A.patt = ws + Wl.patt; A.dlogit = ws + Wl.dlogit;
-    A.su = ws + Wl.su; A.au = ws + Wl.au; A.sn = ws + Wl.sn; A.an = ws + Wl.an;
-    A.aq = ws + Wl.aq; A.agr = ws + Wl.agr; A.err = err_flag;
+    A.xin = wb + Wl.xin; A.p0 = wb + Wl.p0; A.pe = wb + Wl.pe; A.pc = wb + Wl.pc;
+    A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
+    A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
+    A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
+    A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
     if (variants) {
 #define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);
@@ -1752,7 +1808,9 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
       DISPATCH_HN_B(H, max_mol_atoms, CALL);
 #undef CALL
     }
-    // the layer's weight gradients, straight into the torch parameter layout
+    if (hipEventRecord(ev(2 * l), st) != hipSuccess || hipStreamWaitEvent(st2, ev(2 * l), 0) != hipSuccess)
+      return -2;
+    // the layer's weight gradients, straight into the torch parameter layout (aux stream)
     float* G = grad_layers + (size_t)l * R.total_bwd;
     const int32_t* prow = offs + (size_t)l * (num_mols + 1) + num_mols;
     const float* hx = tape + tape_layout(num_atoms, nf, H, n_layers).hx +
@@ -1760,40 +1818,44 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     OuterBatch ob;
     ob.nd = 0;
     int wg = 0;
-    float* part = ws + Wl.part;
-    add_desc(ob, wg, ws + Wl.dp0, H, H, ws + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, PAIR_OUTER);
-    add_desc(ob, wg, ws + Wl.dpe, H, H, ws + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
+    float* part = wb + Wl.part;
+    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, PAIR_OUTER);
+    add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
-    add_desc(ob, wg, ws + Wl.pc, H, H, ws + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);
+    add_desc(ob, wg, wb + Wl.pc, H, H, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
     ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
-    ob.d[ob.nd - 1].rowv = ws + Wl.aphi;
-    if (variants) ob.d[ob.nd - 1].xrow = ws + Wl.patt;          // the message is e * att
+    ob.d[ob.nd - 1].rowv = wb + Wl.aphi;
+    if (variants) ob.d[ob.nd - 1].xrow = wb + Wl.patt;          // the message is e * att
     ob.d[ob.nd - 1].colv = A.Rp + R.wc2;
     // coord_nn.2: d wc2 = sum_rows aphi silu(pc); aphi is one value per row (its "tile-blocked"
     // layout is row-major with width 1)
-    add_desc(ob, wg, ws + Wl.aphi, 1, 1, ws + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr,
+    add_desc(ob, wg, wb + Wl.aphi, 1, 1, wb + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr,
              ENFLOW_OUTER_X3 ? 3 : 1);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
     if (ENFLOW_OUTER_X3) ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;   // folded into coord_nn.0's pass
     if (variants) {   // att_nn.0: d w = sum_rows dlogit e, d b = sum_rows dlogit (0 rows without attention)
-      add_desc(ob, wg, ws + Wl.dlogit, 1, 1, ws + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
+      add_desc(ob, wg, wb + Wl.dlogit, 1, 1, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
       ob.d[ob.nd - 1].xf_x = 1;                                 // X = silu(pre_e) = e
     }
-    add_desc(ob, wg, ws + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
-    add_desc(ob, wg, ws + Wl.aq, 1, 1, ws + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
-    add_desc(ob, wg, ws + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,
+    add_desc(ob, wg, wb + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
+    add_desc(ob, wg, wb + Wl.aq, 1, 1, wb + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
+    add_desc(ob, wg, wb + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,
              G + R.bn1);
-    add_desc(ob, wg, ws + Wl.agr, nf, nf, ws + Wl.sn, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wn2,
+    add_desc(ob, wg, wb + Wl.agr, nf, nf, wb + Wl.sn, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wn2,
              G + R.bn2);
-    const int rc = run_outer(ob, wg, st);
+    const int rc = run_outer(ob, wg, st2);
     if (rc) return rc;
+    if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
   }
+  // join: every weight-gradient pass done before the dequantiser's (buffer 0 again) and the return
+  if (n_layers > 0 && hipStreamWaitEvent(st, ev(1), 0) != hipSuccess) return -2;   // layer 0's pass (the last)
 
   if (dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-    float* apre = ws + Wl.au;
-    float* spre = ws + Wl.su;
-    float* anet = ws + Wl.anet;
+    float* const wb = ws + Wl.buf0;
+    float* apre = wb + Wl.au;
+    float* spre = wb + Wl.su;
+    float* anet = wb + Wl.anet;
 #define CALL(HH, NN)                                                                                      \
   hipLaunchKernelGGL((argmax_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, mol_ptr, nf, h_data, \
                      noise, dequant_raw, adj_h, adj_ldj, apre, spre, anet)
@@ -1803,7 +1865,7 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     OuterBatch ob;
     ob.nd = 0;
     int wg = 0;
-    float* part = ws + Wl.part;
+    float* part = wb + Wl.part;
     add_desc(ob, wg, apre, H, H, h_data, nf, nf, nullptr, num_atoms, num_atoms, part, grad_dequant + rW1,
              grad_dequant + rb1);
     add_desc(ob, wg, anet, 2 * nf, 2 * nf, spre, H, H, nullptr, num_atoms, num_atoms, part, grad_dequant + rW2,

@@ -225,7 +225,8 @@ __global__ void __launch_bounds__(IDB) lg_idmap_kernel(LgArgs B) {
     base[s] += prefix + before;
     prefix += tot;
   }
-  if (tid == 0 && prefix < n) atomicOr(B.err, ENFLOW_ERR_FEW_IMAGES);
+  // prefix < n: columns q >= prefix keep id_mapping -1 (initialised above); the
+  // reference raises only if such a column has a hit (lg_pairs_kernel)
 #pragma unroll
   for (int s = 0; s < 27; ++s) {   // unrolled: cnt / base stay in registers
     int o = base[s];
@@ -308,11 +309,15 @@ __global__ void __launch_bounds__(BLOCK) lg_pairs_kernel(LgArgs B) {
         int c = 0, jl = -1;
         if (ql < qn) {
           jl = qid[ql];
-          if (jl != r0 + il && jl >= 0) {   // jl < 0 only with ENFLOW_ERR_FEW_IMAGES
+          if (jl != r0 + il) {   // self pair by label (base.py:139)
             const float qx = qp[ql * 3 + 0], qy = qp[ql * 3 + 1], qz = qp[ql * 3 + 2];
             for (int t = 0; t < ni; ++t) {   // wave-uniform trip count, broadcast LDS reads
               const float dx = img[w][t * 3 + 0] - qx, dy = img[w][t * 3 + 1] - qy, dz = img[w][t * 3 + 2] - qz;
               c += (dx * dx + dy * dy + dz * dz < r_sq) ? 1 : 0;
+            }
+            if (jl < 0 && c > 0) {   // a hit on column q past id_mapping: the reference's IndexError
+              atomicOr(B.err, ENFLOW_ERR_FEW_IMAGES);
+              c = 0;
             }
           }
         }

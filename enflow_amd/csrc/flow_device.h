@@ -881,7 +881,8 @@ __device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
         }
       }
     }
-    if (lane == 0 && prefix < n) sm.err |= ENFLOW_ERR_FEW_IMAGES;
+    // prefix < n: atom columns q >= prefix have no id_mapping entry (idmap -1);
+    // the reference raises only if such a column has a hit (block_counts)
   }
   __syncthreads();
 }
@@ -901,7 +902,7 @@ __device__ __forceinline__ void block_counts(S& sm, const MolRef& M, int tid, in
     const int il = e / n, q = e - il * n;
     const int i = r0 + il;
     const int jl = sm.idmap[q];
-    if (jl == i || jl < 0) continue;   // jl < 0 only with ENFLOW_ERR_FEW_IMAGES
+    if (jl == i) continue;             // self pair by label (base.py:139)
     const uint32_t mk = sm.mask27[i];
     const float px = sm.pos[i * 3 + 0], py = sm.pos[i * 3 + 1], pz = sm.pos[i * 3 + 2];
     const float qx = sm.pos[q * 3 + 0], qy = sm.pos[q * 3 + 1], qz = sm.pos[q * 3 + 2];
@@ -916,6 +917,10 @@ __device__ __forceinline__ void block_counts(S& sm, const MolRef& M, int tid, in
       if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
     }
     if (cnt) {
+      if (jl < 0) {                    // a hit on column q past id_mapping: the reference's
+        sm.err |= ENFLOW_ERR_FEW_IMAGES;   // IndexError (base.py:137)
+        continue;
+      }
       c_add(sm, il * n + jl, cnt);
       atomicAdd(&sm.cntrow[i], cnt);
     }

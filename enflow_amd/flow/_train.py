@@ -57,7 +57,10 @@ class _FlowFunction(torch.autograd.Function):
             ctx.dq_raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
                                     for p in flow.dequantize.parameters()])
         if meta["check_errors"]:
-            _lib.raise_on_err(err)
+            # no host sync here: the word is read at the next check -- the start of
+            # this graph's backward (before anything consumes the outputs' gradients),
+            # or the next forward -- so the host keeps queueing the loss and backward
+            _lib.defer_err(err)
         ctx.flow, ctx.meta, ctx.kind = flow, meta, kind
         ctx.n_params = len(params)
         ctx.save_for_backward(h_in, tape, counts)
@@ -66,6 +69,8 @@ class _FlowFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gh, gg, gpos, gvel, gldj):
         flow, meta, kind = ctx.flow, ctx.meta, ctx.kind
+        if meta["check_errors"]:
+            _lib.check_pending()          # the forward's deferred word (the reference's IndexError)
         h_in, tape, counts = ctx.saved_tensors
         hid, nf, cw = flow._geometry()
         dev = h_in.device

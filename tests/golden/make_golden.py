@@ -279,7 +279,32 @@ def case_train(hid, n_layers, sizes, seed, name, nf=5, flags=None):
     save(name, inp, res)
 
 
+def case_few_images():
+    """Fewer surviving periodic images than atoms (helpers.py:15-29 keeps only
+    images inside the box + r_cut ellipsoid).  The reference's Data.edges
+    (base.py:137) indexes id_mapping with the ATOM column q of every hit, so it
+    raises IndexError iff some hit has q >= len(id_mapping); without such a hit
+    it returns the (possibly empty) edge list.  Two single-molecule cases: one
+    that raises, one that does not."""
+    box = [3.0, 3.0, 3.0]
+    far = [[40.0 + i, 40.0, 40.0] for i in range(9)]
+    for tag, pos in (("raise", far + [[3.2, 0.1, 0.2]]), ("quiet", [[3.2, 0.1, 0.2]] + far)):
+        n = len(pos)
+        b = {"h": np.eye(5)[np.arange(n) % 5], "g": np.zeros((n, 5)), "pos": f32(pos), "vel": np.zeros((n, 3)),
+             "box": f32(np.tile(box, (n, 1))), "r_cut": f32([1.0]), "mol_ptr": np.array([0, n])}
+        d = ref_data(b)
+        try:
+            e = d.edges
+            out = {"raised": 0, "row": e.row.numpy(), "col": e.col.numpy()}
+        except IndexError:
+            out = {"raised": 1, "row": np.zeros(0, np.int64), "col": np.zeros(0, np.int64)}
+        save(f"edges_fewimg_{tag}", b, out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "fewimg":
+        case_few_images()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "train_variants":
         case_train(64, 2, [22, 40, 7], 41, "train_var_h64_L2", flags=[(False, True, True), (False, False, True)])
         case_train(32, 3, [22, 9, 15, 3], 42, "train_var_h32_L3",

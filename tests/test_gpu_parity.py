@@ -396,3 +396,41 @@ def test_bench_config_roundtrip(bench_run):
     # positions come back wrapped into the box (forward applies pbc each layer)
     dpos = O.apply_pbc(back.pos.cpu().numpy() - b["pos"], b["box"])
     assert np.max(np.abs(dpos)) < 1e-3 * np.max(np.abs(b["pos"]))
+
+
+@pytest.mark.parametrize("tag", ["raise", "quiet"])
+def test_few_images_error_semantics(tag):
+    """Fewer surviving periodic images than atoms: IndexError exactly when the
+    reference raises (a hit on an atom column past id_mapping, base.py:137),
+    from Data.edges and from the flow forward (its first layer); otherwise the
+    reference's (here empty) edge list.  Reference goldens edges_fewimg_*."""
+    from enflow_amd.data import Data
+    inp, out = load(f"edges_fewimg_{tag}")
+    d = data_from_fixture(inp, DEV)
+    model = _make_model(32, 5, 2, 3, 0.01)
+    if int(out["raised"]):
+        with pytest.raises(IndexError):
+            d.edges.row
+        with pytest.raises(IndexError), torch.no_grad():
+            model(data_from_fixture(inp, DEV))
+    else:
+        assert d.edges.row.numel() == out["row"].shape[0]
+        with torch.no_grad():
+            o, ldj = model(data_from_fixture(inp, DEV))
+        assert np.isfinite(float(ldj))
+
+
+def test_training_forward_defers_the_index_error_to_backward():
+    """Training: the forward queues its error word (no host sync); the
+    reference's IndexError surfaces when loss.backward() starts."""
+    from enflow_amd.flow import Alchemical_NLL
+    from enflow_amd import _lib
+    _lib.check_pending()
+    inp, _ = load("edges_fewimg_raise")
+    model = _make_model(32, 5, 2, 3, 0.01)
+    o, ldj = model(data_from_fixture(inp, DEV))            # grad enabled: training path, no raise
+    loss = Alchemical_NLL(kBT=1.0, softening=0.1)(o, ldj)
+    with pytest.raises(IndexError):
+        loss.backward()
+    _lib.check_pending()
+    assert not _lib._pending

@@ -101,3 +101,18 @@ def test_gradient_oracle_matches_reference_backward(name):
             np.testing.assert_allclose(v, out[f"grad_p{i}.{k}"], rtol=1e-9, atol=1e-12 * np.abs(out[f"grad_p{i}.{k}"]).max())
     for k, v in gd.items():
         np.testing.assert_allclose(v, out[f"grad_dq.{k}"], rtol=1e-9, atol=1e-12 * np.abs(out[f"grad_dq.{k}"]).max())
+
+
+@pytest.mark.parametrize("tag", ["raise", "quiet"])
+def test_oracle_few_images_matches_reference(tag):
+    """The reference raises IndexError only for a hit on an atom column past
+    id_mapping (base.py:137), not merely for fewer images than atoms."""
+    inp, out = load(f"edges_fewimg_{tag}")
+    pos, box = inp["pos"].astype(np.float64), inp["box"].astype(np.float64)
+    rc = float(inp["r_cut"][0])
+    if int(out["raised"]):
+        with pytest.raises(IndexError):
+            O.molecule_edges(pos, box[0], rc)
+    else:
+        e = O.molecule_edges(pos, box[0], rc)
+        assert e.shape[0] == out["row"].shape[0]
