@@ -282,6 +282,49 @@ __device__ __forceinline__ float silu_f(float x) {
 #endif
 }
 
+// silu of 4 independent values in lock-step (mul, exp, add, rcp, mul x 4): every
+// transcendental result is consumed 4 instructions later, so no s_nop pads the
+// trans-use hazard (the compiler's per-element chains got one after each exp /
+// rcp).  Same arithmetic as silu_f.
+#ifndef ENFLOW_SILU4_ASM
+#define ENFLOW_SILU4_ASM 1
+#endif
+__device__ __forceinline__ f32x4 silu4(f32x4 z) {
+#if ENFLOW_SILU4_ASM && !(ENFLOW_ABLATE & 8)
+  float t0, t1, t2, t3;
+  f32x4 y;
+  asm("v_mul_f32 %4, 0xbfb8aa3b, %8\n\t"
+      "v_mul_f32 %5, 0xbfb8aa3b, %9\n\t"
+      "v_mul_f32 %6, 0xbfb8aa3b, %10\n\t"
+      "v_mul_f32 %7, 0xbfb8aa3b, %11\n\t"
+      "v_exp_f32 %4, %4\n\t"
+      "v_exp_f32 %5, %5\n\t"
+      "v_exp_f32 %6, %6\n\t"
+      "v_exp_f32 %7, %7\n\t"
+      "v_add_f32 %4, 1.0, %4\n\t"
+      "v_add_f32 %5, 1.0, %5\n\t"
+      "v_add_f32 %6, 1.0, %6\n\t"
+      "v_add_f32 %7, 1.0, %7\n\t"
+      "v_rcp_f32 %4, %4\n\t"
+      "v_rcp_f32 %5, %5\n\t"
+      "v_rcp_f32 %6, %6\n\t"
+      "v_rcp_f32 %7, %7\n\t"
+      "v_mul_f32 %0, %8, %4\n\t"
+      "v_mul_f32 %1, %9, %5\n\t"
+      "v_mul_f32 %2, %10, %6\n\t"
+      "v_mul_f32 %3, %11, %7"
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+      : "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]));
+  return y;
+#else
+  return (f32x4){silu_f(z[0]), silu_f(z[1]), silu_f(z[2]), silu_f(z[3])};
+#endif
+}
+// silu(x * s + b), 4 lanes of a register quad
+__device__ __forceinline__ f32x4 silu4_fma(float x0, float x1, float x2, float x3, float s, f32x4 b) {
+  return silu4((f32x4){fmaf(x0, s, b[0]), fmaf(x1, s, b[1]), fmaf(x2, s, b[2]), fmaf(x3, s, b[3])});
+}
+
 __device__ __forceinline__ float pbc1(float x, float b) { return x - rintf(x / b) * b; }
 
 __device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
@@ -1156,8 +1199,10 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = silu_f(fmaf(x0[0][4 * g4 + u], inv0, b[u]));
+{
+        const f32x4 y = silu4_fma(x0[0][4 * g4], x0[0][4 * g4 + 1], x0[0][4 * g4 + 2], x0[0][4 * g4 + 3], inv0, b);
+        for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = y[u];
+      }
     }
     STAMP(10);
 
@@ -1169,16 +1214,20 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
         const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 32 * t + 8 * g4 + 4 * hh);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = silu_f(fmaf(x0[t][4 * g4 + u], inv0, b[u]));
+{
+          const f32x4 y = silu4_fma(x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3], inv0, b);
+          for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = y[u];
+        }
       }
     });
     STAMP(11);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 8 * g4 + 4 * hh);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = silu_f(fmaf(e[0][4 * g4 + u], inv1, b[u]));
+{
+        const f32x4 y = silu4_fma(e[0][4 * g4], e[0][4 * g4 + 1], e[0][4 * g4 + 2], e[0][4 * g4 + 3], inv1, b);
+        for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = y[u];
+      }
     }
     if (v_att) {   // egcl.py:60-62: out *= sigmoid(att_nn(out)); every tile activated first
 #pragma unroll
@@ -1238,8 +1287,11 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #endif
         if (t + 1 < NT && !v_att) {
           const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * (t + 1) + 8 * g4 + 4 * hh);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = silu_f(fmaf(e[t + 1][4 * g4 + u], inv1, b[u]));
+{
+            const f32x4 y = silu4_fma(e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
+                                      e[t + 1][4 * g4 + 3], inv1, b);
+            for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
+          }
         }
       });
       // coord_nn.2 as a per-pair dot
@@ -1249,8 +1301,11 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         for (int g4 = 0; g4 < 4; ++g4) {
           const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 2 * H + 32 * tp + 8 * g4 + 4 * hh);
           const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * tp + 8 * g4 + 4 * hh);
-#pragma unroll
-          for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(hc[tp][4 * g4 + u], inv2, b[u]));
+{
+            const f32x4 y = silu4_fma(hc[tp][4 * g4], hc[tp][4 * g4 + 1], hc[tp][4 * g4 + 2], hc[tp][4 * g4 + 3],
+                                      inv2, b);
+            for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
+          }
         }
     }
     float phi = part + __shfl_xor(part, 32, 64);
