@@ -62,6 +62,11 @@ SIGNATURES = {
     "enflow_lf_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                     _i, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p,
                                     _p, _i64, _i64, _p, _p]),
+    "enflow_egcl_backward_workspace_size": (_i64, [_i, _i, _i, _i, _i64]),
+    "enflow_egcl_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p,
+                                      _p, _p, _p, _p, _i64, _i64, _p, _p]),
+    "enflow_argmax_backward_workspace_size": (_i64, [_i, _i, _i]),
+    "enflow_argmax_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "enflow_timing_enable": (_i, [_i]),
     "enflow_timing_collect": (_i, []),
     "enflow_timing_entry": (_i, [_i, ctypes.c_char_p, _i, ctypes.POINTER(ctypes.c_double),

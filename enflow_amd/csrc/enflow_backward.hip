@@ -163,6 +163,12 @@ struct BwdArgs {
   float* aq;         // [A]    dQ                                    (DY of vel_scaling_nn.2)
   float* agr;        // [A][nf] dG                                   (DY of node_nn.2)
   int32_t* err;
+  // standalone EGCL.forward backward (enflow_egcl_backward_f32): adjoints of the
+  // network outputs Q [A], F [A][3], G [A][nf] given directly (NULL: the flow's
+  // leapfrog adjoint); the layer-input adjoints then start at zero
+  const float* eg_dQ;
+  const float* eg_dF;
+  const float* eg_dG;
 };
 
 // <= 80 KB at (H, NMAX) = (128, 64): two workgroups per CU.  The node-MLP
@@ -472,6 +478,21 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   STAMP(0);
   // ---- leapfrog adjoint (dynamics.py:13-21 in reverse order)
   const float aldj = B.adj_ldj[0];
+  if (B.eg_dQ) {   // EGCL.forward alone (egcl.py:76-92): d Q / d F / d G given
+    for (int a = tid; a < n; a += BLOCK) {
+      sb.aQ[a] = B.eg_dQ[a0 + a];
+      for (int d = 0; d < 3; ++d) {
+        sb.aF[a * 3 + d] = B.eg_dF[(size_t)(a0 + a) * 3 + d];
+        sb.apos[a * 3 + d] = 0.f;
+        sb.avel[a * 3 + d] = 0.f;
+      }
+      for (int q = 0; q < NFP; ++q) {
+        sb.aG[a * NFP + q] = q < nf ? B.eg_dG[(size_t)(a0 + a) * nf + q] : 0.f;
+        sb.ah[a * NFP + q] = 0.f;
+        sb.ag[a * NFP + q] = 0.f;
+      }
+    }
+  } else
   for (int a = tid; a < n; a += BLOCK) {
     const float eq = expf(sm.Q[a]);
     float s = 0.f;
@@ -1736,16 +1757,17 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
-int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
-                           const int32_t* mol_ptr, const float* r_cut, const float* box,
-                           const float* tape, const int32_t* pair_counts,
-                           const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
-                           int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
-                           float dt, float cw,
-                           float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
-                           float* grad_layers, float* grad_dequant,
-                           void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
-                           int32_t* err_flag, void* stream) {
+static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                            const int32_t* mol_ptr, const float* r_cut, const float* box,
+                            const float* tape, const int32_t* pair_counts,
+                            const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                            int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                            float dt, float cw,
+                            float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                            float* grad_layers, float* grad_dequant,
+                            void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                            int32_t* err_flag, void* stream,
+                            const float* eg_dQ, const float* eg_dF, const float* eg_dG) {
   // dequant_kind may carry ENFLOW_EGCL_VARIANTS: layers with norm_diff / tanh flags
   const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
   dequant_kind &= 0xff;
@@ -1799,6 +1821,7 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
     A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
     A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
+    A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
     if (variants) {
 #define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);
@@ -1877,6 +1900,107 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
                      (long long)n_layers * R.total_bwd, dequant_kind == ENFLOW_DEQUANT_ARGMAX ? grad_dequant : nullptr,
                      (long long)(H * nf + H + 2 * nf * H + 2 * nf));   // ArgMax.network: W1, b1, W2, b2
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                           const int32_t* mol_ptr, const float* r_cut, const float* box,
+                           const float* tape, const int32_t* pair_counts,
+                           const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                           int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                           float dt, float cw,
+                           float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                           float* grad_layers, float* grad_dequant,
+                           void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                           int32_t* err_flag, void* stream) {
+  return lf_backward_impl(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, tape, pair_counts, layers,
+                          layers_bwd, layers_raw, n_layers, dequant_kind, dequant_raw, h_data, noise, dt, cw, adj_h,
+                          adj_g, adj_pos, adj_vel, adj_ldj, grad_layers, grad_dequant, workspace, workspace_bytes,
+                          pair_row_bound, err_flag, stream, nullptr, nullptr, nullptr);
+}
+
+// ---- standalone EGCL.forward backward ------------------------------------
+// Workspace: the one-layer backward's, then scratch for the (unused) velocity /
+// g adjoints and a zero log|detJ| adjoint.
+static size_t egcl_bwd_extra(int num_atoms, int nf) {
+  return al64((size_t)num_atoms * 3) + al64((size_t)num_atoms * nf) + 64;
+}
+int64_t enflow_egcl_backward_workspace_size(int num_mols, int num_atoms, int nf, int H, int64_t pair_row_bound) {
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || pair_row_bound < 0) return -1;
+  return (int64_t)((bwd_ws(num_mols, num_atoms, nf, H, 1, pair_row_bound).total + egcl_bwd_extra(num_atoms, nf)) *
+                   sizeof(float));
+}
+
+int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* tape, const int32_t* pair_counts,
+                             const float* layer, const float* layer_bwd, const float* layer_raw, int egcl_flags,
+                             float cw, const float* adj_Q, const float* adj_F, const float* adj_G,
+                             float* adj_h, float* adj_pos, float* grad_layer,
+                             void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                             int32_t* err_flag, void* stream) {
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || pair_row_bound < 0) return -1;
+  if (!adj_Q || !adj_F || !adj_G || !workspace) return -1;
+  const BwdWs Wl = bwd_ws(num_mols, num_atoms, nf, H, 1, pair_row_bound);
+  if ((uint64_t)workspace_bytes < (Wl.total + egcl_bwd_extra(num_atoms, nf)) * sizeof(float)) return -6;
+  float* extra = reinterpret_cast<float*>(workspace) + Wl.total;
+  float* avel = extra;
+  float* ag = avel + al64((size_t)num_atoms * 3);
+  float* zero = ag + al64((size_t)num_atoms * nf);
+  if (hipMemsetAsync(zero, 0, 64 * sizeof(float), SB(stream)) != hipSuccess) return -2;
+  return lf_backward_impl(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, tape, pair_counts, layer,
+                          layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | (egcl_flags ? ENFLOW_EGCL_VARIANTS : 0),
+                          nullptr, nullptr, nullptr, 0.f, cw, adj_h, ag, adj_pos, avel, zero, grad_layer, nullptr,
+                          workspace, workspace_bytes, pair_row_bound, err_flag, stream, adj_Q, adj_F, adj_G);
+}
+
+// ---- standalone ArgMax.forward backward ------------------------------------
+struct AmBwdWs { size_t apre, spre, anet, part, total; };
+static AmBwdWs am_bwd_ws(int num_atoms, int nf, int H) {
+  AmBwdWs W;
+  size_t o = 0;
+  const size_t A = (size_t)num_atoms;
+  W.apre = o; o += al64(A * H);
+  W.spre = o; o += al64(A * H);
+  W.anet = o; o += al64(A * 2 * nf);
+  const size_t cha = (size_t)cdiv(num_atoms, OA_CHUNK_ATOM);
+  W.part = o; o += al64(cha * ((size_t)H * (nf + 1) + (size_t)2 * nf * (H + 1)));
+  W.total = o;
+  return W;
+}
+int64_t enflow_argmax_backward_workspace_size(int num_atoms, int nf, int H) {
+  if (num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H)) return -1;
+  return (int64_t)(am_bwd_ws(num_atoms, nf, H).total * sizeof(float));
+}
+
+int enflow_argmax_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                               const int32_t* mol_ptr, const float* h, const float* dequant_raw, const float* noise,
+                               const float* adj_z, const float* adj_log_q, float* grad_dequant,
+                               void* workspace, int64_t workspace_bytes, void* stream) {
+  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > NFMAX ||
+      !hid_ok_b(H))
+    return -1;
+  if (!mol_ptr || !h || !dequant_raw || !noise || !adj_z || !adj_log_q || !grad_dequant || !workspace) return -1;
+  const AmBwdWs W = am_bwd_ws(num_atoms, nf, H);
+  if ((uint64_t)workspace_bytes < W.total * sizeof(float)) return -6;
+  if (num_mols == 0) return 0;
+  hipStream_t st = SB(stream);
+  float* ws = reinterpret_cast<float*>(workspace);
+  float *apre = ws + W.apre, *spre = ws + W.spre, *anet = ws + W.anet;
+#define CALL(HH, NN)                                                                                      \
+  hipLaunchKernelGGL((argmax_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, mol_ptr, nf, h,      \
+                     noise, dequant_raw, adj_z, adj_log_q, apre, spre, anet)
+  DISPATCH_HN_B(H, max_mol_atoms, CALL);
+#undef CALL
+  const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
+  OuterBatch ob;
+  ob.nd = 0;
+  int wg = 0;
+  float* part = ws + W.part;
+  add_desc(ob, wg, apre, H, H, h, nf, nf, nullptr, num_atoms, num_atoms, part, grad_dequant + rW1,
+           grad_dequant + rb1);
+  add_desc(ob, wg, anet, 2 * nf, 2 * nf, spre, H, H, nullptr, num_atoms, num_atoms, part, grad_dequant + rW2,
+           grad_dequant + rb2);
+  return run_outer(ob, wg, st);
 }
 
 }  // extern "C"

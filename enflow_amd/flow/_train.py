@@ -235,3 +235,126 @@ class _NLLFunction(torch.autograd.Function):
             _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj), _lib.stream_ptr(dev)),
             "enflow_alchemical_nll_backward_f32")
         return None, None, ah, ag, apos, avel, aldj.reshape(())
+
+
+# ---------------------------------------------------------------------------
+# standalone modules: EGCL.forward (enflow/nn/egcl.py:76-92) and ArgMax.forward
+# (enflow/nn/argmax.py:13-25) as autograd Functions over the HIP backward
+# ---------------------------------------------------------------------------
+def layer_grads(net, flat):
+    """Split one layer's flat gradient (layers_raw layout: default-flag
+    parameters in named order, then att_nn.0 weight / bias in H + 1 slots) into
+    the module's parameters, in named_parameters() order."""
+    off = 0
+    slices = {}
+    for name, p in net.named_parameters():
+        if not name.startswith("att_nn."):
+            slices[name] = flat[off:off + p.numel()]
+            off += p.numel()
+    for name, p in net.named_parameters():
+        if name.startswith("att_nn."):
+            slices[name] = flat[off:off + p.numel()]
+            off += p.numel()
+    return [slices[name].view(p.shape).to(p.dtype) for name, p in net.named_parameters()]
+
+
+class _EGCLFunction(torch.autograd.Function):
+    """EGCL.forward with the HIP backward: outputs from enflow_egcl_forward_f32;
+    the backward regenerates the one-layer tape (message sums, pair counts) with
+    enflow_lf_forward_f32 and runs enflow_egcl_backward_f32."""
+
+    @staticmethod
+    def forward(ctx, net, meta, h, pos, *params):
+        q, f, g = net._infer(h.detach(), pos.detach(), meta)
+        ctx.net, ctx.meta = net, meta
+        ctx.save_for_backward(h.detach().to(torch.float32).contiguous(), pos.detach().to(torch.float32).contiguous())
+        return q, f, g
+
+    @staticmethod
+    def backward(ctx, gq, gf, gg):
+        net, meta = ctx.net, ctx.meta
+        h, pos = ctx.saved_tensors
+        if meta["max_n"] > _lib.TRAIN_MAX_ATOMS:
+            raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
+        L = _lib.lib()
+        dev = h.device
+        A, nf, hid = h.shape[0], net.input_nf, net.hidden_nf
+        M = meta["mol_ptr"].numel() - 1
+        st = _lib.stream_ptr(dev)
+        prec = _lib.PREC_F16X3 | (_lib.EGCL_VARIANTS if net.variant_flags() else 0)
+        # the one-layer tape: layer-input state, message sums, Q; pair counts
+        hw, pw = h.clone(), pos.clone()
+        gw = torch.zeros_like(h)
+        vw = torch.zeros_like(pos)
+        tape = torch.empty(max(L.enflow_lf_tape_size(A, nf, hid, 1), 1), dtype=torch.float32, device=dev)
+        counts = torch.zeros(max(M, 1), dtype=torch.int32, device=dev)
+        ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
+        ldj = torch.empty(1, dtype=torch.float32, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        fwd = net.packed(dev)
+        _lib.check(L.enflow_lf_forward_f32(
+            M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]), _lib.ptr(meta["box"]),
+            _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1, _lib.DEQUANT_NONE, None, None,
+            0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol), _lib.ptr(ldj), _lib.ptr(err), None, _lib.ptr(tape),
+            _lib.ptr(counts), prec, st), "enflow_lf_forward_f32 (EGCL tape)")
+        raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32) for p in net.raw_parameters()] +
+                        [net._att_raw(dev) if net.attention else torch.zeros(hid + 1, device=dev)])
+        bwd = torch.empty(max(L.enflow_egcl_bwd_packed_size(hid, nf), 1), dtype=torch.float32, device=dev)
+        _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw), hid, nf, _lib.ptr(bwd), st), "enflow_pack_egcl_bwd_f32")
+        prb = pair_row_bound(meta["N"])
+        wsb = L.enflow_egcl_backward_workspace_size(M, A, nf, hid, prb)
+        if wsb < 0:
+            raise _lib.HipPathError("enflow_egcl_backward_workspace_size rejected the batch")
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+
+        def adj(t, shape):
+            if t is None:
+                return torch.zeros(shape, dtype=torch.float32, device=dev)
+            return t.detach().to(dtype=torch.float32).reshape(shape).contiguous()
+
+        aq, af, ag = adj(gq, (A,)), adj(gf, (A, 3)), adj(gg, (A, nf))
+        dh = torch.empty((A, nf), dtype=torch.float32, device=dev)
+        dpos = torch.empty((A, 3), dtype=torch.float32, device=dev)
+        grad = torch.empty_like(raw)
+        _lib.check(L.enflow_egcl_backward_f32(
+            M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]), _lib.ptr(meta["box"]),
+            _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw), net.variant_flags(),
+            float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af), _lib.ptr(ag), _lib.ptr(dh), _lib.ptr(dpos),
+            _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err), st), "enflow_egcl_backward_f32")
+        _lib.raise_on_err(err)
+        return (None, None, dh, dpos) + tuple(layer_grads(net, grad))
+
+
+class _ArgMaxFunction(torch.autograd.Function):
+    """ArgMax.forward with the HIP backward (enflow_argmax_backward_f32)."""
+
+    @staticmethod
+    def forward(ctx, am, meta, h, noise, *params):
+        z, lq = am._infer(h.detach(), noise, meta)
+        ctx.am, ctx.meta = am, meta
+        ctx.save_for_backward(h.detach().to(torch.float32).contiguous(), noise)
+        return z, lq
+
+    @staticmethod
+    def backward(ctx, gz, glq):
+        am, meta = ctx.am, ctx.meta
+        h, noise = ctx.saved_tensors
+        L = _lib.lib()
+        dev = h.device
+        A, nf, hid = h.shape[0], am.node_nf, am.hidden_nf
+        raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32) for p in am.parameters()])
+        az = (torch.zeros_like(h) if gz is None else gz.detach().to(torch.float32).contiguous())
+        alq = (torch.zeros(1, device=dev) if glq is None else glq.detach().to(torch.float32).reshape(1).contiguous())
+        grad = torch.empty_like(raw)
+        wsb = L.enflow_argmax_backward_workspace_size(A, nf, hid)
+        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+        _lib.check(L.enflow_argmax_backward_f32(
+            meta["mol_ptr"].numel() - 1, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(h),
+            _lib.ptr(raw), _lib.ptr(noise), _lib.ptr(az), _lib.ptr(alq), _lib.ptr(grad), _lib.ptr(ws), wsb,
+            _lib.stream_ptr(dev)), "enflow_argmax_backward_f32")
+        grads, off = [], 0
+        for p in am.parameters():
+            grads.append(grad[off:off + p.numel()].view(p.shape).to(p.dtype))
+            off += p.numel()
+        # h is the categorical data (one-hot, argmax.py:13): no gradient is returned for it
+        return (None, None, None, None) + tuple(grads)

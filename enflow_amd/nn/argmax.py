@@ -35,37 +35,51 @@ class ArgMax(nn.Module):
         self._packed, self._packed_key = out, key
         return out
 
-    def forward(self, h, noise=None, N=None):
-        """``N``: atoms per molecule (defaults to one molecule holding every
-        atom; log_q is a batch scalar either way).  ``noise``: optional N(0,1)
-        draw of shape h.shape."""
-        _lib.require_gpu(h)
-        L = _lib.lib()
-        dev = h.device
-        n = h.shape[0]
+    def _meta(self, n, N, dev, cap):
+        """Molecule chunks of <= cap atoms (ArgMax is per atom; log_q is a sum)."""
         if N is None:
             N = torch.tensor([n])
         N = torch.as_tensor(N).reshape(-1)
-        # the kernel owns one molecule per workgroup (<= enflow_max_atoms): split
-        # a single big "molecule" into chunks -- log_q is a plain sum over atoms
-        cap = L.enflow_max_atoms()
-        if int(N.max()) > cap:
+        if N.numel() and int(N.max()) > cap:
             chunks = []
             for c in N.tolist():
                 chunks += [cap] * (c // cap) + ([c % cap] if c % cap else [])
             N = torch.tensor(chunks)
-        ptr = mol_ptr_from_counts(N, device=dev)
-        hf = h.detach().to(torch.float32).contiguous()
-        eps = (torch.randn(h.shape, device=dev, dtype=torch.float32) if noise is None
-               else noise.to(device=dev, dtype=torch.float32).contiguous())
+        return dict(mol_ptr=mol_ptr_from_counts(N, device=dev), max_n=int(N.max()) if N.numel() else 0,
+                    num_mols=N.numel())
+
+    def _infer(self, h, eps, meta):
+        L = _lib.lib()
+        dev = h.device
+        n = h.shape[0]
+        hf = h.to(torch.float32).contiguous()
         z = torch.empty_like(hf)
-        lq_mol = torch.empty(N.numel(), dtype=torch.float32, device=dev)
+        lq_mol = torch.empty(max(meta["num_mols"], 1), dtype=torch.float32, device=dev)
         lq = torch.empty(1, dtype=torch.float32, device=dev)
-        _lib.check(L.enflow_argmax_forward_f32(N.numel(), n, int(N.max()), self.node_nf, self.hidden_nf,
-                                               _lib.ptr(ptr), _lib.ptr(hf), _lib.ptr(self.packed(dev)),
+        _lib.check(L.enflow_argmax_forward_f32(meta["num_mols"], n, meta["max_n"], self.node_nf, self.hidden_nf,
+                                               _lib.ptr(meta["mol_ptr"]), _lib.ptr(hf), _lib.ptr(self.packed(dev)),
                                                _lib.ptr(eps), _lib.ptr(z), _lib.ptr(lq_mol), _lib.ptr(lq),
                                                _lib.stream_ptr(dev)), "enflow_argmax_forward_f32")
-        return z.to(h.dtype), lq.reshape(()).to(h.dtype)
+        return z, lq.reshape(())
+
+    def forward(self, h, noise=None, N=None):
+        """argmax.py:13-25.  ``N``: atoms per molecule (defaults to one molecule
+        holding every atom; log_q is a batch scalar either way).  ``noise``:
+        optional N(0,1) draw of shape h.shape.  Differentiable w.r.t. the
+        network parameters when autograd needs it (enflow_argmax_backward_f32);
+        h is categorical data and receives no gradient."""
+        _lib.require_gpu(h)
+        dev = h.device
+        eps = (torch.randn(h.shape, device=dev, dtype=torch.float32) if noise is None
+               else noise.to(device=dev, dtype=torch.float32).contiguous())
+        params = list(self.parameters())
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            from ..flow._train import _ArgMaxFunction
+            meta = self._meta(h.shape[0], N, dev, _lib.TRAIN_MAX_ATOMS)
+            z, lq = _ArgMaxFunction.apply(self, meta, h, eps, *params)
+        else:
+            z, lq = self._infer(h.detach(), eps, self._meta(h.shape[0], N, dev, _lib.lib().enflow_max_atoms()))
+        return z.to(h.dtype), lq.to(h.dtype)
 
     def reverse(self, z):
         return one_hot(torch.argmax(z, dim=-1), dtype=z.dtype)

@@ -7,8 +7,6 @@ state_dict loads unchanged and a given torch seed yields the same weights.
 enflow_egcl_forward_f32: neighbour list, per-edge MLP chain on MFMA and the
 segment reductions all run in one HIP kernel per molecule.
 """
-import warnings
-
 import torch
 from torch import nn
 
@@ -113,42 +111,56 @@ class EGCL(nn.Module):
         self._pack(raw, dst, device)
 
     # ------------------------------------------------------------------
-    def forward(self, h, edges):
-        if not isinstance(edges, Edges):
-            raise TypeError("EGCL.forward expects the Edges handle returned by Data.edges")
-        self._check_supported()
-        _lib.require_gpu(h)
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            warnings.warn("enflow_amd EGCL: a standalone EGCL.forward is not differentiable (the HIP "
-                          "backward runs fused inside LFIntegrator, which trains); outputs are detached",
-                          RuntimeWarning, stacklevel=2)
+    def _meta(self, edges, dev):
+        return dict(mol_ptr=edges.mol_ptr, max_n=edges.max_mol_atoms, N=edges.N, num_mols=edges.num_mols,
+                    box=edges.box.detach().to(device=dev, dtype=torch.float32).contiguous(),
+                    r_cut=torch.as_tensor(edges.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous())
+
+    def _infer(self, h, pos, meta):
+        """EGCL.forward on the HIP kernels: (Q [n, 1], F [n, 3], G [n, nf]) fp32."""
         L = _lib.lib()
         dev = h.device
         n = h.shape[0]
         nf = self.input_nf
-        hf = h.detach().to(torch.float32).contiguous()
-        pos = edges.pos.detach().to(torch.float32).contiguous()
-        box = edges.box.detach().to(torch.float32).contiguous()
-        rc = torch.as_tensor(edges.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous()
+        hf = h.to(torch.float32).contiguous()
+        pos = pos.to(torch.float32).contiguous()
         Q = torch.empty(n, dtype=torch.float32, device=dev)
         F = torch.empty((n, 3), dtype=torch.float32, device=dev)
         G = torch.empty((n, nf), dtype=torch.float32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
-        if _lib.is_large(edges.max_mol_atoms):   # past the fused kernels' LDS image
-            ws = _lib.large_workspace(edges.num_mols, n, edges.max_mol_atoms, nf, dev)
+        M, max_n = meta["num_mols"], meta["max_n"]
+        if _lib.is_large(max_n):   # past the fused kernels' LDS image
+            ws = _lib.large_workspace(M, n, max_n, nf, dev)
             prec = _lib.PREC_F32 | (_lib.EGCL_VARIANTS if self.variant_flags() else 0)
             _lib.check(L.enflow_egcl_forward_large_f32(
-                edges.num_mols, n, edges.max_mol_atoms, nf, self.hidden_nf, _lib.ptr(edges.mol_ptr),
-                _lib.ptr(rc), _lib.ptr(box), _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),
+                M, n, max_n, nf, self.hidden_nf, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),
                 float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F), _lib.ptr(G), _lib.ptr(err), prec,
                 _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)), "enflow_egcl_forward_large_f32")
-            _lib.raise_on_err(err)
-            return (Q.reshape(n, 1).to(h.dtype), F.to(h.dtype), G.to(h.dtype))
-        _lib.check(L.enflow_egcl_forward_f32(edges.num_mols, n, edges.max_mol_atoms, nf, self.hidden_nf,
-                                             _lib.ptr(edges.mol_ptr), _lib.ptr(rc), _lib.ptr(box),
-                                             _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),
-                                             float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F),
-                                             _lib.ptr(G), _lib.ptr(err), _lib.stream_ptr(dev)),
-                   "enflow_egcl_forward_f32")
+        else:
+            _lib.check(L.enflow_egcl_forward_f32(M, n, max_n, nf, self.hidden_nf, _lib.ptr(meta["mol_ptr"]),
+                                                 _lib.ptr(meta["r_cut"]), _lib.ptr(meta["box"]), _lib.ptr(hf),
+                                                 _lib.ptr(pos), _lib.ptr(self.packed(dev)),
+                                                 float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F), _lib.ptr(G),
+                                                 _lib.ptr(err), _lib.stream_ptr(dev)), "enflow_egcl_forward_f32")
         _lib.raise_on_err(err)
-        return (Q.reshape(n, 1).to(h.dtype), F.to(h.dtype), G.to(h.dtype))
+        return Q.reshape(n, 1), F, G
+
+    def forward(self, h, edges):
+        """egcl.py:76-92.  Differentiable (w.r.t. the parameters, h and, through
+        Edges.coord_diff, the positions) when autograd needs it: the backward is
+        the HIP layer backward in EGCL mode (enflow_egcl_backward_f32)."""
+        if not isinstance(edges, Edges):
+            raise TypeError("EGCL.forward expects the Edges handle returned by Data.edges")
+        self._check_supported()
+        _lib.require_gpu(h)
+        dev = h.device
+        meta = self._meta(edges, dev)
+        params = list(self.parameters())
+        if torch.is_grad_enabled() and (h.requires_grad or edges.pos.requires_grad or
+                                        any(p.requires_grad for p in params)):
+            from ..flow._train import _EGCLFunction
+            q, f, g = _EGCLFunction.apply(self, meta, h, edges.pos, *params)
+        else:
+            q, f, g = self._infer(h.detach(), edges.pos.detach(), meta)
+        return q.to(h.dtype), f.to(h.dtype), g.to(h.dtype)

@@ -313,6 +313,39 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
                            int32_t* err_flag, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Standalone module backward passes (the reference's EGCL and ArgMax are
+ * ordinary autograd modules, enflow/nn/egcl.py:76-92, enflow/nn/argmax.py:13-25).
+ * ---------------------------------------------------------------------- */
+
+/* EGCL.forward backward: given the adjoints of its outputs adj_Q [A],
+ * adj_F [A][3], adj_G [A][nf], writes adj_h [A][nf], adj_pos [A][3] (the
+ * gradient reaching h and, through Edges.coord_diff, the positions) and
+ * grad_layer (one layer in the layers_raw layout of enflow_lf_backward_f32).
+ * tape / pair_counts: written by a one-layer enflow_lf_forward_f32 on the same
+ * h / pos (dequant NONE, dt 0); layer / layer_bwd / layer_raw: that layer
+ * packed; egcl_flags: its ENFLOW_EGCL_* flags.  Molecules of <= 64 atoms. */
+int64_t enflow_egcl_backward_workspace_size(int num_mols, int num_atoms, int node_nf, int hidden_nf,
+                                            int64_t pair_row_bound);
+int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* tape, const int32_t* pair_counts,
+                             const float* layer, const float* layer_bwd, const float* layer_raw, int egcl_flags,
+                             float coords_weight, const float* adj_Q, const float* adj_F, const float* adj_G,
+                             float* adj_h, float* adj_pos, float* grad_layer,
+                             void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                             int32_t* err_flag, void* stream);
+
+/* ArgMax.forward backward: adjoints of z [A][nf] and of log_q [1] -> the
+ * gradient of ArgMax.network's parameters (grad_dequant, raw layout of
+ * enflow_pack_argmax_f32).  noise: the forward's N(0,1) draw; h: its input.
+ * mol_ptr chunks the atoms (<= 64 per chunk; ArgMax is per atom). */
+int64_t enflow_argmax_backward_workspace_size(int num_atoms, int node_nf, int hidden_nf);
+int enflow_argmax_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                               const int32_t* mol_ptr, const float* h, const float* dequant_raw, const float* noise,
+                               const float* adj_z, const float* adj_log_q, float* grad_dequant,
+                               void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Per-kernel timing (measurement only; no reference counterpart).  When
  * enabled, every kernel this library launches is bracketed by a hipEvent pair
  * on its own launch stream; collect() waits for the recorded events and adds

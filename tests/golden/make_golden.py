@@ -301,7 +301,63 @@ def case_few_images():
         save(f"edges_fewimg_{tag}", b, out)
 
 
+def case_egcl_grad(hid, seed, flags, name):
+    """A standalone EGCL.forward trained directly (the reference module is an
+    ordinary autograd module, egcl.py:76-92): loss = sum(Q wq) + sum(F wf) +
+    sum(G wg) with fixed random weights; gradients of every parameter, of h and
+    of the positions (through Edges.coord_diff)."""
+    torch.manual_seed(seed)
+    nf = 5
+    att, nd, th = flags
+    net = EGCL(nf, nf, hid, attention=att, norm_diff=nd, tanh=th).double()
+    b = batch_inputs(4, [22, 9, 15, 3], nf, seed=seed, one_hot=False)
+    d = ref_data(b)
+    rng = np.random.default_rng(seed + 5)
+    n = d.h.shape[0]
+    wq, wf, wg = (f32(rng.normal(size=s_)) for s_ in ((n, 1), (n, 3), (n, nf)))
+    d.h.requires_grad_(True)
+    d.pos.requires_grad_(True)
+    q, f, g = net(d.h, d.edges)
+    loss = (q * to_t(wq)).sum() + (f * to_t(wf)).sum() + (g * to_t(wg)).sum()
+    loss.backward()
+    inp = dict(b)
+    inp.update(params_of(net, "p0."))
+    inp["p0.flags"] = np.array(flags, dtype=np.int32)
+    inp.update({"wq": wq, "wf": wf, "wg": wg})
+    res = {"loss": float(loss), "grad_h": d.h.grad.numpy(), "grad_pos": d.pos.grad.numpy()}
+    res.update({f"grad_p0.{k}": v.grad.numpy() for k, v in net.named_parameters()})
+    save(name, inp, res)
+
+
+def case_argmax_grad(hid, seed):
+    """A standalone ArgMax.forward (argmax.py:13-25) trained directly: loss =
+    sum(z wz) + 0.7 log_q; gradients of the network parameters."""
+    torch.manual_seed(seed)
+    nf = 5
+    am = ArgMax(nf, hid).double()
+    b = batch_inputs(3, [22, 9, 15], nf, seed=seed)
+    h = to_t(b["h"])
+    torch.manual_seed(seed + 1)
+    z, log_q = am(h)
+    torch.manual_seed(seed + 1)
+    eps = torch.randn(h.size())
+    wz = f32(np.random.default_rng(seed + 2).normal(size=tuple(h.shape)))
+    loss = (z * to_t(wz)).sum() + 0.7 * log_q
+    loss.backward()
+    inp = {"h": b["h"], "mol_ptr": b["mol_ptr"], "eps": eps.numpy(), "wz": wz}
+    inp.update(params_of(am, "dq."))
+    res = {"loss": float(loss)}
+    res.update({f"grad_dq.{k}": v.grad.numpy() for k, v in am.named_parameters()})
+    save(f"argmax_grad_h{hid}", inp, res)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "module_grads":
+        case_egcl_grad(32, 51, (False, False, False), "egcl_grad_h32")
+        case_egcl_grad(128, 52, (False, False, False), "egcl_grad_h128")
+        case_egcl_grad(64, 53, (True, True, True), "egcl_grad_h64_all")
+        case_argmax_grad(32, 54)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "fewimg":
         case_few_images()
         sys.exit(0)

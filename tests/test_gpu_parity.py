@@ -84,9 +84,9 @@ def test_argmax_matches_reference():
     am = am.to(DEV)
     h = torch.tensor(inp["h"], device=DEV)
     z, lq = am(h, noise=torch.tensor(inp["eps"], device=DEV), N=np.diff(inp["mol_ptr"]))
-    assert rel_err(z.cpu().numpy(), out["z"]) < TOL
+    assert rel_err(z.detach().cpu().numpy(), out["z"]) < TOL
     assert abs(float(lq) - float(out["log_q"])) <= TOL * abs(float(out["log_q"]))
-    np.testing.assert_array_equal(am.reverse(z).cpu().numpy(), out["reverse"])
+    np.testing.assert_array_equal(am.reverse(z.detach()).cpu().numpy(), out["reverse"])
 
 
 # ---------------------------------------------------------------------------
