@@ -655,17 +655,18 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
       if constexpr (PREC == PREC_F16X3) {
-        const int ks_n = (2 * nf + 1 + 15) >> 4;
-        for (int ks = 0; ks < ks_n; ++ks) {
+        const int ks_n = gemm0_ksteps(nf);
+        for (int ks = 0; ks < ks_n; ++ks) {   // k order gemm0_col (as the forward)
           f32x16 in;
+          if (ks == 0) {
+            const float* hrow = &sm.h[(hh ? jl : i) * NFP];   // rows zero-padded past nf
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) {
-            const int k = 16 * ks + 8 * hh + jj;
-            float v = 0.f;
-            if (k < nf) v = sm.h[i * NFP + k];
-            else if (k < 2 * nf) v = sm.h[jl * NFP + k - nf];
-            else if (k == 2 * nf) v = radial;
-            in[jj] = v;
+            for (int jj = 0; jj < 8; ++jj) in[jj] = hrow[jj];
+            if (hh && nf <= 7) in[7] = radial;
+          } else {
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) in[jj] = 0.f;
+            if (hh == 0) in[0] = radial;
           }
           f16x8 bh, bl;
           split_f16(in, 0, bh, bl);

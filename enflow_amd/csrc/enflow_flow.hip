@@ -99,8 +99,8 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
       const int row = 32 * t + (lane & 31);
       uint32_t bits = 0;
       for (int q = 0; q < 2; ++q) {
-        const int k = 16 * ks + 8 * (lane >> 5) + 2 * (d & 3) + q;
-        const float w = k < K1 ? raw[R.We1 + row * K1 + k] * sc : 0.f;
+        const int k = gemm0_col(ks, 8 * (lane >> 5) + 2 * (d & 3) + q, nf);
+        const float w = k >= 0 ? raw[R.We1 + row * K1 + k] * sc : 0.f;
         const _Float16 hi = (_Float16)w;
         const _Float16 part = d < 4 ? hi : (_Float16)(w - (float)hi);
         bits |= (uint32_t)__builtin_bit_cast(uint16_t, part) << (16 * q);

@@ -100,6 +100,21 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   return L;
 }
 
+// F16X3 edge_nn.0 (GEMM0) k order, chosen so each lane half reads ONE atom's
+// zero-padded feature row: k-slice 0 = [h_i[0..7] | h_j[0..6], radial] for
+// nf <= 7 ([.., h_j[7]] for nf == 8), k-slice 1 (nf == 8 only) = [radial, 0..].
+// Returns the raw edge_nn.0 input column of (k-slice ks, k = 8 half + slot), or -1.
+__host__ __device__ inline int gemm0_col(int ks, int kk, int nf) {
+  const int half = kk >> 3, s = kk & 7;
+  if (ks == 0) {
+    if (half == 0) return s < nf ? s : -1;
+    if (s < 7) return s < nf ? nf + s : -1;
+    return nf <= 7 ? 2 * nf : nf + 7;
+  }
+  return (nf == 8 && kk == 0) ? 2 * nf : -1;
+}
+__host__ __device__ inline int gemm0_ksteps(int nf) { return nf == 8 ? 2 : 1; }
+
 struct RawEgcl {  // offsets into the raw (torch) concatenation
   int We1, be1, We2, be2, Wn1, bn1, Wn2, bn2, Wc1, bc1, wc2, Wv1, bv1, Wv2, bv2, total;
   // training backward (layers_raw / grad_layers): att_nn.0.weight, att_nn.0.bias
@@ -1059,7 +1074,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   }
   if constexpr (PREC != PREC_F32 && Smem<H, NMAX, RB>::W1X_LDS) {   // GEMM0 is F16X3 in bf16 mode too
     // edge_nn.0 split fragments: one L2 pass per layer instead of one per tile
-    const int ks_n = (2 * nf + 1 + 15) >> 4;
+    const int ks_n = gemm0_ksteps(nf);
     for (int e = tid; e < NT * ks_n * 128; e += BLOCK) {   // 128 x 16 B per (t, ks)
       const int blk = e >> 7, r = e & 127, ln = r >> 1, part = r & 1;
       const int t = blk / ks_n, ks = blk - t * ks_n;
@@ -1134,18 +1149,24 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
     if constexpr (PREC != PREC_F32) {   // F16X3 (bf16 mode too: a 16-wide k-step on the matrix cores
       // beats 9 f32 k-steps; only edge_nn.2 / coord_nn.0 run in bf16)
-      // k = raw column of edge_nn.0: [h_i (nf), h_j (nf), radial], 16 per k-step
-      const int ks_n = (2 * nf + 1 + 15) >> 4;
+      // k order gemm0_col: lane half 0 = h_i's padded row, half 1 = h_j's (+ radial)
+      const int ks_n = gemm0_ksteps(nf);
       for (int ks = 0; ks < ks_n; ++ks) {
         f32x16 in;
+        if (ks == 0) {
+          if constexpr (BIG) {
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const int k = 16 * ks + 8 * hh + jj;
-          float v = 0.f;
-          if (k < nf) v = sm.h[i * NFP + k];
-          else if (k < 2 * nf) v = chf(k - nf);
-          else if (k == 2 * nf) v = radial;
-          in[jj] = v;
+            for (int jj = 0; jj < 8; ++jj) in[jj] = hh ? (jj < nf ? chf(jj) : 0.f) : sm.h[i * NFP + jj];
+          } else {
+            const float* hrow = &sm.h[(hh ? jl : i) * NFP];   // rows zero-padded past nf
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) in[jj] = hrow[jj];
+          }
+          if (hh && nf <= 7) in[7] = radial;
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) in[jj] = 0.f;
+          if (hh == 0) in[0] = radial;
         }
         f16x8 bh, bl;
         split_f16(in, 0, bh, bl);
@@ -1576,14 +1597,22 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
 template <int H, int NMAX, int RB>
 __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const float* __restrict__ noise,
                                 int a0, int n, int nf) {
+  using S = Smem<H, NMAX, RB>;
   constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
-  constexpr int ACT = H + 1;            // hidden activations staged in agg (free before layer 0)
-  static_assert(Smem<H, NMAX, RB>::AST >= ACT, "agg too small for the ArgMax activations");
+  // hidden activations staged in agg (free before layer 0); 16-B aligned rows
+  constexpr int ACT = S::AST % 4 == 0 ? S::AST : H + 1;
+  static_assert(S::AST >= ACT && ACT >= H, "agg too small for the ArgMax activations");
   float* const act = sm.agg;
   const AmLayout L = argmax_layout(H, nf);
   const int tid = threadIdx.x;
   float* net = sm.u.net;
   float lq = 0.f;
+  // network.2.weight staged in the (still unused) edge_nn.0 fragment buffer: the
+  // output loop then reads both operands as float4 from LDS
+  constexpr bool WLDS = S::W1X_LDS && ACT % 4 == 0 && sizeof(sm.w1x) >= sizeof(float) * 2 * NFMAX * H;
+  if constexpr (WLDS) {
+    for (int e = tid; e < 2 * nf * H / 4; e += BLOCK) st4(&sm.w1x[4 * e], ld4(Dp + L.wa2 + 4 * e));
+  }
   for (int c0 = 0; c0 < n; c0 += RB) {   // atoms in chunks of RB (the agg image)
     const int cn = min(RB, n - c0);
     {
@@ -1602,8 +1631,18 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
     for (int e = tid; e < cn * 2 * nf; e += BLOCK) {
       const int a = e / (2 * nf), o = e - a * 2 * nf;
       float s = Dp[L.ba2 + o];
-      const float* wr = Dp + L.wa2 + o * H;
-      for (int k = 0; k < H; ++k) s += wr[k] * act[a * ACT + k];
+      if constexpr (WLDS) {
+        f32x4 acc4 = (f32x4)0.f;
+#pragma unroll 8
+        for (int k = 0; k < H; k += 4) {
+          const f32x4 w4 = ld4(&sm.w1x[o * H + k]), x4 = ld4(&act[a * ACT + k]);
+          acc4 += w4 * x4;
+        }
+        s += (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+      } else {
+        const float* wr = Dp + L.wa2 + o * H;
+        for (int k = 0; k < H; ++k) s += wr[k] * act[a * ACT + k];
+      }
       net[a * 2 * NFMAX + o] = s;          // chunk-local rows
     }
     __syncthreads();
