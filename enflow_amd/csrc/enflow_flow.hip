@@ -261,6 +261,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       __syncthreads();
     }
     if (!(ENFLOW_ABLATE & 1) || it == 0) build_images(sm, Ml, tid_l);
+    STAMP(3);
     int npairs_layer = 0;
     auto block_pass = [&](const int r0, const int rb) {
       int tot;
@@ -279,7 +280,6 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
         atomicAdd(&A.stats[0], (unsigned long long)tot);
         atomicAdd(&A.stats[1], edges);
       }
-      STAMP(3);
       edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS);
       if constexpr (BLOCKED) {   // blocks with more pairs than the buffer: further passes
         constexpr int PC = Smem<H, NMAX, RB>::PC;

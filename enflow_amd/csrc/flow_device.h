@@ -844,6 +844,12 @@ struct Smem {
   alignas(16) float head[BWD ? 1 : WAVES][BWD ? 1 : H + 4];
   uint32_t pairs[PC];
   uint32_t mask27[NMAX];
+  // <= 32-atom images: the surviving periodic images that can reach the
+  // molecule's bounding box within r_cut (bit s of near27[a]), their positions
+  // imgp[a][s] kept in the edge_nn.0 fragment buffer (free during the pair build)
+  static constexpr bool IMG_LDS = W1X_LDS && NT * 2 * 512 >= NMAX * 27 * 4;
+  uint32_t near27[IMG_LDS ? NMAX : 1];
+  float bbox[8];
   int idmap[NMAX];
   int cntrow[NMAX];
   int headrow[WAVES];
@@ -895,17 +901,47 @@ __device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
     sm.mask27[a] = 0u;
     sm.idmap[a] = -1;
     sm.cntrow[a] = 0;
+    if constexpr (S::IMG_LDS) sm.near27[a] = 0u;
+  }
+  if constexpr (S::IMG_LDS) {   // the molecule's bounding box (n <= 32: one wave)
+    if (tid < 64) {
+      float lo[3], hi[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        const float x = tid < n ? sm.pos[tid * 3 + d] : sm.pos[d];
+        hi[d] = wave_max(x);
+        lo[d] = -wave_max(-x);
+      }
+      if (tid < 3) {
+        sm.bbox[tid] = tid == 0 ? lo[0] : (tid == 1 ? lo[1] : lo[2]);
+        sm.bbox[4 + tid] = tid == 0 ? hi[0] : (tid == 1 ? hi[1] : hi[2]);
+      }
+    }
   }
   __syncthreads();
   // (a) image masks, one (atom, image) per thread: bit s <=> image s of atom a
   //     lies in the ellipsoid with radii box + r_cut (helpers.py:17-22)
+  const float r_sq = M.rc * M.rc;
   for (int e = tid; e < n * 27; e += BLOCK) {
     const int a = e / 27, s = e - a * 27;
     const float ix = sm.pos[a * 3 + 0] + shift_of(s % 3, M.bx);
     const float iy = sm.pos[a * 3 + 1] + shift_of((s / 3) % 3, M.by);
     const float iz = sm.pos[a * 3 + 2] + shift_of(s / 9, M.bz);
     const float sx = ix / rx, sy = iy / ry, sz = iz / rz;
-    if (sx * sx + sy * sy + sz * sz <= 1.0f) atomicOr(&sm.mask27[a], 1u << s);
+    if (sx * sx + sy * sy + sz * sz <= 1.0f) {
+      atomicOr(&sm.mask27[a], 1u << s);
+      if constexpr (S::IMG_LDS) {
+        // farther than r_cut from the bounding box (1e-4 relative margin over fp32
+        // rounding) no atom can be hit: the image is skipped by the distance tests
+        const float ex = fmaxf(fmaxf(sm.bbox[0] - ix, ix - sm.bbox[4]), 0.f);
+        const float ey = fmaxf(fmaxf(sm.bbox[1] - iy, iy - sm.bbox[5]), 0.f);
+        const float ez = fmaxf(fmaxf(sm.bbox[2] - iz, iz - sm.bbox[6]), 0.f);
+        if (ex * ex + ey * ey + ez * ez <= r_sq * 1.0001f) {
+          atomicOr(&sm.near27[a], 1u << s);
+          st4(&sm.w1x[(a * 27 + s) * 4], (f32x4){ix, iy, iz, 0.f});
+        }
+      }
+    }
   }
   __syncthreads();
   // (b) id_mapping[q] for q < n: the q-th surviving image in (image, atom) order (helpers.py:25-27)
@@ -961,18 +997,29 @@ __device__ __forceinline__ void block_counts(S& sm, const MolRef& M, int tid, in
     const int i = r0 + il;
     const int jl = sm.idmap[q];
     if (jl == i) continue;             // self pair by label (base.py:139)
-    const uint32_t mk = sm.mask27[i];
-    const float px = sm.pos[i * 3 + 0], py = sm.pos[i * 3 + 1], pz = sm.pos[i * 3 + 2];
     const float qx = sm.pos[q * 3 + 0], qy = sm.pos[q * 3 + 1], qz = sm.pos[q * 3 + 2];
     int cnt = 0;
-    uint32_t bits = mk;
-    while (bits) {
-      const int s = __builtin_ctz(bits);
-      bits &= bits - 1;
-      const float ix = px + shift_of(s % 3, M.bx), iy = py + shift_of((s / 3) % 3, M.by),
-                  iz = pz + shift_of(s / 9, M.bz);
-      const float dx = ix - qx, dy = iy - qy, dz = iz - qz;
-      if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
+    if constexpr (S::IMG_LDS) {   // the row's near images, positions precomputed (same fp32 values)
+      uint32_t bits = sm.near27[i];
+      const float* img = &sm.w1x[i * 27 * 4];
+      while (bits) {
+        const int s = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const f32x4 im = ld4(img + 4 * s);
+        const float dx = im[0] - qx, dy = im[1] - qy, dz = im[2] - qz;
+        if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
+      }
+    } else {
+      const float px = sm.pos[i * 3 + 0], py = sm.pos[i * 3 + 1], pz = sm.pos[i * 3 + 2];
+      uint32_t bits = sm.mask27[i];
+      while (bits) {
+        const int s = __builtin_ctz(bits);
+        bits &= bits - 1;
+        const float ix = px + shift_of(s % 3, M.bx), iy = py + shift_of((s / 3) % 3, M.by),
+                    iz = pz + shift_of(s / 9, M.bz);
+        const float dx = ix - qx, dy = iy - qy, dz = iz - qz;
+        if (dx * dx + dy * dy + dz * dz < r_sq) ++cnt;
+      }
     }
     if (cnt) {
       if (jl < 0) {                    // a hit on column q past id_mapping: the reference's

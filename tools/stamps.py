@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "enflow_amd", "libenflow_hip_stamps.so")
-PHASES = ["load", "dequant", "pairs", "-", "edge_tiles(all)", "node", "update", "writeback",
+PHASES = ["load", "dequant", "pairs:counts+compact", "pairs:images+idmap", "edge_tiles(all)", "node", "update", "writeback",
           "  tiles:setup", "  gemm0", "  silu0", "  gemm1", "  silu1", "  segsum", "  gemm2+phi+force", "  tail-barrier"]
 
 
