@@ -922,25 +922,39 @@ __device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
   // (a) image masks, one (atom, image) per thread: bit s <=> image s of atom a
   //     lies in the ellipsoid with radii box + r_cut (helpers.py:17-22)
   const float r_sq = M.rc * M.rc;
-  for (int e = tid; e < n * 27; e += BLOCK) {
-    const int a = e / 27, s = e - a * 27;
-    const float ix = sm.pos[a * 3 + 0] + shift_of(s % 3, M.bx);
-    const float iy = sm.pos[a * 3 + 1] + shift_of((s / 3) % 3, M.by);
-    const float iz = sm.pos[a * 3 + 2] + shift_of(s / 9, M.bz);
-    const float sx = ix / rx, sy = iy / ry, sz = iz / rz;
-    if (sx * sx + sy * sy + sz * sz <= 1.0f) {
-      atomicOr(&sm.mask27[a], 1u << s);
-      if constexpr (S::IMG_LDS) {
-        // farther than r_cut from the bounding box (1e-4 relative margin over fp32
-        // rounding) no atom can be hit: the image is skipped by the distance tests
-        const float ex = fmaxf(fmaxf(sm.bbox[0] - ix, ix - sm.bbox[4]), 0.f);
-        const float ey = fmaxf(fmaxf(sm.bbox[1] - iy, iy - sm.bbox[5]), 0.f);
-        const float ez = fmaxf(fmaxf(sm.bbox[2] - iz, iz - sm.bbox[6]), 0.f);
-        if (ex * ex + ey * ey + ez * ez <= r_sq * 1.0001f) {
-          atomicOr(&sm.near27[a], 1u << s);
-          st4(&sm.w1x[(a * 27 + s) * 4], (f32x4){ix, iy, iz, 0.f});
+  //     one (atom, y/z shift) per thread, its three x shifts in registers
+  for (int e = tid; e < n * 9; e += BLOCK) {
+    const int a = e / 9, yz = e - a * 9;
+    const float iy = sm.pos[a * 3 + 1] + shift_of(yz % 3, M.by);
+    const float iz = sm.pos[a * 3 + 2] + shift_of(yz / 3, M.bz);
+    const float sy = iy / ry, sz = iz / rz;
+    float ey = 0.f, ez = 0.f;
+    if constexpr (S::IMG_LDS) {
+      ey = fmaxf(fmaxf(sm.bbox[1] - iy, iy - sm.bbox[5]), 0.f);
+      ez = fmaxf(fmaxf(sm.bbox[2] - iz, iz - sm.bbox[6]), 0.f);
+    }
+    uint32_t mk = 0u, nr = 0u;
+#pragma unroll
+    for (int xs = 0; xs < 3; ++xs) {
+      const int s = xs + 3 * yz;
+      const float ix = sm.pos[a * 3 + 0] + shift_of(xs, M.bx);
+      const float sx = ix / rx;
+      if (sx * sx + sy * sy + sz * sz <= 1.0f) {
+        mk |= 1u << s;
+        if constexpr (S::IMG_LDS) {
+          // farther than r_cut from the bounding box (1e-4 relative margin over fp32
+          // rounding) no atom can be hit: the image is skipped by the distance tests
+          const float ex = fmaxf(fmaxf(sm.bbox[0] - ix, ix - sm.bbox[4]), 0.f);
+          if (ex * ex + ey * ey + ez * ez <= r_sq * 1.0001f) {
+            nr |= 1u << s;
+            st4(&sm.w1x[(a * 27 + s) * 4], (f32x4){ix, iy, iz, 0.f});
+          }
         }
       }
+    }
+    if (mk) atomicOr(&sm.mask27[a], mk);
+    if constexpr (S::IMG_LDS) {
+      if (nr) atomicOr(&sm.near27[a], nr);
     }
   }
   __syncthreads();
@@ -1527,7 +1541,9 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
   const int vo = lane * 32;
   // every fragment of the wave's first item is requested before the bias
   // staging barrier, so the L2 round trips overlap instead of serialising
-  f32x4 vh, vl, nh, nl, gfh[2], gfl[2], ah[3], al[3];
+  // every fragment of an item is requested up front (the node phase runs outside
+  // the tile loop's register budget): one L2 round trip per item, not one per k-step
+  f32x4 vh, vl, nh, nl, gfh[2], gfl[2], ah[KS], al[KS];
   auto issue = [&](int it) {
     const int tp = it % NT;
     vh = bload4(W, vo, (L.wv1x + tp * 512) * 4);
@@ -1540,7 +1556,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
       gfl[s2] = bload4(W, vo + 16, (L.wn2x + (tp * 2 + s2) * 512) * 4);
     }
 #pragma unroll
-    for (int d = 0; d < 2; ++d) {
+    for (int d = 0; d < KS; ++d) {
       ah[d] = bload4(W, vo, (L.wn1ax + (tp * KS + d) * 512) * 4);
       al[d] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + d) * 512) * 4);
     }
@@ -1590,10 +1606,6 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     const float* arow = &sm.agg[ac * AST];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      if (ks + 2 < KS) {
-        ah[(ks + 2) % 3] = bload4(W, vo, (L.wn1ax + (tp * KS + ks + 2) * 512) * 4);
-        al[(ks + 2) % 3] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + ks + 2) * 512) * 4);
-      }
       f32x16 av;
       {   // two ds_read_b128 (rows 16-B aligned, AST % 4 == 0); invalid atoms read row 0, zeroed
         static_assert(AST % 4 == 0, "node phase reads agg rows as float4");
@@ -1606,9 +1618,9 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
       }
       f16x8 bh, bl;
       split_f16(av, 0, bh, bl);
-      acc = mfma_f16(ah[ks % 3], bh, acc);
-      acc = mfma_f16(ah[ks % 3], bl, acc);
-      acc = mfma_f16(al[ks % 3], bh, acc);
+      acc = mfma_f16(ah[ks], bh, acc);
+      acc = mfma_f16(ah[ks], bl, acc);
+      acc = mfma_f16(al[ks], bh, acc);
     }
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
