@@ -40,7 +40,7 @@ SIGNATURES = {
                                    _i, _f, _f, _p, _p, _p, _i, _p]),
     "enflow_lf_large_workspace_size": (_i64, [_i, _i, _i, _i]),
     "enflow_lf_forward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
-                                         _i, _p, _p, _f, _f, _f, _p, _p, _p, _i, _p, _i64, _p]),
+                                         _i, _p, _p, _f, _f, _f, _p, _p, _p, _i, _p, _p, _p, _i64, _p]),
     "enflow_lf_reverse_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                          _i, _f, _f, _p, _p, _p, _i, _p, _i64, _p]),
     "enflow_egcl_forward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f,
@@ -62,6 +62,10 @@ SIGNATURES = {
     "enflow_lf_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                     _i, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p,
                                     _p, _i64, _i64, _p, _p]),
+    "enflow_lf_backward_large_workspace_size": (_i64, [_i, _i, _i, _i, _i, _i64]),
+    "enflow_lf_backward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _i,
+                                          _i, _p, _p, _p, _f, _f, _p, _p, _p, _p, _p, _p, _p,
+                                          _p, _i64, _i64, _p, _p]),
     "enflow_egcl_backward_workspace_size": (_i64, [_i, _i, _i, _i, _i64]),
     "enflow_egcl_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p,
                                       _p, _p, _p, _p, _i64, _i64, _p, _p]),
@@ -118,9 +122,12 @@ def require_gpu(t):
                            "(there is no CPU fallback)")
 
 
-TRAIN_MAX_ATOMS = 64      # the HIP backward keeps whole-molecule pair lists in LDS
-LARGE_TRAIN_MSG = (f"the HIP training backward handles molecules of <= {TRAIN_MAX_ATOMS} atoms; larger systems "
-                   "run forward / reverse / EGCL only")
+# the fused training backward keeps whole-molecule pair lists in LDS up to this
+# size; batches with larger molecules train through the large-system kernels
+# (enflow_lf_forward_large_f32 with a tape, enflow_lf_backward_large_f32)
+TRAIN_MAX_ATOMS = 64
+LARGE_TRAIN_MSG = (f"the standalone EGCL backward handles molecules of <= {TRAIN_MAX_ATOMS} atoms (the flow "
+                   "trains any size)")
 _large_ws = {}
 
 

@@ -13,7 +13,7 @@ ARCH = os.environ.get("ENFLOW_OFFLOAD_ARCH", "gfx950")
 
 def build(force=False, verbose=False, out=OUT, defines=()):
     """defines: extra -D flags (A/B and ablation variants built to another `out`)."""
-    deps = SRCS + [os.path.join(CSRC, "flow_device.h"), os.path.join(CSRC, "enflow_timing.h"),
+    deps = SRCS + [os.path.join(CSRC, "flow_device.h"), os.path.join(CSRC, "enflow_timing.h"), os.path.join(CSRC, "enflow_large.h"),
                    os.path.join(ROOT, "include", "enflow_hip.h")]
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
@@ -26,7 +26,7 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     stamp = out + ".flags"
     flags = " ".join(base)
     same_flags = os.path.exists(stamp) and open(stamp).read() == flags
-    hdrs = [os.path.join(CSRC, "flow_device.h"), os.path.join(CSRC, "enflow_timing.h"),
+    hdrs = [os.path.join(CSRC, "flow_device.h"), os.path.join(CSRC, "enflow_timing.h"), os.path.join(CSRC, "enflow_large.h"),
             os.path.join(ROOT, "include", "enflow_hip.h")]
     procs = []
     for src, obj in zip(SRCS, objs):

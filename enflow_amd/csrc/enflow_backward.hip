@@ -24,7 +24,7 @@
 // All arithmetic is float32.
 
 #define ENFLOW_BACKWARD_TU   // -DENFLOW_STAMPS_BWD stamps this file's kernels only (tools/stamps_bwd.py)
-#include "flow_device.h"
+#include "enflow_large.h"
 
 // ---------------------------------------------------------------------------
 // packing of the backward weight section
@@ -169,7 +169,21 @@ struct BwdArgs {
   const float* eg_dQ;
   const float* eg_dF;
   const float* eg_dG;
+  // large systems (lf_layer_bwd_kernel<.., BIG = true>): one workgroup per block of
+  // rbl rows; the rows' pair words come from the large path's neighbour search
+  // (enflow_large.h), column atoms are read from the tape; each pair's column-side
+  // d h / d pos goes to colc (summed per column by lg_colsum / lg_colfinal)
+  const int32_t* blk_start;
+  int rbl, max_n;
+  const int32_t* npairs_g;    // [A] pair words of row a
+  const int32_t* cntrow_g;    // [A] edges of row a
+  const uint32_t* pairs_g;    // [A][max_n] (label << 5 | mult << 27)
+  const int32_t* boff;        // [blocks] first pair row of the block (32-aligned)
+  int32_t* rowstart;          // [A] out: first pair row of row atom a
+  float* colc;                // [pair rows][CSTR] out
+  long long prb;              // pair rows allocated
 };
+constexpr int CSTR = 12;      // colc row: d h_j [NFMAX], d pos_j [3], pad
 
 // <= 80 KB at (H, NMAX) = (128, 64): two workgroups per CU.  The node-MLP
 // adjoint rows go through LDS a chunk of Smem::NBCH atoms at a time, in the
@@ -418,17 +432,37 @@ __device__ __forceinline__ size_t trow(size_t rtile, int W, int f, int j) {
 // VAR: layers may carry EGCL_NORM_DIFF / EGCL_TANH (read per layer from the
 // packed forward layer; a second instance so the default kernel keeps its
 // register allocation).  EGCL_ATTENTION is refused by the host.
-template <int H, int NMAX, bool VAR = false, int PREC = ENFLOW_BWD_PREC>
+template <int H, int NMAX, bool VAR = false, int PREC = ENFLOW_BWD_PREC, bool BIG = false>
 __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   static_assert(PREC == PREC_F32 || PREC == PREC_F16X3, "backward: fp32-accurate precisions only");
+  static_assert(!BIG || NMAX == 32, "large systems: 32-row blocks");
   __shared__ BwdSmem<H, NMAX> sb;
+  __shared__ int roff[BIG ? 33 : 1];   // BIG: the rows' first pair word within the block
   using Img = typename BwdSmem<H, NMAX>::Img;
   Img& sm = sb.f;
   constexpr int NT = H / 32;
   constexpr int AST = Img::AST;
   constexpr int NBCH = Img::NBCH;
-  const int m = blockIdx.x, tid = threadIdx.x;
-  const int a0 = B.mol_ptr[m], n = B.mol_ptr[m + 1] - a0;
+  const int tid = threadIdx.x;
+  // fused: m = the molecule, a0 / n its atoms.  BIG: a0 / n = the block's rows,
+  // ma0 / mn = their molecule's atoms
+  int m, a0, n, ma0, mn;
+  if constexpr (BIG) {
+    const int b = blockIdx.x;
+    if (b >= B.blk_start[B.num_mols]) return;
+    m = seg_of(B.blk_start, B.num_mols, b);
+    ma0 = B.mol_ptr[m];
+    mn = B.mol_ptr[m + 1] - ma0;
+    const int r0 = (b - B.blk_start[m]) * B.rbl;
+    a0 = ma0 + r0;
+    n = min(B.rbl, mn - r0);
+  } else {
+    m = blockIdx.x;
+    a0 = B.mol_ptr[m];
+    n = B.mol_ptr[m + 1] - a0;
+    ma0 = a0;
+    mn = n;
+  }
   if (n > NMAX || B.nf > NFMAX) {
     if (tid == 0) atomicOr(B.err, n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
     return;
@@ -466,14 +500,35 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
   }
   for (int a = tid; a < n; a += BLOCK) sm.Q[a] = B.tape[T.q + la + a];
   if (tid == 0) sm.err = 0;
+  if constexpr (BIG) {
+    for (int a = tid; a < n; a += BLOCK) sm.cntrow[a] = B.cntrow_g[a0 + a];
+    if (tid == 0) {
+      int acc = 0;
+      for (int a = 0; a < n; ++a) { roff[a] = acc; acc += B.npairs_g[a0 + a]; }
+      for (int a = n; a <= 32; ++a) roff[a] = acc;
+    }
+  }
   __syncthreads();
+  if constexpr (BIG) {   // the host's pair-row bound comes from the forward's counts
+    if ((long long)B.boff[blockIdx.x] + ((roff[32] + 31) & ~31) > B.prb) {
+      if (tid == 0) atomicOr(B.err, ENFLOW_ERR_TOO_MANY_ATOMS);
+      return;
+    }
+    for (int a = tid; a < n; a += BLOCK) B.rowstart[a0 + a] = B.boff[blockIdx.x] + roff[a];
+  }
   MolRef M;
-  M.a0 = a0;
-  M.n = n;
+  M.a0 = ma0;
+  M.n = mn;
   M.rc = B.r_cut[m];
-  M.bx = n > 0 ? sm.boxa[0] : 0.f;
-  M.by = n > 0 ? sm.boxa[1] : 0.f;
-  M.bz = n > 0 ? sm.boxa[2] : 0.f;
+  if constexpr (BIG) {   // the molecule's edge box: its first atom's (base.py:130)
+    M.bx = B.box[(size_t)ma0 * 3 + 0];
+    M.by = B.box[(size_t)ma0 * 3 + 1];
+    M.bz = B.box[(size_t)ma0 * 3 + 2];
+  } else {
+    M.bx = n > 0 ? sm.boxa[0] : 0.f;
+    M.by = n > 0 ? sm.boxa[1] : 0.f;
+    M.bz = n > 0 ? sm.boxa[2] : 0.f;
+  }
 
   STAMP(0);
   // ---- leapfrog adjoint (dynamics.py:13-21 in reverse order)
@@ -588,21 +643,22 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     sm.bias[2 * H + k] = B.Lp[L.bc1 + k];
     sm.bias[3 * H + k] = B.Lp[L.wc2 + k];
   }
-  build_pairs(sm, M, tid);   // same positions as the forward -> same pairs (reuses sm.u)
+  if constexpr (!BIG) build_pairs(sm, M, tid);   // same positions as the forward -> same pairs (reuses sm.u)
 
   STAMP(3);
   // ---- edge chain backward, one 32-pair tile per wave step (egcl.py:57-74, 76-89)
   {
     const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
     const int j = lane & 31, hh = lane >> 5;
-    const int P = sm.npairs;
-    const int TT = (P + 31) >> 5;
-    const int tpw = (TT + WAVES - 1) / WAVES;
-    const int t0 = w * tpw, t1 = min(TT, t0 + tpw);
+    const int P_all = BIG ? roff[32] : sm.npairs;   // pairs of the molecule / row block
+    const int TT_all = (P_all + 31) >> 5;
     const rsrc_t W = weights_rsrc(B.Lp, L.total);
     const rsrc_t WB = weights_rsrc(B.Bp, LB.total);
     const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
-    const size_t prow0 = (size_t)B.pair_off[m];
+    const size_t prow0 = BIG ? (size_t)B.boff[blockIdx.x] : (size_t)B.pair_off[m];
+    // BIG: column atoms from the tape (this layer's input state of the molecule)
+    const float* cpos = B.tape + T.pos + ((size_t)B.layer * B.num_atoms + ma0) * 3;
+    const float* chx = B.tape + T.hx + ((size_t)B.layer * B.num_atoms + ma0) * T.ldhx;
     const bool x3 = PREC == PREC_F16X3;
     const float inv1 = x3 ? B.Lp[L.scl + 1] : 1.f;   // edge_nn.2 / coord_nn.0 / edge_nn.0 (and ^T)
     const float inv2 = x3 ? B.Lp[L.scl + 3] : 1.f;
@@ -613,7 +669,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const bool v_att = VAR && (vfl & EGCL_ATTENTION) != 0;
     // the molecule's tile-blocked rows (trow): buffer resources on its first
     // row, per element a wave-uniform byte offset (tile, feature) + the lane's
-    const size_t nrow = (size_t)TT * 32;
+    const size_t nrow = (size_t)TT_all * 32;
     const rsrc_t rp0 = rows_rsrc(B.p0 + prow0 * H, nrow * H), rpe = rows_rsrc(B.pe + prow0 * H, nrow * H);
     const rsrc_t rpc = rows_rsrc(B.pc + prow0 * H, nrow * H);
     const rsrc_t rdp0 = rows_rsrc(B.dp0 + prow0 * H, nrow * H), rdpe = rows_rsrc(B.dpe + prow0 * H, nrow * H);
@@ -626,17 +682,62 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     float* const wacc = sm.u.nb + (size_t)w * n * EW;
     for (int e = tid; e < WAVES * n * EW; e += BLOCK) sm.u.nb[e] = 0.f;
     __syncthreads();
+    constexpr int PCAP = Img::PC;   // BIG: pair words per pass through sm.pairs
+    static_assert(PCAP % 32 == 0, "passes of whole tiles");
+    for (int pp0 = 0;; pp0 += PCAP) {
+    int P = P_all;
+    if constexpr (BIG) {   // the next pass of the rows' pair words (| local row)
+      P = min(PCAP, P_all - pp0);
+      for (int e = tid; e < P; e += BLOCK) {
+        const int pe = pp0 + e;
+        int lo = 0, hi = n;   // row il: roff[il] <= pe < roff[il + 1]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (roff[mid] <= pe) lo = mid;
+          else hi = mid;
+        }
+        sm.pairs[e] = B.pairs_g[(size_t)(a0 + lo) * B.max_n + (pe - roff[lo])] | (uint32_t)lo;
+      }
+      __syncthreads();
+    }
+    const int TT = (P + 31) >> 5;
+    const int tpw = (TT + WAVES - 1) / WAVES;
+    const int t0 = w * tpw, t1 = min(TT, t0 + tpw);
     for (int tile = t0; tile < t1; ++tile) {
       const int p = tile * 32 + j;
       const bool valid = p < P;
       const uint32_t pr = valid ? sm.pairs[p] : 0u;
-      const int i = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu);
-      const float c = (float)(pr >> 16);       // multiplicity; 0 on padding lanes
-      const size_t Rw = prow0 + (size_t)p;
-      const int tsb = tile * H * 128;   // tile byte offset in an H-wide array (16-wide: / (H / 16))
-      const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], hbx);
-      const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], hby);
-      const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], hbz);
+      int i, jl;
+      float c;   // multiplicity; 0 on padding lanes
+      if constexpr (BIG) {
+        i = (int)(pr & 31u);
+        jl = (int)((pr >> 5) & 0x3fffffu);
+        c = (float)(pr >> 27);
+      } else {
+        i = (int)(pr & 0xffu);
+        jl = (int)((pr >> 8) & 0xffu);
+        c = (float)(pr >> 16);
+      }
+      const int gt = (pp0 >> 5) + tile;   // tile index within the molecule's / block's rows
+      const size_t Rw = prow0 + (size_t)(pp0 + p);
+      const int tsb = gt * H * 128;   // tile byte offset in an H-wide array (16-wide: / (H / 16))
+      float cx, cy, cz;   // column atom position
+      if constexpr (BIG) {
+        cx = cpos[jl * 3 + 0];
+        cy = cpos[jl * 3 + 1];
+        cz = cpos[jl * 3 + 2];
+      } else {
+        cx = sm.pos[jl * 3 + 0];
+        cy = sm.pos[jl * 3 + 1];
+        cz = sm.pos[jl * 3 + 2];
+      }
+      auto colh = [&](int q) -> float {   // column atom feature q < nf
+        if constexpr (BIG) return chx[(size_t)jl * T.ldhx + q];
+        else return sm.h[jl * NFP + q];
+      };
+      const float dx = pbc1(sm.pos[i * 3 + 0] - cx, hbx);
+      const float dy = pbc1(sm.pos[i * 3 + 1] - cy, hby);
+      const float dz = pbc1(sm.pos[i * 3 + 2] - cz, hbz);
       const float radial = dx * dx + dy * dy + dz * dz;
 
       // X row of edge_nn.0: [h_i, h_j, radial]
@@ -645,9 +746,9 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
         const int q = 8 * hh + u;
         float v = 0.f;
         if (q < nf) v = sm.h[i * NFP + q];
-        else if (q < 2 * nf) v = sm.h[jl * NFP + q - nf];
+        else if (q < 2 * nf) v = colh(q - nf);
         else if (q == 2 * nf) v = radial;
-        ST_OUT(rxin, (hh * 256 + j) * 4, tile * 2048 + u * 128, valid ? v : 0.f);
+        ST_OUT(rxin, (hh * 256 + j) * 4, gt * 2048 + u * 128, valid ? v : 0.f);
       }
 
       // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1
@@ -659,9 +760,14 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
         for (int ks = 0; ks < ks_n; ++ks) {   // k order gemm0_col (as the forward)
           f32x16 in;
           if (ks == 0) {
-            const float* hrow = &sm.h[(hh ? jl : i) * NFP];   // rows zero-padded past nf
+            if (BIG && hh) {
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) in[jj] = hrow[jj];
+              for (int jj = 0; jj < 8; ++jj) in[jj] = jj < nf ? colh(jj) : 0.f;
+            } else {
+              const float* hrow = &sm.h[(hh ? jl : i) * NFP];   // rows zero-padded past nf
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) in[jj] = hrow[jj];
+            }
             if (hh && nf <= 7) in[7] = radial;
           } else {
 #pragma unroll
@@ -685,8 +791,10 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       } else {
 #pragma unroll
         for (int s = 0; s < NFMAX + 1; ++s) {
+          const int qc = 2 * (s - NFMAX / 2) + hh;
           const float b = s < NFMAX / 2 ? sm.h[i * NFP + 2 * s + hh]
-                        : (s < NFMAX ? sm.h[jl * NFP + 2 * (s - NFMAX / 2) + hh] : (hh == 0 ? radial : 0.f));
+                        : (s < NFMAX ? (BIG ? (qc < nf ? colh(qc) : 0.f) : sm.h[jl * NFP + qc])
+                                     : (hh == 0 ? radial : 0.f));
 #pragma unroll
           for (int t = 0; t < NT; ++t)
             x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
@@ -901,8 +1009,10 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
         for (int r = 0; r < 16; ++r) {
           const int q = rho(r, hh);
           if (q < nf) atomicAdd(&wacc[i * EW + q], ain[r]);
-          else if (q < 2 * nf) atomicAdd(&wacc[jl * EW + q - nf], ain[r]);
-          else if (q == 2 * nf) arad = ain[r];
+          else if (q < 2 * nf) {
+            if constexpr (BIG) B.colc[Rw * CSTR + q - nf] = ain[r];
+            else atomicAdd(&wacc[jl * EW + q - nf], ain[r]);
+          } else if (q == 2 * nf) arad = ain[r];
         }
       }
       // d coord_diff (radial = |cd|^2, trans = cd * phi), d pos_i += ., d pos_j -= .
@@ -917,7 +1027,22 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       const float tx = ux + 2.f * dx * arad;
       const float ty = uy + 2.f * dy * arad;
       const float tz = uz + 2.f * dz * arad;
-      if (valid && (tx != 0.f || ty != 0.f || tz != 0.f)) {
+      if constexpr (BIG) {   // the column's d pos: both half-waves' parts, one store
+        const float sx = tx + __shfl_xor(tx, 32, 64), sy = ty + __shfl_xor(ty, 32, 64),
+                    sz = tz + __shfl_xor(tz, 32, 64);
+        if (valid) {
+          if (tx != 0.f || ty != 0.f || tz != 0.f) {
+            atomicAdd(&wacc[i * EW + nf + 0], tx);
+            atomicAdd(&wacc[i * EW + nf + 1], ty);
+            atomicAdd(&wacc[i * EW + nf + 2], tz);
+          }
+          if (hh == 0) {
+            B.colc[Rw * CSTR + NFMAX + 0] = -sx;
+            B.colc[Rw * CSTR + NFMAX + 1] = -sy;
+            B.colc[Rw * CSTR + NFMAX + 2] = -sz;
+          }
+        }
+      } else if (valid && (tx != 0.f || ty != 0.f || tz != 0.f)) {
         atomicAdd(&wacc[i * EW + nf + 0], tx);
         atomicAdd(&wacc[i * EW + nf + 1], ty);
         atomicAdd(&wacc[i * EW + nf + 2], tz);
@@ -925,6 +1050,10 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
         atomicAdd(&wacc[jl * EW + nf + 1], -ty);
         atomicAdd(&wacc[jl * EW + nf + 2], -tz);
       }
+    }
+    if constexpr (!BIG) break;
+    __syncthreads();   // sm.pairs consumed
+    if (pp0 + PCAP >= P_all) break;
     }
     __syncthreads();
     for (int e = tid; e < n * EW; e += BLOCK) {
@@ -1528,6 +1657,148 @@ __global__ void __launch_bounds__(BLOCK) nll_bwd_kernel(const int32_t* mol_ptr, 
 }
 
 // ---------------------------------------------------------------------------
+// large systems: pair-row offsets of the row blocks, column-side adjoint sums
+// ---------------------------------------------------------------------------
+// one workgroup: boff[b] = 32-aligned exclusive prefix of the blocks' pair words,
+// total[0] = all rows (the weight-gradient passes' row count)
+__device__ __forceinline__ int lg_block_words(const int32_t* mol_ptr, int num_mols, const int32_t* blk_start,
+                                              int rbl, const int32_t* npairs, int b) {
+  const int m = seg_of(blk_start, num_mols, b);
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
+  const int r0 = (b - blk_start[m]) * rbl, rb = min(rbl, n - r0);
+  int t = 0;
+  for (int a = 0; a < rb; ++a) t += npairs[a0 + r0 + a];
+  return (t + 31) & ~31;
+}
+__global__ void __launch_bounds__(BLOCK) lg_bwd_offsets_kernel(const int32_t* mol_ptr, int num_mols,
+                                                               const int32_t* blk_start, int rbl,
+                                                               const int32_t* npairs, int32_t* boff,
+                                                               int32_t* total) {
+  __shared__ int part[BLOCK + 1];
+  const int tid = threadIdx.x;
+  const int nb = blk_start[num_mols];
+  const int per = (nb + BLOCK - 1) / BLOCK;
+  const int b0 = min(nb, tid * per), b1 = min(nb, b0 + per);
+  int s = 0;
+  for (int b = b0; b < b1; ++b) s += lg_block_words(mol_ptr, num_mols, blk_start, rbl, npairs, b);
+  part[tid] = s;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int k = 0; k < BLOCK; ++k) { const int v = part[k]; part[k] = acc; acc += v; }
+    part[BLOCK] = acc;
+    total[0] = acc;
+  }
+  __syncthreads();
+  int acc = part[tid];
+  for (int b = b0; b < b1; ++b) {
+    boff[b] = acc;
+    acc += lg_block_words(mol_ptr, num_mols, blk_start, rbl, npairs, b);
+  }
+}
+
+// partial column sums: thread = column atom q of its molecule, blockIdx.y = a
+// chunk of LG_RC rows; the rows' slots of q (smap, coalesced over q) locate the
+// pair's column adjoints in colc; rows in increasing order -> deterministic
+constexpr int LG_RC = 256;
+__global__ void __launch_bounds__(BLOCK) lg_colsum_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
+                                                          int max_n, const int32_t* smap, const int32_t* rowstart,
+                                                          const float* colc, int nf, float* part) {
+  const int q = blockIdx.x * BLOCK + threadIdx.x, ch = blockIdx.y;
+  if (q >= num_atoms) return;
+  const int m = seg_of(mol_ptr, num_mols, q);
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0, ql = q - a0;
+  const int i0 = min(n, ch * LG_RC), i1 = min(n, i0 + LG_RC);
+  float acc[NFMAX + 3];
+#pragma unroll
+  for (int k = 0; k < NFMAX + 3; ++k) acc[k] = 0.f;
+  for (int i = i0; i < i1; ++i) {
+    const int k = smap[(size_t)(a0 + i) * max_n + ql];
+    if (k >= 0) {
+      const float* c = colc + (size_t)(rowstart[a0 + i] + k) * CSTR;
+      for (int f = 0; f < nf; ++f) acc[f] += c[f];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) acc[NFMAX + d] += c[NFMAX + d];
+    }
+  }
+  float* o = part + ((size_t)ch * num_atoms + q) * CSTR;
+#pragma unroll
+  for (int k = 0; k < NFMAX + 3; ++k) o[k] = acc[k];
+}
+
+// column label c = id_mapping[q] (base.py:137): atom c receives the column sums
+// of every q mapped to it, q and chunks in increasing order
+__global__ void __launch_bounds__(BLOCK) lg_colfinal_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
+                                                            const int32_t* idmap, const float* part, int nch,
+                                                            int nf, float* ah, float* apos) {
+  const int c = blockIdx.x * BLOCK + threadIdx.x;
+  if (c >= num_atoms) return;
+  const int m = seg_of(mol_ptr, num_mols, c);
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0, cl = c - a0;
+  float acc[NFMAX + 3];
+#pragma unroll
+  for (int k = 0; k < NFMAX + 3; ++k) acc[k] = 0.f;
+  for (int q = 0; q < n; ++q) {
+    if (idmap[a0 + q] != cl) continue;
+    for (int ch = 0; ch < nch; ++ch) {
+      const float* o = part + ((size_t)ch * num_atoms + a0 + q) * CSTR;
+      for (int f = 0; f < nf; ++f) acc[f] += o[f];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) acc[NFMAX + d] += o[NFMAX + d];
+    }
+  }
+  for (int f = 0; f < nf; ++f) ah[(size_t)c * nf + f] += acc[f];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) apos[(size_t)c * 3 + d] += acc[NFMAX + d];
+}
+
+// atom chunks of <= 32 for the per-atom ArgMax backward on large systems
+__global__ void __launch_bounds__(BLOCK) chunk_ptr_kernel(int num_atoms, int chunks, int32_t* ptr) {
+  const int k = blockIdx.x * BLOCK + threadIdx.x;
+  if (k <= chunks) ptr[k] = min(32 * k, num_atoms);
+}
+
+// Alchemical_NLL backward for molecules past 64 atoms: thread per atom, the
+// molecule's positions from global memory (L2); same arithmetic and b order as
+// nll_bwd_kernel
+__global__ void __launch_bounds__(BLOCK) nll_bwd_large_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
+                                                              int nf, const float* h, const float* g,
+                                                              const float* pos, const float* vel, float kBT,
+                                                              float softening, const float* grad_loss, float* ah,
+                                                              float* ag, float* apos, float* avel,
+                                                              float* adj_ldj) {
+  const int a = blockIdx.x * BLOCK + threadIdx.x;
+  const float s = grad_loss ? grad_loss[0] : 1.f;
+  const float invM = s / (float)num_mols;
+  const float cH = invM / kBT;
+  if (a == 0) adj_ldj[0] = -invM;                                // log_px += ldj
+  if (a >= num_atoms) return;
+  const int m = seg_of(mol_ptr, num_mols, a);
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
+  for (int d = 0; d < 3; ++d) avel[(size_t)a * 3 + d] = cH * vel[(size_t)a * 3 + d];   // H = LJ + 0.5 vel^2
+  for (int q = 0; q < nf; ++q) {                                 // -log_gaussian(h), (g)
+    ah[(size_t)a * nf + q] = invM * h[(size_t)a * nf + q];
+    ag[(size_t)a * nf + q] = invM * g[(size_t)a * nf + q];
+  }
+  const float px = pos[(size_t)a * 3], py = pos[(size_t)a * 3 + 1], pz = pos[(size_t)a * 3 + 2];
+  float f[3] = {0.f, 0.f, 0.f};
+  for (int bl = 0; bl < n; ++bl) {
+    const int b = a0 + bl;
+    if (b == a) continue;
+    const float qx = pos[(size_t)b * 3], qy = pos[(size_t)b * 3 + 1], qz = pos[(size_t)b * 3 + 2];
+    const float dx = px - qx, dy = py - qy, dz = pz - qz;
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    if (d2 == 0.f) continue;                                     // dist_sq != 0 (loss.py:15)
+    const float r = d2 + softening, ir = 1.f / r, ir2 = ir * ir, ir4 = ir2 * ir2;
+    const float dEdR = 4.f * (-6.f * ir4 * ir2 * ir + 3.f * ir4);
+    f[0] += dEdR * 2.f * dx;
+    f[1] += dEdR * 2.f * dy;
+    f[2] += dEdR * 2.f * dz;
+  }
+  for (int d = 0; d < 3; ++d) apos[(size_t)a * 3 + d] = cH * f[d];
+}
+
+// ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
 static inline hipStream_t SB(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -1701,6 +1972,68 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
     }                                                         \
   } while (0)
 
+// One layer's weight gradients from its pair rows (prow: device count of pair
+// rows) and atom rows, straight into the torch parameter layout G.
+static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const int32_t* prow, int prb,
+                              bool variants, float* G, const float* Rp, const RawEgcl& R, const float* hx,
+                              int num_atoms, int nf, int H) {
+    OuterBatch ob;
+    ob.nd = 0;
+    int wg = 0;
+    float* part = wb + Wl.part;
+    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, PAIR_OUTER);
+    add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
+    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
+    add_desc(ob, wg, wb + Wl.pc, H, H, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);
+    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
+    ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
+    ob.d[ob.nd - 1].rowv = wb + Wl.aphi;
+    if (variants) ob.d[ob.nd - 1].xrow = wb + Wl.patt;          // the message is e * att
+    ob.d[ob.nd - 1].colv = Rp + R.wc2;
+    // coord_nn.2: d wc2 = sum_rows aphi silu(pc); aphi is one value per row (its "tile-blocked"
+    // layout is row-major with width 1)
+    add_desc(ob, wg, wb + Wl.aphi, 1, 1, wb + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr,
+             ENFLOW_OUTER_X3 ? 3 : 1);
+    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
+    if (ENFLOW_OUTER_X3) ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;   // folded into coord_nn.0's pass
+    if (variants) {   // att_nn.0: d w = sum_rows dlogit e, d b = sum_rows dlogit (0 rows without attention)
+      add_desc(ob, wg, wb + Wl.dlogit, 1, 1, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
+      ob.d[ob.nd - 1].xf_x = 1;                                 // X = silu(pre_e) = e
+    }
+    add_desc(ob, wg, wb + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
+    add_desc(ob, wg, wb + Wl.aq, 1, 1, wb + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
+    add_desc(ob, wg, wb + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,
+             G + R.bn1);
+    add_desc(ob, wg, wb + Wl.agr, nf, nf, wb + Wl.sn, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wn2,
+             G + R.bn2);
+    return run_outer(ob, wg, st2);
+}
+
+// ArgMax.network's gradients (the flow's dequantiser) into grad_dequant; ptr /
+// chunks: the atom chunks argmax_bwd_kernel runs on (<= nmax_sel atoms each)
+static int argmax_grads(hipStream_t st, const BwdWs& Wl, float* wb, const int32_t* ptr, int chunks, int nmax_sel,
+                        int H, int nf, int num_atoms, const float* h_data, const float* noise,
+                        const float* dequant_raw, const float* adj_h, const float* adj_ldj, float* grad_dequant) {
+    float* apre = wb + Wl.au;
+    float* spre = wb + Wl.su;
+    float* anet = wb + Wl.anet;
+#define CALL(HH, NN)                                                                                    \
+  hipLaunchKernelGGL((argmax_bwd_kernel<HH, NN>), dim3(chunks), dim3(BLOCK), 0, st, ptr, nf, h_data, noise, \
+                     dequant_raw, adj_h, adj_ldj, apre, spre, anet)
+    DISPATCH_HN_B(H, nmax_sel, CALL);
+#undef CALL
+    const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
+    OuterBatch ob;
+    ob.nd = 0;
+    int wg = 0;
+    float* part = wb + Wl.part;
+    add_desc(ob, wg, apre, H, H, h_data, nf, nf, nullptr, num_atoms, num_atoms, part, grad_dequant + rW1,
+             grad_dequant + rb1);
+    add_desc(ob, wg, anet, 2 * nf, 2 * nf, spre, H, H, nullptr, num_atoms, num_atoms, part, grad_dequant + rW2,
+             grad_dequant + rb2);
+    return run_outer(ob, wg, st);
+}
+
 extern "C" {
 
 #if defined(ENFLOW_STAMPS_BWD) && !defined(ENFLOW_STAMPS)
@@ -1745,10 +2078,13 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
                                        const float* pos, const float* vel, float kBT, float softening,
                                        const float* grad_loss, float* adj_h, float* adj_g, float* adj_pos,
                                        float* adj_vel, float* adj_ldj, void* stream) {
-  (void)num_atoms;
-  if (num_mols < 1 || max_mol_atoms > 64 || nf < 1 || !adj_ldj) return -1;
+  if (num_mols < 1 || num_atoms < 0 || nf < 1 || !adj_ldj) return -1;
   const int tm = enflow_tm_begin("nll_bwd_kernel", SB(stream));
-  if (max_mol_atoms <= 32)
+  if (max_mol_atoms > 64)
+    hipLaunchKernelGGL(nll_bwd_large_kernel, dim3((num_atoms + BLOCK) / BLOCK), dim3(BLOCK), 0, SB(stream), mol_ptr,
+                       num_mols, num_atoms, nf, h, g, pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos,
+                       adj_vel, adj_ldj);
+  else if (max_mol_atoms <= 32)
     hipLaunchKernelGGL((nll_bwd_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, SB(stream), mol_ptr, num_mols, nf, h, g,
                        pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos, adj_vel, adj_ldj);
   else
@@ -1808,7 +2144,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     float* const wb = ws + Wl.buf0 + (size_t)(l & 1) * Wl.span;   // this layer's buffer
     // the buffer was last read by layer l + 2's weight-gradient pass
     if (l + 2 < n_layers && hipStreamWaitEvent(st, ev(2 * (l + 2) + 1), 0) != hipSuccess) return -2;
-    BwdArgs A;
+    BwdArgs A{};
     A.mol_ptr = mol_ptr; A.r_cut = r_cut; A.box = box; A.tape = tape;
     A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
     A.Lp = layers + (size_t)l * L.total;
@@ -1835,40 +2171,11 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     if (hipEventRecord(ev(2 * l), st) != hipSuccess || hipStreamWaitEvent(st2, ev(2 * l), 0) != hipSuccess)
       return -2;
     // the layer's weight gradients, straight into the torch parameter layout (aux stream)
-    float* G = grad_layers + (size_t)l * R.total_bwd;
-    const int32_t* prow = offs + (size_t)l * (num_mols + 1) + num_mols;
-    const float* hx = tape + tape_layout(num_atoms, nf, H, n_layers).hx +
-                      (size_t)l * num_atoms * (nf + H);
-    OuterBatch ob;
-    ob.nd = 0;
-    int wg = 0;
-    float* part = wb + Wl.part;
-    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, PAIR_OUTER);
-    add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
-    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
-    add_desc(ob, wg, wb + Wl.pc, H, H, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);
-    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
-    ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
-    ob.d[ob.nd - 1].rowv = wb + Wl.aphi;
-    if (variants) ob.d[ob.nd - 1].xrow = wb + Wl.patt;          // the message is e * att
-    ob.d[ob.nd - 1].colv = A.Rp + R.wc2;
-    // coord_nn.2: d wc2 = sum_rows aphi silu(pc); aphi is one value per row (its "tile-blocked"
-    // layout is row-major with width 1)
-    add_desc(ob, wg, wb + Wl.aphi, 1, 1, wb + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr,
-             ENFLOW_OUTER_X3 ? 3 : 1);
-    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
-    if (ENFLOW_OUTER_X3) ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;   // folded into coord_nn.0's pass
-    if (variants) {   // att_nn.0: d w = sum_rows dlogit e, d b = sum_rows dlogit (0 rows without attention)
-      add_desc(ob, wg, wb + Wl.dlogit, 1, 1, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
-      ob.d[ob.nd - 1].xf_x = 1;                                 // X = silu(pre_e) = e
-    }
-    add_desc(ob, wg, wb + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
-    add_desc(ob, wg, wb + Wl.aq, 1, 1, wb + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);
-    add_desc(ob, wg, wb + Wl.an, H, H, hx, nf + H, nf + H, nullptr, num_atoms, num_atoms, part, G + R.Wn1,
-             G + R.bn1);
-    add_desc(ob, wg, wb + Wl.agr, nf, nf, wb + Wl.sn, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wn2,
-             G + R.bn2);
-    const int rc = run_outer(ob, wg, st2);
+    const int rc = layer_weight_grads(st2, Wl, wb, offs + (size_t)l * (num_mols + 1) + num_mols, prb, variants,
+                                      grad_layers + (size_t)l * R.total_bwd, A.Rp, R,
+                                      tape + tape_layout(num_atoms, nf, H, n_layers).hx +
+                                          (size_t)l * num_atoms * (nf + H),
+                                      num_atoms, nf, H);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
   }
@@ -1876,25 +2183,8 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
   if (n_layers > 0 && hipStreamWaitEvent(st, ev(1), 0) != hipSuccess) return -2;   // layer 0's pass (the last)
 
   if (dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-    float* const wb = ws + Wl.buf0;
-    float* apre = wb + Wl.au;
-    float* spre = wb + Wl.su;
-    float* anet = wb + Wl.anet;
-#define CALL(HH, NN)                                                                                      \
-  hipLaunchKernelGGL((argmax_bwd_kernel<HH, NN>), dim3(num_mols), dim3(BLOCK), 0, st, mol_ptr, nf, h_data, \
-                     noise, dequant_raw, adj_h, adj_ldj, apre, spre, anet)
-    DISPATCH_HN_B(H, max_mol_atoms, CALL);
-#undef CALL
-    const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
-    OuterBatch ob;
-    ob.nd = 0;
-    int wg = 0;
-    float* part = wb + Wl.part;
-    add_desc(ob, wg, apre, H, H, h_data, nf, nf, nullptr, num_atoms, num_atoms, part, grad_dequant + rW1,
-             grad_dequant + rb1);
-    add_desc(ob, wg, anet, 2 * nf, 2 * nf, spre, H, H, nullptr, num_atoms, num_atoms, part, grad_dequant + rW2,
-             grad_dequant + rb2);
-    const int rc = run_outer(ob, wg, st);
+    const int rc = argmax_grads(st, Wl, ws + Wl.buf0, mol_ptr, num_mols, max_mol_atoms, H, nf, num_atoms, h_data,
+                                noise, dequant_raw, adj_h, adj_ldj, grad_dequant);
     if (rc) return rc;
   }
   hipLaunchKernelGGL(poison_on_err_kernel, dim3(64), dim3(256), 0, st, err_flag, grad_layers,
@@ -1917,6 +2207,153 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
                           layers_bwd, layers_raw, n_layers, dequant_kind, dequant_raw, h_data, noise, dt, cw, adj_h,
                           adj_g, adj_pos, adj_vel, adj_ldj, grad_layers, grad_dequant, workspace, workspace_bytes,
                           pair_row_bound, err_flag, stream, nullptr, nullptr, nullptr);
+}
+
+// ---- large systems (molecules past the fused backward's 64-atom image) -----
+// Per layer, last to first: the neighbour list of the layer's taped positions
+// (the forward's own search kernels, + the dense slot map), the pair-row offsets
+// of the row blocks, lf_layer_bwd_kernel<.., BIG> per block of rows (row-side
+// adjoints in LDS, column-side per pair into colc), the column sums (colsum per
+// row chunk, colfinal per id_mapping label), then the weight gradients on the
+// auxiliary stream as in the fused backward.
+struct LgBwdWs { size_t lg, smap, bwd, colc, part, boff, tot, rowstart, chunk, total; int nch, nb; };
+static LgBwdWs lg_bwd_ws(int num_mols, int num_atoms, int max_n, int nf, int H, long long prb) {
+  LgBwdWs W;
+  const size_t A = (size_t)num_atoms;
+  W.nch = max(1, cdiv(max_n, LG_RC));
+  W.nb = num_atoms / lg_rows(num_atoms) + num_mols + 1;
+  size_t o = 0;
+  W.lg = o; o = al256(o + lg_workspace(num_mols, num_atoms, max_n, nf).total);
+  W.smap = o; o = al256(o + A * (size_t)max_n * 4);
+  W.bwd = o; o = al256(o + bwd_ws(num_mols, num_atoms, nf, H, 0, prb).total * sizeof(float));
+  W.colc = o; o = al256(o + (size_t)prb * CSTR * 4);
+  W.part = o; o = al256(o + (size_t)W.nch * A * CSTR * 4);
+  W.boff = o; o = al256(o + 2 * ((size_t)W.nb + 1) * 4);
+  W.tot = o; o = al256(o + 2 * 4);
+  W.rowstart = o; o = al256(o + A * 4);
+  W.chunk = o; o = al256(o + ((A + 31) / 32 + 2) * 4);
+  W.total = o;
+  return W;
+}
+
+int64_t enflow_lf_backward_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                                                int64_t pair_row_bound) {
+  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms >= (1 << 22) || nf < 1 || nf > NFMAX ||
+      !hid_ok_b(H) || pair_row_bound < 0 || pair_row_bound > 0x7fffffffLL)
+    return -1;
+  return (int64_t)lg_bwd_ws(num_mols, num_atoms, max_mol_atoms, nf, H, pair_row_bound).total;
+}
+
+int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                                 const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
+                                 const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                                 int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                                 float dt, float cw,
+                                 float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                                 float* grad_layers, float* grad_dequant,
+                                 void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                                 int32_t* err_flag, void* stream) {
+  const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
+  dequant_kind &= 0xff;
+  const int64_t need = enflow_lf_backward_large_workspace_size(num_mols, num_atoms, max_mol_atoms, nf, H,
+                                                               pair_row_bound);
+  if (need < 0 || n_layers < 0) return -1;
+  if (!mol_ptr || !r_cut || !box || !tape || !layers || !layers_bwd || !layers_raw || !adj_h || !adj_g ||
+      !adj_pos || !adj_vel || !adj_ldj || !grad_layers || !workspace || !err_flag)
+    return -1;
+  if (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!dequant_raw || !h_data || !noise || !grad_dequant)) return -1;
+  if (workspace_bytes < need) return -6;
+  if (num_mols == 0) return 0;
+  const LgBwdWs W = lg_bwd_ws(num_mols, num_atoms, max_mol_atoms, nf, H, pair_row_bound);
+  const BwdWs Wl = bwd_ws(num_mols, num_atoms, nf, H, 0, pair_row_bound);
+  char* base = static_cast<char*>(workspace);
+  float* ws = reinterpret_cast<float*>(base + W.bwd);
+  int32_t* smap = reinterpret_cast<int32_t*>(base + W.smap);
+  float* colc = reinterpret_cast<float*>(base + W.colc);
+  float* part = reinterpret_cast<float*>(base + W.part);
+  int32_t* boff = reinterpret_cast<int32_t*>(base + W.boff);
+  int32_t* tot = reinterpret_cast<int32_t*>(base + W.tot);
+  int32_t* rowstart = reinterpret_cast<int32_t*>(base + W.rowstart);
+  int32_t* chunk = reinterpret_cast<int32_t*>(base + W.chunk);
+  hipStream_t st = SB(stream);
+  const EgclLayout L = egcl_layout(H, nf);
+  const EgclBwdLayout LB = egcl_bwd_layout(H);
+  const RawEgcl R = raw_egcl(H, nf);
+  const TapeLayout T = tape_layout(num_atoms, nf, H, n_layers);
+  const int prb = (int)pair_row_bound;
+  LgArgs G = lg_args(num_mols, num_atoms, max_mol_atoms, nf, mol_ptr, r_cut, box, nullptr, nullptr, nullptr,
+                     nullptr, dt, cw, err_flag, base + W.lg);
+  G.smap = smap;
+  int dev = 0;
+  if ((st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev)) != hipSuccess || dev < 0 || dev >= 64) return -2;
+  std::lock_guard<std::mutex> aux_lock(g_aux_mu);
+  hipStream_t st2 = aux_stream(dev);
+  if (!st2) return -2;
+  auto ev = [&](int i) { return aux_event(dev, (size_t)i); };
+  for (int i = 0; i < 2 * n_layers + 1; ++i)
+    if (!ev(i)) return -2;
+  lg_setup(st, G);
+  const int grid = lg_grid(G);
+  const int ga = (num_atoms + BLOCK - 1) / BLOCK;
+  for (int l = n_layers - 1; l >= 0; --l) {
+    float* const wb = ws + Wl.buf0 + (size_t)(l & 1) * Wl.span;
+    int32_t* const boff_l = boff + (size_t)(l & 1) * (W.nb + 1);
+    int32_t* const tot_l = tot + (l & 1);
+    if (l + 2 < n_layers && hipStreamWaitEvent(st, ev(2 * (l + 2) + 1), 0) != hipSuccess) return -2;
+    G.pos = const_cast<float*>(tape + T.pos + (size_t)l * num_atoms * 3);
+    lg_search(st, G);
+    hipLaunchKernelGGL(lg_bwd_offsets_kernel, dim3(1), dim3(BLOCK), 0, st, mol_ptr, num_mols, G.blk_start, G.rbl,
+                       G.npairs, boff_l, tot_l);
+    BwdArgs A{};
+    A.mol_ptr = mol_ptr; A.r_cut = r_cut; A.box = box; A.tape = tape;
+    A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
+    A.Lp = layers + (size_t)l * L.total;
+    A.Bp = layers_bwd + (size_t)l * LB.total;
+    A.Rp = layers_raw + (size_t)l * R.total_bwd;
+    A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
+    A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
+    A.xin = wb + Wl.xin; A.p0 = wb + Wl.p0; A.pe = wb + Wl.pe; A.pc = wb + Wl.pc;
+    A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
+    A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
+    A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
+    A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
+    A.blk_start = G.blk_start; A.rbl = G.rbl; A.max_n = max_mol_atoms;
+    A.npairs_g = G.npairs; A.cntrow_g = G.cntrow; A.pairs_g = G.pairs;
+    A.boff = boff_l; A.rowstart = rowstart; A.colc = colc; A.prb = pair_row_bound;
+#define CALLB(HH)                                                                                              \
+  do {                                                                                                         \
+    if (variants) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, true, ENFLOW_BWD_PREC, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
+    else ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, false, ENFLOW_BWD_PREC, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
+  } while (0)
+    if (H == 32) CALLB(32);
+    else if (H == 64) CALLB(64);
+    else CALLB(128);
+#undef CALLB
+    if (num_atoms > 0) {
+      hipLaunchKernelGGL(lg_colsum_kernel, dim3(ga, W.nch), dim3(BLOCK), 0, st, mol_ptr, num_mols, num_atoms,
+                         max_mol_atoms, smap, rowstart, colc, nf, part);
+      hipLaunchKernelGGL(lg_colfinal_kernel, dim3(ga), dim3(BLOCK), 0, st, mol_ptr, num_mols, num_atoms, G.idmap,
+                         part, W.nch, nf, adj_h, adj_pos);
+    }
+    if (hipEventRecord(ev(2 * l), st) != hipSuccess || hipStreamWaitEvent(st2, ev(2 * l), 0) != hipSuccess)
+      return -2;
+    const int rc = layer_weight_grads(st2, Wl, wb, tot_l, prb, variants, grad_layers + (size_t)l * R.total_bwd,
+                                      A.Rp, R, tape + T.hx + (size_t)l * num_atoms * (nf + H), num_atoms, nf, H);
+    if (rc) return rc;
+    if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
+  }
+  if (n_layers > 0 && hipStreamWaitEvent(st, ev(1), 0) != hipSuccess) return -2;
+  if (dequant_kind == ENFLOW_DEQUANT_ARGMAX && num_atoms > 0) {
+    const int chunks = (num_atoms + 31) / 32;
+    hipLaunchKernelGGL(chunk_ptr_kernel, dim3(chunks / BLOCK + 1), dim3(BLOCK), 0, st, num_atoms, chunks, chunk);
+    const int rc = argmax_grads(st, Wl, ws + Wl.buf0, chunk, chunks, 32, H, nf, num_atoms, h_data, noise,
+                                dequant_raw, adj_h, adj_ldj, grad_dequant);
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(poison_on_err_kernel, dim3(64), dim3(256), 0, st, err_flag, grad_layers,
+                     (long long)n_layers * R.total_bwd, dequant_kind == ENFLOW_DEQUANT_ARGMAX ? grad_dequant : nullptr,
+                     (long long)(H * nf + H + 2 * nf * H + 2 * nf));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // ---- standalone EGCL.forward backward ------------------------------------

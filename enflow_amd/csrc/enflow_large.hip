@@ -38,48 +38,7 @@
 // reductions run in a fixed order: results are bitwise reproducible.
 #include <stdlib.h>
 
-#include "flow_device.h"
-
-struct LgArgs {
-  const int32_t* mol_ptr;
-  const float* r_cut;
-  const float* box;
-  float* h;          // this layer's state (forward: read only here, next state -> h2 / pos2)
-  float* g;
-  float* pos;
-  float* vel;
-  float* h2;
-  float* pos2;
-  const float* layer;   // packed EGCL layer
-  int nf;
-  float dt, cw;
-  uint32_t* mask;       // [A]
-  int32_t* idmap;       // [A] molecule-local labels (-1 past the surviving images)
-  int32_t* npairs;      // [A] pair words of row a
-  int32_t* cntrow;      // [A] edges of row a (with multiplicity)
-  uint32_t* pairs;      // [A][max_n]
-  int max_n;
-  int32_t* blk_start;   // [M + 1] first row block of molecule m
-  float* aabb;          // [M][6] bounding box of the molecule's positions (this layer)
-  int rbl;              // rows per block (4 .. 32; the host picks it to fill the CUs)
-  float* ldj_blk;       // [blocks] log|detJ| per row block
-  float* Qo;            // EGCL mode outputs (else null)
-  float* Fo;
-  float* Go;
-  int32_t* err;
-  int num_mols, num_atoms;
-};
-
-// largest m with ptr[m] <= x (ptr non-decreasing, ptr[0] = 0 <= x < ptr[count])
-__device__ __forceinline__ int seg_of(const int32_t* __restrict__ ptr, int count, int x) {
-  int lo = 0, hi = count;
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (ptr[mid] <= x) lo = mid;
-    else hi = mid;
-  }
-  return lo;
-}
+#include "enflow_large.h"
 
 __device__ __forceinline__ int wave_sum_i(int v) {
 #pragma unroll
@@ -323,6 +282,8 @@ __global__ void __launch_bounds__(BLOCK) lg_pairs_kernel(LgArgs B) {
         }
         const uint64_t bal = __ballot(c > 0);
         if (c > 0) out[np[k] + __popcll(bal & lt)] = ((uint32_t)jl << 5) | ((uint32_t)c << 27);
+        if (B.smap && ql < qn)   // training backward: column q's slot in the row (dense, coalesced)
+          B.smap[(size_t)a * B.max_n + q0 + ql] = c > 0 ? np[k] + __popcll(bal & lt) : -1;
         np[k] += __popcll(bal);
         edges[k] += c;
       }
@@ -401,9 +362,28 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   if constexpr (PREC != PREC_F32) node_phase_x3(sm, B.layer, L, rb, nf, tid, 0, rb);
   else node_phase(sm, B.layer, L, rb, nf, tid, 0, rb);
 
+  const bool tape = mode == 0 && B.tape != nullptr;
+  if (tape) {   // training tape (as the fused kernel's): layer-input h / pos, message sums, Q
+    const TapeLayout T = tape_layout(B.num_atoms, nf, H, B.n_layers);
+    const size_t la = (size_t)B.layer_idx * B.num_atoms + g0;
+    float* hx = B.tape + T.hx + la * T.ldhx;
+    for (int e = tid; e < rb * T.ldhx; e += BLOCK) {
+      const int a = e / T.ldhx, c = e - a * T.ldhx;
+      hx[e] = c < nf ? sm.h[a * NFP + c] : sm.agg[a * AST + (c - nf)];
+    }
+    for (int e = tid; e < rb * 3; e += BLOCK) B.tape[T.pos + la * 3 + e] = sm.pos[e];
+    for (int a = tid; a < rb; a += BLOCK) B.tape[T.q + la + a] = sm.Q[a];
+    if (tid == 0) atomicAdd(B.pair_rows + B.layer_idx, (tot + 31) & ~31);   // the backward's pair rows
+  }
   float ldj = 0.f;
   for (int a = tid; a < rb; a += BLOCK) {
     const size_t ga = (size_t)(g0 + a);
+    if (tape) {   // layer-input g / vel, read before the update below overwrites them (same thread)
+      const TapeLayout T = tape_layout(B.num_atoms, nf, H, B.n_layers);
+      const size_t la = (size_t)B.layer_idx * B.num_atoms + ga;
+      for (int qf = 0; qf < nf; ++qf) B.tape[T.g + la * nf + qf] = B.g[ga * nf + qf];
+      for (int d = 0; d < 3; ++d) B.tape[T.vel + la * 3 + d] = B.vel[ga * 3 + d];
+    }
     const float q = sm.Q[a];
     const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);   // helpers.py:63-70
     float F[3];
@@ -523,9 +503,7 @@ __global__ void __launch_bounds__(BLOCK) lg_ldj_kernel(LgArgs B, float* ldj_mol,
 static inline hipStream_t LS(void* s) { return reinterpret_cast<hipStream_t>(s); }
 static const double kLog2PiL = 1.8378770664093453;
 
-struct LgWorkspace { size_t mask, idmap, npairs, cntrow, blk_start, aabb, ldj_blk, pos2, h2, pairs, total; };
-static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
-static LgWorkspace lg_workspace(int num_mols, int num_atoms, int max_n, int nf) {
+LgWorkspace lg_workspace(int num_mols, int num_atoms, int max_n, int nf) {
   LgWorkspace W;
   const size_t A = (size_t)num_atoms, NB = (size_t)num_atoms / 4 + num_mols + 1;   // blocks of >= 4 rows
   size_t o = 0;
@@ -573,20 +551,31 @@ static void lg_layer(int H, int prec, int grid, hipStream_t st, const LgArgs& B,
   else lg_layer_prec<128>(prec, grid, st, B, mode);
 }
 
-// images -> id_mapping -> pair words -> layer, for one layer
-static void lg_one_layer(int H, int prec, hipStream_t st, LgArgs& B, int rev, int mode) {
+// images -> id_mapping -> pair words (reverse: after the pre-network half step)
+static void lg_search_rev(hipStream_t st, const LgArgs& B, int rev) {
   const int A = B.num_atoms;
   ENFLOW_TIMED("lg_images_kernel", st, hipLaunchKernelGGL(lg_images_kernel, dim3((A + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, B, rev));
   ENFLOW_TIMED("lg_idmap_kernel", st, hipLaunchKernelGGL(lg_idmap_kernel, dim3(B.num_mols), dim3(IDB), 0, st, B));
-  const int grid = A / B.rbl + B.num_mols + 1;   // >= the number of row blocks
-  ENFLOW_TIMED("lg_pairs_kernel", st, hipLaunchKernelGGL(lg_pairs_kernel, dim3(grid), dim3(BLOCK), 0, st, B));
-  lg_layer(H, prec, grid, st, B, mode);
+  ENFLOW_TIMED("lg_pairs_kernel", st, hipLaunchKernelGGL(lg_pairs_kernel, dim3(lg_grid(B)), dim3(BLOCK), 0, st, B));
+}
+void lg_search(hipStream_t st, const LgArgs& B) {
+  if (B.num_atoms > 0) lg_search_rev(st, B, 0);
+}
+void lg_setup(hipStream_t st, const LgArgs& B) {
+  hipLaunchKernelGGL(lg_setup_kernel, dim3(1), dim3(BLOCK), 0, st, B.mol_ptr, B.num_mols, B.rbl,
+                     const_cast<int32_t*>(B.blk_start));
+}
+
+// images -> id_mapping -> pair words -> layer, for one layer
+static void lg_one_layer(int H, int prec, hipStream_t st, LgArgs& B, int rev, int mode) {
+  lg_search_rev(st, B, rev);
+  lg_layer(H, prec, lg_grid(B), st, B, mode);
 }
 
 // rows per block: the largest of 32 / 16 / 8 / 4 that still gives >= 2
 // workgroups per CU (a single 2944-atom box: 4 rows, ~740 blocks; a batch of
 // many mid-size molecules: 32).  ENFLOW_LARGE_ROWS overrides (A/B runs).
-static int lg_rows(int num_atoms) {
+int lg_rows(int num_atoms) {
   if (const char* e = getenv("ENFLOW_LARGE_ROWS")) {
     const int v = atoi(e);
     if (v == 4 || v == 8 || v == 16 || v == 32) return v;
@@ -596,7 +585,7 @@ static int lg_rows(int num_atoms) {
   return 4;
 }
 
-static LgArgs lg_args(int num_mols, int num_atoms, int max_n, int nf, const int32_t* mol_ptr, const float* r_cut,
+LgArgs lg_args(int num_mols, int num_atoms, int max_n, int nf, const int32_t* mol_ptr, const float* r_cut,
                       const float* box, float* h, float* g, float* pos, float* vel, float dt, float cw,
                       int32_t* err, void* ws) {
   const LgWorkspace W = lg_workspace(num_mols, num_atoms, max_n, nf);
@@ -636,19 +625,26 @@ int enflow_lf_forward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, 
                                 int dequant_kind, const float* dequant, const float* noise,
                                 float dequant_scale, float dt, float cw,
                                 float* ldj_mol, float* ldj_total, int32_t* err_flag, int gemm_precision,
+                                float* tape, int32_t* pair_rows,
                                 void* workspace, int64_t workspace_bytes, void* stream) {
   int rc = lg_check(num_mols, num_atoms, max_mol_atoms, nf, H, gemm_precision);
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
       (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant) || !workspace || !ldj_mol || !ldj_total || !err_flag)
     return -1;
+  // the tape feeds the fp32-accurate backward (enflow_lf_backward_large_f32)
+  if (tape && (!pair_rows || (gemm_precision & 0xff) == ENFLOW_PREC_BF16)) return -1;
   if (workspace_bytes < enflow_lf_large_workspace_size(num_mols, num_atoms, max_mol_atoms, nf)) return -6;
   const hipStream_t st = LS(stream);
   LgArgs B = lg_args(num_mols, num_atoms, max_mol_atoms, nf, mol_ptr, r_cut, box, h, g, pos, vel, dt, cw,
                      err_flag, workspace);
-  const int grid_blk = num_atoms / B.rbl + num_mols + 1;
+  const int grid_blk = lg_grid(B);
+  B.tape = tape;
+  B.pair_rows = pair_rows;
+  B.n_layers = n_layers;
+  if (tape && n_layers > 0 && hipMemsetAsync(pair_rows, 0, (size_t)n_layers * 4, st) != hipSuccess) return -2;
   if (num_mols > 0) {
-    hipLaunchKernelGGL(lg_setup_kernel, dim3(1), dim3(BLOCK), 0, st, mol_ptr, num_mols, B.rbl, B.blk_start);
+    lg_setup(st, B);
     if (H == 32) hipLaunchKernelGGL((lg_dequant_kernel<32>), dim3(grid_blk), dim3(BLOCK), 0, st, B, dequant_kind, dequant, noise, dequant_scale);
     else if (H == 64) hipLaunchKernelGGL((lg_dequant_kernel<64>), dim3(grid_blk), dim3(BLOCK), 0, st, B, dequant_kind, dequant, noise, dequant_scale);
     else hipLaunchKernelGGL((lg_dequant_kernel<128>), dim3(grid_blk), dim3(BLOCK), 0, st, B, dequant_kind, dequant, noise, dequant_scale);
@@ -656,6 +652,7 @@ int enflow_lf_forward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, 
     float *cur_h = h, *cur_pos = pos, *nxt_h = B.h2, *nxt_pos = B.pos2;
     for (int l = 0; l < n_layers; ++l) {
       B.layer = layers + (size_t)l * stride;
+      B.layer_idx = l;
       B.h = cur_h; B.pos = cur_pos; B.h2 = nxt_h; B.pos2 = nxt_pos;
       lg_one_layer(H, gemm_precision, st, B, 0, 0);
       float* t = cur_h; cur_h = nxt_h; nxt_h = t;

@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 6
+#define ENFLOW_ABI 7
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8

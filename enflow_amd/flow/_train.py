@@ -33,7 +33,8 @@ class _FlowFunction(torch.autograd.Function):
         h_in = h.detach().clone()
         hw, gw, pw, vw = (t.detach().clone() for t in (h, g, pos, vel))
         tape = torch.empty(max(L.enflow_lf_tape_size(A, nf, hid, n_layers), 1), dtype=torch.float32, device=dev)
-        counts = torch.zeros(max(n_layers * M, 1), dtype=torch.int32, device=dev)
+        # fused: unique pairs [n_layers][M]; large: the backward's pair rows per layer
+        counts = torch.zeros(max(n_layers * (1 if meta["large"] else M), 1), dtype=torch.int32, device=dev)
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -93,19 +94,36 @@ class _FlowFunction(torch.autograd.Function):
         if kind == _lib.DEQUANT_ARGMAX:
             dq_raw = ctx.dq_raw
             grad_dq = torch.empty_like(dq_raw)
-        prb = meta["pair_row_bound"]
-        wsb = L.enflow_lf_backward_workspace_size(M, A, nf, hid, n_layers, prb)
-        if wsb < 0:
-            raise _lib.HipPathError("enflow_lf_backward_workspace_size rejected the batch")
-        ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
-        _lib.check(L.enflow_lf_backward_f32(
-            M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
-            _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw),
-            n_layers, kind | (_lib.EGCL_VARIANTS if flow._has_variants() else 0), _lib.ptr(dq_raw), _lib.ptr(h_in), _lib.ptr(meta["noise"]), float(flow.dt), cw,
-            _lib.ptr(ah), _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj),
-            _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
-            _lib.stream_ptr(dev)), "enflow_lf_backward_f32")
+        kindv = kind | (_lib.EGCL_VARIANTS if flow._has_variants() else 0)
+        if meta["large"]:
+            # the forward counted each layer's pair rows on the device: size the
+            # workspace by their maximum (one small read; large systems only)
+            prb = int(counts[:max(n_layers, 1)].max().item()) if n_layers else 0
+            wsb = L.enflow_lf_backward_large_workspace_size(M, A, meta["max_n"], nf, hid, prb)
+            if wsb < 0:
+                raise _lib.HipPathError("enflow_lf_backward_large_workspace_size rejected the batch")
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            _lib.check(L.enflow_lf_backward_large_f32(
+                M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw), n_layers,
+                kindv, _lib.ptr(dq_raw), _lib.ptr(h_in), _lib.ptr(meta["noise"]), float(flow.dt), cw,
+                _lib.ptr(ah), _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj),
+                _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
+                _lib.stream_ptr(dev)), "enflow_lf_backward_large_f32")
+        else:
+            prb = meta["pair_row_bound"]
+            wsb = L.enflow_lf_backward_workspace_size(M, A, nf, hid, n_layers, prb)
+            if wsb < 0:
+                raise _lib.HipPathError("enflow_lf_backward_workspace_size rejected the batch")
+            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            _lib.check(L.enflow_lf_backward_f32(
+                M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd),
+                _lib.ptr(raw), n_layers, kindv, _lib.ptr(dq_raw), _lib.ptr(h_in), _lib.ptr(meta["noise"]),
+                float(flow.dt), cw, _lib.ptr(ah), _lib.ptr(ag), _lib.ptr(apos), _lib.ptr(avel), _lib.ptr(aldj),
+                _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
+                _lib.stream_ptr(dev)), "enflow_lf_backward_f32")
         if meta["check_errors"]:
             # the forward already validated this batch's geometry; the backward's
             # word is read at the next check instead of stalling the host here
@@ -138,32 +156,6 @@ class _FlowFunction(torch.autograd.Function):
         return (None, None, gh_in, ag, apos, avel) + tuple(grads)
 
 
-def trainable_batch(data):
-    """True if the HIP backward covers the batch (every molecule <= the
-    backward's whole-molecule pair-list limit)."""
-    N = torch.as_tensor(data.N)
-    return (int(N.max()) if N.numel() else 0) <= _lib.TRAIN_MAX_ATOMS
-
-
-class _Untrainable(torch.autograd.Function):
-    """Identity on the flow outputs whose backward raises: the grad-enabled
-    forward of a batch the HIP backward does not cover."""
-
-    @staticmethod
-    def forward(ctx, h, g, pos, vel, ldj, *params):
-        return h.clone(), g.clone(), pos.clone(), vel.clone(), ldj.clone()
-
-    @staticmethod
-    def backward(ctx, *grads):
-        raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
-
-
-def guard_untrainable(flow, data, ldj):
-    params = [p for p in flow.parameters() if p.requires_grad]
-    data.h, data.g, data.pos, data.vel, ldj = _Untrainable.apply(data.h, data.g, data.pos, data.vel, ldj, *params)
-    return data, ldj
-
-
 _warned_bf16 = []
 
 
@@ -180,8 +172,10 @@ def flow_forward_train(flow, data, noise, check_errors):
             noise = torch.rand(s["h"].shape, device=dev, dtype=torch.float32)
     else:
         noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+    large = s["max_n"] > _lib.TRAIN_MAX_ATOMS   # past the fused backward: large-system training kernels
     meta = dict(box=s["box"], r_cut=s["r_cut"], mol_ptr=s["mol_ptr"], max_n=s["max_n"], noise=noise,
-                check_errors=check_errors, pair_row_bound=pair_row_bound(data.N))
+                check_errors=check_errors, large=large,
+                pair_row_bound=0 if large else pair_row_bound(data.N))
     params = [p for n in flow.networks for _, p in n.named_parameters()]
     if isinstance(flow.dequantize, ArgMax):
         params += list(flow.dequantize.parameters())
@@ -220,8 +214,6 @@ class _NLLFunction(torch.autograd.Function):
     def backward(ctx, gloss):
         h, g, pos, vel = ctx.saved_tensors
         nll, meta = ctx.nll, ctx.meta
-        if meta["max_n"] > _lib.TRAIN_MAX_ATOMS:
-            raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
         L = _lib.lib()
         dev = h.device
         M = meta["mol_ptr"].numel() - 1

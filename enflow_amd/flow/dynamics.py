@@ -152,16 +152,17 @@ class LFIntegrator(BaseFlow):
         dq = self.dequantize.packed(dev) if kind == _lib.DEQUANT_ARGMAX else None
         scale = float(getattr(self.dequantize, "dequant_scale", 1.0)) if kind == _lib.DEQUANT_FLOOR else 0.0
         L = _lib.lib()
-        if _lib.is_large(max_mol_atoms):
-            if tape is not None:
-                raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
+        # training past the fused backward's molecule size records its tape on the
+        # large-system path (pair_counts then holds the per-layer pair rows)
+        if _lib.is_large(max_mol_atoms) or (tape is not None and max_mol_atoms > _lib.TRAIN_MAX_ATOMS):
             ws = _lib.large_workspace(mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, dev)
             _lib.check(L.enflow_lf_forward_large_f32(
                 mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
                 _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
                 _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
                 _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
-                _lib.ptr(err), prec, _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)),
+                _lib.ptr(err), prec, _lib.ptr(tape), _lib.ptr(pair_counts if tape is not None else None),
+                _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)),
                 "enflow_lf_forward_large_f32")
             return
         _lib.check(L.enflow_lf_forward_f32(
@@ -210,20 +211,12 @@ class LFIntegrator(BaseFlow):
         draw (N(0,1) for ArgMax, U[0,1) for Floor), shape h.shape.
 
         With autograd enabled and trainable parameters the outputs carry a
-        grad_fn whose backward is the HIP backward (enflow_lf_backward_f32),
+        grad_fn whose backward is the HIP backward (enflow_lf_backward_f32;
+        batches with molecules past 64 atoms: enflow_lf_backward_large_f32),
         so the reference's ``loss.backward()`` / optimiser loop runs unchanged."""
         if self._needs_grad():
-            from ._train import flow_forward_train, trainable_batch, guard_untrainable
-            if trainable_batch(data):
-                return flow_forward_train(self, data, noise, check_errors)
-            # past the HIP backward's molecule size: run the inference kernels (the
-            # reference's Main.generate calls model(out) with autograd on, main.py:275);
-            # only an actual loss.backward() through these outputs raises
-            warnings.warn("enflow_amd: " + _lib.LARGE_TRAIN_MSG + "; this forward is not differentiable "
-                          "(loss.backward() through it raises NotImplementedError)", RuntimeWarning, stacklevel=2)
-            with torch.no_grad():
-                out, ldj = self.forward(data, noise=noise, check_errors=check_errors)
-            return guard_untrainable(self, out, ldj)
+            from ._train import flow_forward_train
+            return flow_forward_train(self, data, noise, check_errors)
         s = self._state(data)
         dev = s["dev"]
         kind = self._dequant_kind()

@@ -51,7 +51,9 @@ extern "C" {
 #define ENFLOW_DEQUANT_FLOOR  2  /* enflow/nn/floor.py  */
 
 /* ABI version of this header; bump on any signature or error-semantics change (6: ENFLOW_ERR_RANGE,
- * bf16 + tape rejected, NaN-poisoned gradients on a backward error, enflow_timing_*). */
+ * bf16 + tape rejected, NaN-poisoned gradients on a backward error, enflow_timing_*; 7: training
+ * on large systems -- tape / pair_rows of enflow_lf_forward_large_f32, enflow_lf_backward_large_f32,
+ * enflow_alchemical_nll_backward_f32 for any molecule size). */
 int enflow_abi_version(void);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept. */
@@ -158,11 +160,18 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
  * enflow_lf_reverse_f32 / enflow_egcl_forward_f32 (LFIntegrator.forward /
  * .reverse, enflow/flow/dynamics.py:10-37; EGCL.forward, enflow/nn/egcl.py:76-92;
  * neighbour list enflow/data/base.py:122-144), any molecule size below 2^22
- * atoms, without the training tape.  Each layer runs as grid-wide launches
+ * atoms.  Each layer runs as grid-wide launches
  * (image masks, id_mapping, pair words, one workgroup per 32-row block), so
  * `workspace` (device, enflow_lf_large_workspace_size bytes, no
  * initialisation needed) holds the per-layer neighbour list: 4 x max_mol_atoms
  * bytes per atom plus O(atoms).  Returns -6 if workspace_bytes is too small.
+ *
+ * Training (enflow_lf_forward_large_f32 with tape != NULL; any molecule size,
+ * also 65..256-atom molecules the fused kernels run at inference): tape of
+ * enflow_lf_tape_size floats (the same layout as enflow_lf_forward_f32's) and
+ * pair_rows [n_layers] (out; zeroed here) = per layer the backward's pair rows
+ * (sum over row blocks of the block's pair words rounded up to 32); its
+ * maximum over layers is the pair_row_bound of enflow_lf_backward_large_f32.
  * ---------------------------------------------------------------------- */
 int64_t enflow_lf_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int node_nf);
 
@@ -173,6 +182,7 @@ int enflow_lf_forward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, 
                                 int dequant_kind, const float* dequant, const float* noise,
                                 float dequant_scale, float dt, float coords_weight,
                                 float* ldj_mol, float* ldj_total, int32_t* err_flag, int gemm_precision,
+                                float* tape, int32_t* pair_rows,
                                 void* workspace, int64_t workspace_bytes, void* stream);
 
 int enflow_lf_reverse_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
@@ -311,6 +321,29 @@ int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int n
                            float* grad_layers, float* grad_dequant,
                            void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
                            int32_t* err_flag, void* stream);
+
+/*
+ * LFIntegrator.forward backward for large systems (molecules past 64 atoms;
+ * the reference trains the LJ / simulated boxes of enflow/data/lj.py:32-89
+ * through enflow/main.py:212-223).  Same arguments and results as
+ * enflow_lf_backward_f32; tape from enflow_lf_forward_large_f32 on the same
+ * inputs; pair_row_bound >= max over layers of its pair_rows (a smaller bound
+ * sets ENFLOW_ERR_TOO_MANY_ATOMS and NaN-poisons the gradients).  Per layer the
+ * neighbour list of the taped positions is rebuilt with the forward's kernels;
+ * the column-side adjoints are summed per column in a fixed order (bitwise
+ * reproducible).  Workspace: O(max_mol_atoms x atoms) + O(pair_row_bound).
+ */
+int64_t enflow_lf_backward_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int node_nf,
+                                                int hidden_nf, int64_t pair_row_bound);
+int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                                 const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
+                                 const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                                 int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                                 float dt, float coords_weight,
+                                 float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                                 float* grad_layers, float* grad_dequant,
+                                 void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                                 int32_t* err_flag, void* stream);
 
 /* ------------------------------------------------------------------------
  * Standalone module backward passes (the reference's EGCL and ArgMax are

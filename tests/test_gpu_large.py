@@ -91,16 +91,27 @@ def test_large_flow_forward_and_roundtrip(prec):
     assert rel_err(back.vel.cpu().numpy(), b["vel"]) < 1e-4      # round trip
 
 
-def test_large_training_is_rejected_cleanly():
-    """The training backward keeps whole-molecule pair lists (<= 64 atoms): a
-    grad-enabled forward of a 100-atom molecule runs the inference kernels and
-    warns; loss.backward() through it raises NotImplementedError."""
+def test_training_past_64_atoms_vs_oracle():
+    """Molecules of 65..256 atoms (the row-blocked kernels' range at inference)
+    train through the large-system tape and backward: gradients of a ragged
+    [100, 22] batch vs the float64 gradient oracle, 1e-4 normwise."""
+    from oracle import enflow_oracle_grad as OG
     from enflow_amd.data import Data
     from enflow_amd.flow import Alchemical_NLL
     b = _batch([100, 22], 8)
-    model = _model(32, 5, 1, 9)
-    with pytest.warns(RuntimeWarning):
-        o, ldj = model(Data.from_arrays(b, device=DEV))
-    assert o.pos.requires_grad
-    with pytest.raises(NotImplementedError):
-        Alchemical_NLL(kBT=1.0, softening=0.1)(o, ldj).backward()
+    model = _model(64, 5, 2, 9)
+    eps = np.random.default_rng(10).normal(size=b["h"].shape).astype(np.float32)
+    model.zero_grad(set_to_none=True)
+    o, ldj = model(Data.from_arrays(b, device=DEV), noise=torch.tensor(eps, device=DEV))
+    loss = Alchemical_NLL(kBT=1.0, softening=0.1)(o, ldj)
+    loss.backward()
+    layers = [{k: v.detach().double().cpu().numpy() for k, v in n.named_parameters()} for n in model.networks]
+    dq = {k: v.detach().double().cpu().numpy() for k, v in model.dequantize.named_parameters()}
+    rloss, _, gl, gd, _ = OG.train_loss_and_grads(layers, dq, b, eps.astype(np.float64), model.dt, 1.0, 0.1)
+    assert abs(float(loss) - rloss) <= 1e-5 * abs(rloss)
+    nw = lambda a, r: float(np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-300))  # noqa: E731
+    errs = {f"p{i}.{k}": nw(p.grad.cpu().double().numpy(), gl[i][k])
+            for i, n in enumerate(model.networks) for k, p in n.named_parameters()}
+    errs.update({f"dq.{k}": nw(p.grad.cpu().double().numpy(), gd[k]) for k, p in model.dequantize.named_parameters()})
+    print("100+22-atom training: max normwise grad err", f"{max(errs.values()):.2e}")
+    assert max(errs.values()) <= 1e-4, {k: v for k, v in errs.items() if v > 1e-4}
