@@ -591,6 +591,62 @@ def run_lj(args, world, rank, device, dist):
         print(json.dumps(line), flush=True)
 
 
+LJ_TRAIN_METRIC = "LJ-box training steps/sec (2944-atom periodic box, 8 layers, H=128: forward + NLL + backward + Adam)"
+
+
+def run_lj_train(args, world, rank, local, device, dist):
+    """Training on the reference's LJ system (enflow/data/lj.py:32-89 boxes
+    through enflow/main.py:212-223): one 2944-atom periodic box per GPU, 8
+    layers, hidden 128; the large-system tape and backward
+    (enflow_lf_forward_large_f32 / enflow_lf_backward_large_f32).  Not a
+    BASELINE.json config: reported for the large-system training path."""
+    from enflow_amd.data.synthetic import make_lj_systems, default_kBT
+    from enflow_amd.flow import Alchemical_NLL
+    from enflow_amd.data import Data
+    n = args.atoms or 2944
+    b = make_lj_systems([n], seed=4000 + rank, nf=NF)
+    b["pos"] = b["pos"] - np.round(b["pos"] / b["box"]) * b["box"]
+    model = build_model(device, LAYERS)
+    net = model
+    if dist:
+        from torch.nn.parallel import DistributedDataParallel as DDP
+        net = DDP(model, device_ids=[local])
+    opt = torch.optim.Adam(model.parameters(), lr=1e-5)
+    nll = Alchemical_NLL(kBT=default_kBT(), softening=0.1)
+    base = Data.from_arrays(b, device=device)
+    noise = torch.empty_like(base.h)
+    gen = torch.Generator(device).manual_seed(rank)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        torch.randn(noise.shape, generator=gen, out=noise)
+        out, ldj = net(base._replace(), noise=noise)
+        loss = nll(out, ldj)
+        loss.backward()
+        opt.step()
+        return loss
+
+    losses = []
+    elapsed = timed(lambda: losses.append(step()), args.steps, args.warmup, dist, device)
+    kt = kernel_times(step, max(args.steps, 3))
+    from enflow_amd import _lib as L_
+    L_.check_pending()
+    if rank == 0:
+        line = {
+            "metric": LJ_TRAIN_METRIC, "value": world * args.steps / elapsed, "unit": "box-training-steps/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32 (f16x3 GEMMs)",
+            "data": f"synthetic ({n}-atom LJ box, density 0.8, r_cut 2.5 sigma, random-init weights)",
+            "config": {"workload": f"lf_train_1x{n}lj_L{LAYERS}_H{HID}_nf{NF}_f32", "atoms": n,
+                       "coupling_layers": LAYERS, "hidden_nf": HID, "node_nf": NF,
+                       "parallelism": f"independent boxes x{world}, DDP grad all-reduce" if world > 1
+                       else "single GPU"},
+            "kernels": kt, "final_loss": float(losses[-1]) if losses else None, "cpu_baseline": None,
+        }
+        print(json.dumps(line), flush=True)
+
+
 def self_launch(n, argv):
     """Start N ranks under torch.distributed.run (a child process: this one has
     not touched the GPU) and return its exit code."""
@@ -613,10 +669,11 @@ def main():
     ap.add_argument("--cpu-per-core", type=int, default=192,
                     help="cpu_baseline sample: molecules per host core (16 cores: ~15 s)")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--mode", choices=("forward", "generate", "chain", "train", "lj"), default="forward",
+    ap.add_argument("--mode", choices=("forward", "generate", "chain", "train", "lj", "lj_train"), default="forward",
                     help="forward: the headline metric (configs[1]); generate: configs[2] (bf16 reverse); "
                          "chain: configs[4] (256-atom chains, 16 layers); train: configs[3] per GPU; "
-                         "lj: example/generate.yaml's 2944-atom LJ box (large-system kernels)")
+                         "lj: example/generate.yaml's 2944-atom LJ box (large-system kernels); "
+                         "lj_train: a training step on that box")
     ap.add_argument("--atoms", type=int, default=None,
                     help="train mode: atoms per molecule (default 64); lj mode: atoms per box (default 2944)")
     args = ap.parse_args()
@@ -650,6 +707,8 @@ def main():
         run_train(args, world, rank, local, device, dist)
     elif args.mode == "lj":
         run_lj(args, world, rank, device, dist)
+    elif args.mode == "lj_train":
+        run_lj_train(args, world, rank, local, device, dist)
     else:
         run_flow(args, world, rank, device, dist, cpu)
     if dist:

@@ -69,6 +69,9 @@ SIGNATURES = {
     "enflow_egcl_backward_workspace_size": (_i64, [_i, _i, _i, _i, _i64]),
     "enflow_egcl_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p, _p,
                                       _p, _p, _p, _p, _i64, _i64, _p, _p]),
+    "enflow_egcl_backward_large_workspace_size": (_i64, [_i, _i, _i, _i, _i, _i64]),
+    "enflow_egcl_backward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _i, _f, _p, _p,
+                                            _p, _p, _p, _p, _p, _i64, _i64, _p, _p]),
     "enflow_argmax_backward_workspace_size": (_i64, [_i, _i, _i]),
     "enflow_argmax_backward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i64, _p]),
     "enflow_timing_enable": (_i, [_i]),
@@ -126,8 +129,6 @@ def require_gpu(t):
 # size; batches with larger molecules train through the large-system kernels
 # (enflow_lf_forward_large_f32 with a tape, enflow_lf_backward_large_f32)
 TRAIN_MAX_ATOMS = 64
-LARGE_TRAIN_MSG = (f"the standalone EGCL backward handles molecules of <= {TRAIN_MAX_ATOMS} atoms (the flow "
-                   "trains any size)")
 _large_ws = {}
 
 

@@ -1700,7 +1700,7 @@ __global__ void __launch_bounds__(BLOCK) lg_bwd_offsets_kernel(const int32_t* mo
 // partial column sums: thread = column atom q of its molecule, blockIdx.y = a
 // chunk of LG_RC rows; the rows' slots of q (smap, coalesced over q) locate the
 // pair's column adjoints in colc; rows in increasing order -> deterministic
-constexpr int LG_RC = 256;
+constexpr int LG_RC = 64;
 __global__ void __launch_bounds__(BLOCK) lg_colsum_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
                                                           int max_n, const int32_t* smap, const int32_t* rowstart,
                                                           const float* colc, int nf, float* part) {
@@ -1727,29 +1727,31 @@ __global__ void __launch_bounds__(BLOCK) lg_colsum_kernel(const int32_t* mol_ptr
 }
 
 // column label c = id_mapping[q] (base.py:137): atom c receives the column sums
-// of every q mapped to it, q and chunks in increasing order
+// of every q mapped to it, q and chunks in increasing order.  One wave per label:
+// the lanes test 64 q at a time, the matches are taken in q order (ballot bits),
+// lane k < nf + 3 sums component k
 __global__ void __launch_bounds__(BLOCK) lg_colfinal_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
                                                             const int32_t* idmap, const float* part, int nch,
                                                             int nf, float* ah, float* apos) {
-  const int c = blockIdx.x * BLOCK + threadIdx.x;
-  if (c >= num_atoms) return;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (c >= num_atoms) return;   // wave-uniform
   const int m = seg_of(mol_ptr, num_mols, c);
   const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0, cl = c - a0;
-  float acc[NFMAX + 3];
-#pragma unroll
-  for (int k = 0; k < NFMAX + 3; ++k) acc[k] = 0.f;
-  for (int q = 0; q < n; ++q) {
-    if (idmap[a0 + q] != cl) continue;
-    for (int ch = 0; ch < nch; ++ch) {
-      const float* o = part + ((size_t)ch * num_atoms + a0 + q) * CSTR;
-      for (int f = 0; f < nf; ++f) acc[f] += o[f];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) acc[NFMAX + d] += o[NFMAX + d];
+  const int comp = lane < nf ? lane : (lane >= NFMAX && lane < NFMAX + 3 ? lane : -1);
+  float acc = 0.f;
+  for (int q0 = 0; q0 < n; q0 += 64) {
+    const int q = q0 + lane;
+    uint64_t hit = __ballot(q < n && idmap[a0 + q] == cl);
+    while (hit) {   // wave-uniform loop over the matches, lowest q first
+      const int qq = q0 + __builtin_ctzll(hit);
+      hit &= hit - 1;
+      if (comp >= 0)
+        for (int ch = 0; ch < nch; ++ch) acc += part[((size_t)ch * num_atoms + a0 + qq) * CSTR + comp];
     }
   }
-  for (int f = 0; f < nf; ++f) ah[(size_t)c * nf + f] += acc[f];
-#pragma unroll
-  for (int d = 0; d < 3; ++d) apos[(size_t)c * 3 + d] += acc[NFMAX + d];
+  if (lane < nf) ah[(size_t)c * nf + lane] += acc;
+  else if (comp >= 0) apos[(size_t)c * 3 + (lane - NFMAX)] += acc;
 }
 
 // atom chunks of <= 32 for the per-atom ArgMax backward on large systems
@@ -1758,44 +1760,49 @@ __global__ void __launch_bounds__(BLOCK) chunk_ptr_kernel(int num_atoms, int chu
   if (k <= chunks) ptr[k] = min(32 * k, num_atoms);
 }
 
-// Alchemical_NLL backward for molecules past 64 atoms: thread per atom, the
-// molecule's positions from global memory (L2); same arithmetic and b order as
-// nll_bwd_kernel
+// Alchemical_NLL backward for molecules past 64 atoms: one wave per atom (lanes
+// over the molecule's other atoms, fixed butterfly reduction), positions from L2
 __global__ void __launch_bounds__(BLOCK) nll_bwd_large_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
                                                               int nf, const float* h, const float* g,
                                                               const float* pos, const float* vel, float kBT,
                                                               float softening, const float* grad_loss, float* ah,
                                                               float* ag, float* apos, float* avel,
                                                               float* adj_ldj) {
-  const int a = blockIdx.x * BLOCK + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int a = blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const float s = grad_loss ? grad_loss[0] : 1.f;
   const float invM = s / (float)num_mols;
   const float cH = invM / kBT;
-  if (a == 0) adj_ldj[0] = -invM;                                // log_px += ldj
-  if (a >= num_atoms) return;
+  if (a == 0 && lane == 0) adj_ldj[0] = -invM;                   // log_px += ldj
+  if (a >= num_atoms) return;                                    // wave-uniform
   const int m = seg_of(mol_ptr, num_mols, a);
   const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
-  for (int d = 0; d < 3; ++d) avel[(size_t)a * 3 + d] = cH * vel[(size_t)a * 3 + d];   // H = LJ + 0.5 vel^2
-  for (int q = 0; q < nf; ++q) {                                 // -log_gaussian(h), (g)
-    ah[(size_t)a * nf + q] = invM * h[(size_t)a * nf + q];
-    ag[(size_t)a * nf + q] = invM * g[(size_t)a * nf + q];
+  if (lane < 3) avel[(size_t)a * 3 + lane] = cH * vel[(size_t)a * 3 + lane];   // H = LJ + 0.5 vel^2
+  if (lane < nf) {                                               // -log_gaussian(h), (g)
+    ah[(size_t)a * nf + lane] = invM * h[(size_t)a * nf + lane];
+    ag[(size_t)a * nf + lane] = invM * g[(size_t)a * nf + lane];
   }
   const float px = pos[(size_t)a * 3], py = pos[(size_t)a * 3 + 1], pz = pos[(size_t)a * 3 + 2];
-  float f[3] = {0.f, 0.f, 0.f};
-  for (int bl = 0; bl < n; ++bl) {
-    const int b = a0 + bl;
+  float fx = 0.f, fy = 0.f, fz = 0.f;
+  for (int b = a0 + lane; b < a0 + n; b += 64) {
     if (b == a) continue;
-    const float qx = pos[(size_t)b * 3], qy = pos[(size_t)b * 3 + 1], qz = pos[(size_t)b * 3 + 2];
-    const float dx = px - qx, dy = py - qy, dz = pz - qz;
+    const float dx = px - pos[(size_t)b * 3], dy = py - pos[(size_t)b * 3 + 1], dz = pz - pos[(size_t)b * 3 + 2];
     const float d2 = dx * dx + dy * dy + dz * dz;
     if (d2 == 0.f) continue;                                     // dist_sq != 0 (loss.py:15)
     const float r = d2 + softening, ir = 1.f / r, ir2 = ir * ir, ir4 = ir2 * ir2;
     const float dEdR = 4.f * (-6.f * ir4 * ir2 * ir + 3.f * ir4);
-    f[0] += dEdR * 2.f * dx;
-    f[1] += dEdR * 2.f * dy;
-    f[2] += dEdR * 2.f * dz;
+    fx += dEdR * 2.f * dx;
+    fy += dEdR * 2.f * dy;
+    fz += dEdR * 2.f * dz;
   }
-  for (int d = 0; d < 3; ++d) apos[(size_t)a * 3 + d] = cH * f[d];
+  fx = wave_sum(fx);
+  fy = wave_sum(fy);
+  fz = wave_sum(fz);
+  if (lane == 0) {
+    apos[(size_t)a * 3 + 0] = cH * fx;
+    apos[(size_t)a * 3 + 1] = cH * fy;
+    apos[(size_t)a * 3 + 2] = cH * fz;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -2081,7 +2088,7 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
   if (num_mols < 1 || num_atoms < 0 || nf < 1 || !adj_ldj) return -1;
   const int tm = enflow_tm_begin("nll_bwd_kernel", SB(stream));
   if (max_mol_atoms > 64)
-    hipLaunchKernelGGL(nll_bwd_large_kernel, dim3((num_atoms + BLOCK) / BLOCK), dim3(BLOCK), 0, SB(stream), mol_ptr,
+    hipLaunchKernelGGL(nll_bwd_large_kernel, dim3(num_atoms / WAVES + 1), dim3(BLOCK), 0, SB(stream), mol_ptr,
                        num_mols, num_atoms, nf, h, g, pos, vel, kBT, softening, grad_loss, adj_h, adj_g, adj_pos,
                        adj_vel, adj_ldj);
   else if (max_mol_atoms <= 32)
@@ -2244,15 +2251,15 @@ int64_t enflow_lf_backward_large_workspace_size(int num_mols, int num_atoms, int
   return (int64_t)lg_bwd_ws(num_mols, num_atoms, max_mol_atoms, nf, H, pair_row_bound).total;
 }
 
-int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
-                                 const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
-                                 const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
-                                 int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
-                                 float dt, float cw,
-                                 float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
-                                 float* grad_layers, float* grad_dequant,
-                                 void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
-                                 int32_t* err_flag, void* stream) {
+static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                                  const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
+                                  const float* layers, const float* layers_bwd, const float* layers_raw,
+                                  int n_layers, int dequant_kind, const float* dequant_raw, const float* h_data,
+                                  const float* noise, float dt, float cw, float* adj_h, float* adj_g,
+                                  float* adj_pos, float* adj_vel, const float* adj_ldj, float* grad_layers,
+                                  float* grad_dequant, void* workspace, int64_t workspace_bytes,
+                                  int64_t pair_row_bound, int32_t* err_flag, void* stream, const float* eg_dQ,
+                                  const float* eg_dF, const float* eg_dG) {
   const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
   dequant_kind &= 0xff;
   const int64_t need = enflow_lf_backward_large_workspace_size(num_mols, num_atoms, max_mol_atoms, nf, H,
@@ -2302,8 +2309,8 @@ int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms,
     if (l + 2 < n_layers && hipStreamWaitEvent(st, ev(2 * (l + 2) + 1), 0) != hipSuccess) return -2;
     G.pos = const_cast<float*>(tape + T.pos + (size_t)l * num_atoms * 3);
     lg_search(st, G);
-    hipLaunchKernelGGL(lg_bwd_offsets_kernel, dim3(1), dim3(BLOCK), 0, st, mol_ptr, num_mols, G.blk_start, G.rbl,
-                       G.npairs, boff_l, tot_l);
+    ENFLOW_TIMED("lg_bwd_offsets_kernel", st, hipLaunchKernelGGL(lg_bwd_offsets_kernel, dim3(1), dim3(BLOCK), 0, st, mol_ptr, num_mols, G.blk_start, G.rbl,
+                       G.npairs, boff_l, tot_l));
     BwdArgs A{};
     A.mol_ptr = mol_ptr; A.r_cut = r_cut; A.box = box; A.tape = tape;
     A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
@@ -2320,6 +2327,7 @@ int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms,
     A.blk_start = G.blk_start; A.rbl = G.rbl; A.max_n = max_mol_atoms;
     A.npairs_g = G.npairs; A.cntrow_g = G.cntrow; A.pairs_g = G.pairs;
     A.boff = boff_l; A.rowstart = rowstart; A.colc = colc; A.prb = pair_row_bound;
+    A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
 #define CALLB(HH)                                                                                              \
   do {                                                                                                         \
     if (variants) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, true, ENFLOW_BWD_PREC, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
@@ -2330,10 +2338,10 @@ int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms,
     else CALLB(128);
 #undef CALLB
     if (num_atoms > 0) {
-      hipLaunchKernelGGL(lg_colsum_kernel, dim3(ga, W.nch), dim3(BLOCK), 0, st, mol_ptr, num_mols, num_atoms,
-                         max_mol_atoms, smap, rowstart, colc, nf, part);
-      hipLaunchKernelGGL(lg_colfinal_kernel, dim3(ga), dim3(BLOCK), 0, st, mol_ptr, num_mols, num_atoms, G.idmap,
-                         part, W.nch, nf, adj_h, adj_pos);
+      ENFLOW_TIMED("lg_colsum_kernel", st, hipLaunchKernelGGL(lg_colsum_kernel, dim3(ga, W.nch), dim3(BLOCK), 0, st, mol_ptr, num_mols, num_atoms,
+                         max_mol_atoms, smap, rowstart, colc, nf, part));
+      ENFLOW_TIMED("lg_colfinal_kernel", st, hipLaunchKernelGGL(lg_colfinal_kernel, dim3((num_atoms + WAVES - 1) / WAVES), dim3(BLOCK), 0, st, mol_ptr, num_mols, num_atoms, G.idmap,
+                         part, W.nch, nf, adj_h, adj_pos));
     }
     if (hipEventRecord(ev(2 * l), st) != hipSuccess || hipStreamWaitEvent(st2, ev(2 * l), 0) != hipSuccess)
       return -2;
@@ -2354,6 +2362,21 @@ int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms,
                      (long long)n_layers * R.total_bwd, dequant_kind == ENFLOW_DEQUANT_ARGMAX ? grad_dequant : nullptr,
                      (long long)(H * nf + H + 2 * nf * H + 2 * nf));
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                                 const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
+                                 const float* layers, const float* layers_bwd, const float* layers_raw, int n_layers,
+                                 int dequant_kind, const float* dequant_raw, const float* h_data, const float* noise,
+                                 float dt, float cw,
+                                 float* adj_h, float* adj_g, float* adj_pos, float* adj_vel, const float* adj_ldj,
+                                 float* grad_layers, float* grad_dequant,
+                                 void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                                 int32_t* err_flag, void* stream) {
+  return lf_backward_large_impl(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, tape, layers,
+                                layers_bwd, layers_raw, n_layers, dequant_kind, dequant_raw, h_data, noise, dt, cw,
+                                adj_h, adj_g, adj_pos, adj_vel, adj_ldj, grad_layers, grad_dequant, workspace,
+                                workspace_bytes, pair_row_bound, err_flag, stream, nullptr, nullptr, nullptr);
 }
 
 // ---- standalone EGCL.forward backward ------------------------------------
@@ -2389,6 +2412,38 @@ int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int
                           layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | (egcl_flags ? ENFLOW_EGCL_VARIANTS : 0),
                           nullptr, nullptr, nullptr, 0.f, cw, adj_h, ag, adj_pos, avel, zero, grad_layer, nullptr,
                           workspace, workspace_bytes, pair_row_bound, err_flag, stream, adj_Q, adj_F, adj_G);
+}
+
+// molecules past 64 atoms: the large-system backward on a one-layer tape of
+// enflow_lf_forward_large_f32 (dt 0, dequant NONE)
+int64_t enflow_egcl_backward_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                                                  int64_t pair_row_bound) {
+  const int64_t w = enflow_lf_backward_large_workspace_size(num_mols, num_atoms, max_mol_atoms, nf, H,
+                                                            pair_row_bound);
+  if (w < 0) return -1;
+  return w + (int64_t)(egcl_bwd_extra(num_atoms, nf) * sizeof(float));
+}
+
+int enflow_egcl_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                                   const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
+                                   const float* layer, const float* layer_bwd, const float* layer_raw,
+                                   int egcl_flags, float cw, const float* adj_Q, const float* adj_F,
+                                   const float* adj_G, float* adj_h, float* adj_pos, float* grad_layer,
+                                   void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                                   int32_t* err_flag, void* stream) {
+  const int64_t w = enflow_lf_backward_large_workspace_size(num_mols, num_atoms, max_mol_atoms, nf, H,
+                                                            pair_row_bound);
+  if (w < 0 || !adj_Q || !adj_F || !adj_G || !workspace) return -1;
+  if (workspace_bytes < w + (int64_t)(egcl_bwd_extra(num_atoms, nf) * sizeof(float))) return -6;
+  float* extra = reinterpret_cast<float*>(static_cast<char*>(workspace) + w);
+  float* avel = extra;
+  float* ag = avel + al64((size_t)num_atoms * 3);
+  float* zero = ag + al64((size_t)num_atoms * nf);
+  if (hipMemsetAsync(zero, 0, 64 * sizeof(float), SB(stream)) != hipSuccess) return -2;
+  return lf_backward_large_impl(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, tape, layer,
+                                layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | (egcl_flags ? ENFLOW_EGCL_VARIANTS : 0),
+                                nullptr, nullptr, nullptr, 0.f, cw, adj_h, ag, adj_pos, avel, zero, grad_layer,
+                                nullptr, workspace, w, pair_row_bound, err_flag, stream, adj_Q, adj_F, adj_G);
 }
 
 // ---- standalone ArgMax.forward backward ------------------------------------

@@ -25,7 +25,7 @@
 //
 // All arithmetic is float32; MFMA f32 is an exact fmaf chain.
 
-#include "flow_device.h"
+#include "enflow_large.h"
 
 // ---------------------------------------------------------------------------
 // packing kernels
@@ -491,21 +491,52 @@ __global__ void __launch_bounds__(BLOCK) neighbour_pairs_kernel(FlowArgs A, int 
   }
 }
 
+// Large systems: per atom i the LJ energy sum over every other atom k of its
+// molecule (each pair counted from both ends; the molecule's sum is halved),
+// one wave per atom (lanes over k, fixed butterfly reduction), positions from L2
+__global__ void __launch_bounds__(BLOCK) nll_atom_lj_kernel(const int32_t* mol_ptr, int num_mols, int num_atoms,
+                                                          const float* pos, float softening, float* part) {
+  const int lane = threadIdx.x & 63;
+  const int a = blockIdx.x * WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (a >= num_atoms) return;   // wave-uniform
+  const int m = seg_of(mol_ptr, num_mols, a);
+  const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
+  const float px = pos[(size_t)a * 3], py = pos[(size_t)a * 3 + 1], pz = pos[(size_t)a * 3 + 2];
+  float lj = 0.f;
+  for (int k = a0 + lane; k < a0 + n; k += 64) {
+    if (k == a) continue;
+    const float dx = px - pos[(size_t)k * 3], dy = py - pos[(size_t)k * 3 + 1], dz = pz - pos[(size_t)k * 3 + 2];
+    const float d2 = dx * dx + dy * dy + dz * dz;
+    if (d2 != 0.f) {
+      const float r2 = d2 + softening;
+      const float r6 = r2 * r2 * r2;
+      lj += 4.f * (1.f / (r6 * r6) - 1.f / r6);
+    }
+  }
+  lj = wave_sum(lj);
+  if (lane == 0) part[a] = lj;
+}
+
 // Alchemical_NLL per-molecule sums (loss.py:11-19, 21-24)
 template <int NMAX>
 __global__ void __launch_bounds__(BLOCK) nll_mol_kernel(const int32_t* mol_ptr, int nf, const float* h, const float* g,
-                                                      const float* pos, const float* vel, float softening, float* out) {
-  // NMAX == 0: molecules past the LDS image (large-system path) read pos from global memory
+                                                      const float* pos, const float* vel, float softening, float* out,
+                                                      const float* lj_part) {
+  // NMAX == 0: molecules past the LDS image (large-system path): the LJ sum from
+  // nll_atom_lj_kernel's per-atom partials
   __shared__ float spos_l[NMAX > 0 ? NMAX * 3 : 1];
   __shared__ float red[4][WAVES];
   const int m = blockIdx.x, tid = threadIdx.x;
   const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
-  const float* spos = NMAX > 0 ? spos_l : pos + (size_t)a0 * 3;
+  const float* spos = spos_l;
   if constexpr (NMAX > 0) {
     for (int e = tid; e < n * 3; e += BLOCK) spos_l[e] = pos[(size_t)a0 * 3 + e];
     __syncthreads();
   }
   float lj = 0.f, v2 = 0.f, h2 = 0.f, g2 = 0.f;
+  if constexpr (NMAX == 0)
+    for (int a = tid; a < n; a += BLOCK) lj += 0.5f * lj_part[a0 + a];
+  else
   for (long long e = tid; e < (long long)n * n; e += BLOCK) {
     const int i = (int)(e / n), k = (int)(e - (long long)i * n);
     if (k <= i) continue;
@@ -821,13 +852,21 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
   const int tm = enflow_tm_begin("nll_mol_kernel", S(stream));
   if (num_mols > 0) {
     if (max_mol_atoms <= 32)
-      hipLaunchKernelGGL((nll_mol_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+      hipLaunchKernelGGL((nll_mol_kernel<32>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol, nullptr);
     else if (max_mol_atoms <= 64)
-      hipLaunchKernelGGL((nll_mol_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+      hipLaunchKernelGGL((nll_mol_kernel<64>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol, nullptr);
     else if (max_mol_atoms <= MAX_ATOMS)
-      hipLaunchKernelGGL((nll_mol_kernel<256>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
-    else
-      hipLaunchKernelGGL((nll_mol_kernel<0>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol);
+      hipLaunchKernelGGL((nll_mol_kernel<256>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol, nullptr);
+    else {   // per-atom partials in stream-ordered scratch (freed behind the kernels)
+      float* part = nullptr;
+      if (hipMallocAsync(reinterpret_cast<void**>(&part), (size_t)(num_atoms > 0 ? num_atoms : 1) * 4, S(stream)) != hipSuccess)
+        return -2;
+      if (num_atoms > 0)
+        hipLaunchKernelGGL(nll_atom_lj_kernel, dim3((num_atoms + WAVES - 1) / WAVES), dim3(BLOCK), 0, S(stream),
+                           mol_ptr, num_mols, num_atoms, pos, softening, part);
+      hipLaunchKernelGGL((nll_mol_kernel<0>), dim3(num_mols), dim3(BLOCK), 0, S(stream), mol_ptr, nf, h, g, pos, vel, softening, nll_mol, part);
+      if (hipFreeAsync(part, S(stream)) != hipSuccess) return -2;
+    }
   }
   hipLaunchKernelGGL(reduce_nll_kernel, dim3(1), dim3(BLOCK), 0, S(stream), nll_mol, num_mols, num_atoms, ldj_total,
                      kBT, partition_func, loss);

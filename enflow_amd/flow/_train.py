@@ -266,8 +266,7 @@ class _EGCLFunction(torch.autograd.Function):
     def backward(ctx, gq, gf, gg):
         net, meta = ctx.net, ctx.meta
         h, pos = ctx.saved_tensors
-        if meta["max_n"] > _lib.TRAIN_MAX_ATOMS:
-            raise NotImplementedError(_lib.LARGE_TRAIN_MSG)
+        large = meta["max_n"] > _lib.TRAIN_MAX_ATOMS
         L = _lib.lib()
         dev = h.device
         A, nf, hid = h.shape[0], net.input_nf, net.hidden_nf
@@ -284,17 +283,30 @@ class _EGCLFunction(torch.autograd.Function):
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         fwd = net.packed(dev)
-        _lib.check(L.enflow_lf_forward_f32(
-            M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]), _lib.ptr(meta["box"]),
-            _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1, _lib.DEQUANT_NONE, None, None,
-            0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol), _lib.ptr(ldj), _lib.ptr(err), None, _lib.ptr(tape),
-            _lib.ptr(counts), prec, st), "enflow_lf_forward_f32 (EGCL tape)")
+        if large:   # the large-system forward records the tape and the backward's pair rows
+            lws = _lib.large_workspace(M, A, meta["max_n"], nf, dev)
+            _lib.check(L.enflow_lf_forward_large_f32(
+                M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1,
+                _lib.DEQUANT_NONE, None, None, 0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol), _lib.ptr(ldj),
+                _lib.ptr(err), prec, _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(lws), lws.numel(), st),
+                "enflow_lf_forward_large_f32 (EGCL tape)")
+        else:
+            _lib.check(L.enflow_lf_forward_f32(
+                M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1,
+                _lib.DEQUANT_NONE, None, None, 0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol), _lib.ptr(ldj),
+                _lib.ptr(err), None, _lib.ptr(tape), _lib.ptr(counts), prec, st), "enflow_lf_forward_f32 (EGCL tape)")
         raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32) for p in net.raw_parameters()] +
                         [net._att_raw(dev) if net.attention else torch.zeros(hid + 1, device=dev)])
         bwd = torch.empty(max(L.enflow_egcl_bwd_packed_size(hid, nf), 1), dtype=torch.float32, device=dev)
         _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw), hid, nf, _lib.ptr(bwd), st), "enflow_pack_egcl_bwd_f32")
-        prb = pair_row_bound(meta["N"])
-        wsb = L.enflow_egcl_backward_workspace_size(M, A, nf, hid, prb)
+        if large:
+            prb = int(counts[0].item())
+            wsb = L.enflow_egcl_backward_large_workspace_size(M, A, meta["max_n"], nf, hid, prb)
+        else:
+            prb = pair_row_bound(meta["N"])
+            wsb = L.enflow_egcl_backward_workspace_size(M, A, nf, hid, prb)
         if wsb < 0:
             raise _lib.HipPathError("enflow_egcl_backward_workspace_size rejected the batch")
         ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
@@ -308,11 +320,20 @@ class _EGCLFunction(torch.autograd.Function):
         dh = torch.empty((A, nf), dtype=torch.float32, device=dev)
         dpos = torch.empty((A, 3), dtype=torch.float32, device=dev)
         grad = torch.empty_like(raw)
-        _lib.check(L.enflow_egcl_backward_f32(
-            M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]), _lib.ptr(meta["box"]),
-            _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw), net.variant_flags(),
-            float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af), _lib.ptr(ag), _lib.ptr(dh), _lib.ptr(dpos),
-            _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err), st), "enflow_egcl_backward_f32")
+        if large:
+            _lib.check(L.enflow_egcl_backward_large_f32(
+                M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw),
+                net.variant_flags(), float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af), _lib.ptr(ag),
+                _lib.ptr(dh), _lib.ptr(dpos), _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err), st),
+                "enflow_egcl_backward_large_f32")
+        else:
+            _lib.check(L.enflow_egcl_backward_f32(
+                M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd),
+                _lib.ptr(raw), net.variant_flags(), float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af),
+                _lib.ptr(ag), _lib.ptr(dh), _lib.ptr(dpos), _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
+                st), "enflow_egcl_backward_f32")
         _lib.raise_on_err(err)
         return (None, None, dh, dpos) + tuple(layer_grads(net, grad))
 

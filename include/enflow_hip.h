@@ -368,6 +368,19 @@ int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int
                              void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
                              int32_t* err_flag, void* stream);
 
+/* The same for molecules past 64 atoms: tape / pair_rows from a one-layer
+ * enflow_lf_forward_large_f32 on the same h / pos (dequant NONE, dt 0; its
+ * pair_rows[0] = the pair_row_bound), then the large-system backward. */
+int64_t enflow_egcl_backward_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int node_nf,
+                                                  int hidden_nf, int64_t pair_row_bound);
+int enflow_egcl_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                                   const int32_t* mol_ptr, const float* r_cut, const float* box, const float* tape,
+                                   const float* layer, const float* layer_bwd, const float* layer_raw,
+                                   int egcl_flags, float coords_weight, const float* adj_Q, const float* adj_F,
+                                   const float* adj_G, float* adj_h, float* adj_pos, float* grad_layer,
+                                   void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
+                                   int32_t* err_flag, void* stream);
+
 /* ArgMax.forward backward: adjoints of z [A][nf] and of log_q [1] -> the
  * gradient of ArgMax.network's parameters (grad_dequant, raw layout of
  * enflow_pack_argmax_f32).  noise: the forward's N(0,1) draw; h: its input.

@@ -96,3 +96,45 @@ def test_egcl_training_loop_reduces_loss():
         opt.step()
         losses.append(float(loss))
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("hid,variants", [(128, {}), (64, dict(attention=True, norm_diff=True, tanh=True))])
+def test_egcl_backward_large_box_vs_oracle(hid, variants):
+    """EGCL.forward on a 300-atom periodic box (past the fused backward's
+    64-atom image: enflow_egcl_backward_large_f32) -- gradients of h, pos and
+    every parameter vs the float64 gradient oracle's EGCL (pinned to the
+    reference's loss.backward() goldens), 1e-4 normwise."""
+    from oracle import enflow_oracle as O
+    from oracle import enflow_oracle_grad as OG
+    from enflow_amd.nn import EGCL
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_lj_systems
+    b = make_lj_systems([300], nf=5, seed=61)
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        b[k] = b[k].astype(np.float32).astype(np.float64)
+    torch.manual_seed(62)
+    net = EGCL(5, 5, hid, **variants).to(DEV)
+    d = Data.from_arrays(b, device=DEV)
+    d.h.requires_grad_(True)
+    d.pos.requires_grad_(True)
+    q, f, g = net(d.h, d.edges)
+    rng = np.random.default_rng(63)
+    wq, wf, wg = rng.normal(size=(300,)), rng.normal(size=(300, 3)), rng.normal(size=(300, 5))
+    t32 = lambda a: torch.tensor(a, dtype=torch.float32, device=DEV)  # noqa: E731
+    loss = (q.reshape(-1) * t32(wq)).sum() + (f * t32(wf)).sum() + (g * t32(wg)).sum()
+    loss.backward()
+    t = lambda a: torch.tensor(np.asarray(a, dtype=np.float64))  # noqa: E731
+    P = {k: t(v.detach().cpu().numpy()).requires_grad_(True) for k, v in net.named_parameters()}
+    h64, pos64 = t(b["h"]).requires_grad_(True), t(b["pos"]).requires_grad_(True)
+    row, col, eb = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    rq, rf, rg = OG._egcl(P, h64, pos64, torch.as_tensor(row), torch.as_tensor(col), t(eb), 300,
+                          float(net.coords_weight), (bool(net.attention), bool(net.norm_diff), bool(net.tanh)))
+    rloss = (rq.reshape(-1) * t(wq)).sum() + (rf * t(wf)).sum() + (rg * t(wg)).sum()
+    rloss.backward()
+    assert abs(float(loss) - float(rloss)) <= LOSS_TOL * abs(float(rloss)) + 1e-6
+    errs = {"h": normwise(d.h.grad.cpu().numpy(), h64.grad.numpy()),
+            "pos": normwise(d.pos.grad.cpu().numpy(), pos64.grad.numpy())}
+    for k, p in net.named_parameters():
+        errs[k] = normwise(p.grad.cpu().numpy(), P[k].grad.numpy())
+    print(f"EGCL 300-atom box H={hid} {sorted(variants)}: max normwise grad err {max(errs.values()):.2e}")
+    assert max(errs.values()) <= GRAD_TOL, errs

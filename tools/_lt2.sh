@@ -1,0 +1,6 @@
+set -e
+mkdir -p gpurun_out/lt2
+timeout -k 10 400 python -u -m pytest tests/test_gpu_modules.py -x -v -s --timeout 200 --timeout-method thread > gpurun_out/lt2/modules.log 2>&1
+timeout -k 10 300 python -u bench.py --mode lj_train --steps 5 --warmup 2 > gpurun_out/lt2/lj_train.json 2> gpurun_out/lt2/lj_train.err
+timeout -k 10 300 python -u bench.py --mode lj_train --atoms 300 --steps 10 --warmup 2 > gpurun_out/lt2/lj_train300.json 2> gpurun_out/lt2/lj_train300.err
+echo done
