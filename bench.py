@@ -321,7 +321,18 @@ def cpu_baseline(per_core=192):
     with ctx.Pool(cores) as pool:
         per = pool.map(_cpu_chunk, chunks)
     wall = time.perf_counter() - t0
+    ref = None   # the reference itself (torch float64, build container; tools/ref_cpu_timing.py)
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02", "r02_reference_cpu.json")) as f:
+            r = json.load(f)
+        ref = {"value": r["configs[1]_forward"]["value"], "unit": "molecule-transforms/s",
+               "threads": r["host"]["torch_threads"], "cpu": r["host"]["cpu"],
+               "sample": r["configs[1]_forward"]["sample"],
+               "source": "profiles/r02/r02_reference_cpu.json (build container, not this host)"}
+    except (OSError, KeyError, ValueError):
+        pass
     return {"value": total / wall, "unit": "molecule-transforms/s", "cores": cores, "kind": "port",
+            "reference_torch": ref,
             "sample": f"{total} molecules x {ATOMS} atoms ({per_core} per core), {LAYERS} layers, hidden {HID}: "
                       f"numpy float64 oracle (oracle/enflow_oracle.py), one single-thread process per core, "
                       f"{wall:.1f} s wall (per-core {min(per):.1f}-{max(per):.1f} s); host CPUs visible "
