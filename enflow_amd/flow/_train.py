@@ -12,6 +12,7 @@ import torch
 
 from .. import _lib
 from ..nn.argmax import ArgMax
+from ..nn._pad import ARGMAX_HDIMS, EGCL_HDIMS, unpad_grads
 
 
 def pair_row_bound(N):
@@ -55,8 +56,7 @@ class _FlowFunction(torch.autograd.Function):
         flow.training_layers(dev)
         ctx.dq_raw = None
         if kind == _lib.DEQUANT_ARGMAX:
-            ctx.dq_raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32)
-                                    for p in flow.dequantize.parameters()])
+            ctx.dq_raw = flow.dequantize.kernel_raw(dev, hid)
         if meta["check_errors"]:
             # no host sync here: the word is read at the next check -- the start of
             # this graph's backward (before anything consumes the outputs' gradients),
@@ -129,28 +129,14 @@ class _FlowFunction(torch.autograd.Function):
             # word is read at the next check instead of stalling the host here
             _lib.defer_err(err)
         # split the flat gradients into the parameters' shapes (inputs order)
-        # per layer: the default-flag parameters in raw order, then att_nn.0 (weight,
-        # bias) in the H + 1 slots every layer carries; emitted in named order
         grads = []
         rstride = grad_layers.numel() // max(len(flow.networks), 1)
         for li, net in enumerate(flow.networks):
-            off = li * rstride
-            slices = {}
-            for name, p in net.named_parameters():
-                if not name.startswith("att_nn."):
-                    slices[name] = grad_layers[off:off + p.numel()]
-                    off += p.numel()
-            for name, p in net.named_parameters():
-                if name.startswith("att_nn."):
-                    slices[name] = grad_layers[off:off + p.numel()]
-                    off += p.numel()
-            for name, p in net.named_parameters():
-                grads.append(slices[name].view(p.shape).to(p.dtype))
+            grads += layer_grads(net, grad_layers[li * rstride:(li + 1) * rstride])
         if kind == _lib.DEQUANT_ARGMAX:
-            off = 0
-            for p in flow.dequantize.parameters():
-                grads.append(grad_dq[off:off + p.numel()].view(p.shape).to(p.dtype))
-                off += p.numel()
+            am = flow.dequantize
+            gd, _ = unpad_grads(grad_dq, list(am.named_parameters()), ARGMAX_HDIMS, am.hidden_nf, hid)
+            grads += [gd[k].contiguous().to(p.dtype) for k, p in am.named_parameters()]
         # d h of the data only exists without a learned dequantiser (z = h + noise)
         gh_in = ah if kind != _lib.DEQUANT_ARGMAX else None
         return (None, None, gh_in, ag, apos, avel) + tuple(grads)
@@ -234,20 +220,17 @@ class _NLLFunction(torch.autograd.Function):
 # (enflow/nn/argmax.py:13-25) as autograd Functions over the HIP backward
 # ---------------------------------------------------------------------------
 def layer_grads(net, flat):
-    """Split one layer's flat gradient (layers_raw layout: default-flag
-    parameters in named order, then att_nn.0 weight / bias in H + 1 slots) into
-    the module's parameters, in named_parameters() order."""
-    off = 0
-    slices = {}
-    for name, p in net.named_parameters():
-        if not name.startswith("att_nn."):
-            slices[name] = flat[off:off + p.numel()]
-            off += p.numel()
-    for name, p in net.named_parameters():
-        if name.startswith("att_nn."):
-            slices[name] = flat[off:off + p.numel()]
-            off += p.numel()
-    return [slices[name].view(p.shape).to(p.dtype) for name, p in net.named_parameters()]
+    """Split one layer's flat gradient (layers_raw layout at the kernel width:
+    default-flag parameters in named order, then att_nn.0 weight / bias in the
+    width + 1 slots) into the module's parameters, in named_parameters() order
+    (the real block of each zero-padded tensor, nn/_pad.py)."""
+    H, Hp = net.hidden_nf, net.kernel_hidden
+    g, off = unpad_grads(flat, net.raw_named(), EGCL_HDIMS, H, Hp)
+    att = [(k, p) for k, p in net.named_parameters() if k.startswith("att_nn.")]
+    if att:
+        ga, _ = unpad_grads(flat[off:], att, EGCL_HDIMS, H, Hp)
+        g.update(ga)
+    return [g[name].contiguous().to(p.dtype) for name, p in net.named_parameters()]
 
 
 class _EGCLFunction(torch.autograd.Function):
@@ -269,7 +252,7 @@ class _EGCLFunction(torch.autograd.Function):
         large = meta["max_n"] > _lib.TRAIN_MAX_ATOMS
         L = _lib.lib()
         dev = h.device
-        A, nf, hid = h.shape[0], net.input_nf, net.hidden_nf
+        A, nf, hid = h.shape[0], net.input_nf, net.kernel_hidden
         M = meta["mol_ptr"].numel() - 1
         st = _lib.stream_ptr(dev)
         prec = _lib.PREC_F16X3 | (_lib.EGCL_VARIANTS if net.variant_flags() else 0)
@@ -297,8 +280,7 @@ class _EGCLFunction(torch.autograd.Function):
                 _lib.ptr(meta["box"]), _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1,
                 _lib.DEQUANT_NONE, None, None, 0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol), _lib.ptr(ldj),
                 _lib.ptr(err), None, _lib.ptr(tape), _lib.ptr(counts), prec, st), "enflow_lf_forward_f32 (EGCL tape)")
-        raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32) for p in net.raw_parameters()] +
-                        [net._att_raw(dev) if net.attention else torch.zeros(hid + 1, device=dev)])
+        raw = torch.cat([net.kernel_raw(dev), net._att_raw(dev) if net.attention else torch.zeros(hid + 1, device=dev)])
         bwd = torch.empty(max(L.enflow_egcl_bwd_packed_size(hid, nf), 1), dtype=torch.float32, device=dev)
         _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw), hid, nf, _lib.ptr(bwd), st), "enflow_pack_egcl_bwd_f32")
         if large:
@@ -354,8 +336,8 @@ class _ArgMaxFunction(torch.autograd.Function):
         h, noise = ctx.saved_tensors
         L = _lib.lib()
         dev = h.device
-        A, nf, hid = h.shape[0], am.node_nf, am.hidden_nf
-        raw = torch.cat([p.detach().reshape(-1).to(device=dev, dtype=torch.float32) for p in am.parameters()])
+        A, nf, hid = h.shape[0], am.node_nf, am.kernel_hidden
+        raw = am.kernel_raw(dev)
         az = (torch.zeros_like(h) if gz is None else gz.detach().to(torch.float32).contiguous())
         alq = (torch.zeros(1, device=dev) if glq is None else glq.detach().to(torch.float32).reshape(1).contiguous())
         grad = torch.empty_like(raw)
@@ -365,9 +347,7 @@ class _ArgMaxFunction(torch.autograd.Function):
             meta["mol_ptr"].numel() - 1, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(h),
             _lib.ptr(raw), _lib.ptr(noise), _lib.ptr(az), _lib.ptr(alq), _lib.ptr(grad), _lib.ptr(ws), wsb,
             _lib.stream_ptr(dev)), "enflow_argmax_backward_f32")
-        grads, off = [], 0
-        for p in am.parameters():
-            grads.append(grad[off:off + p.numel()].view(p.shape).to(p.dtype))
-            off += p.numel()
+        gd, _ = unpad_grads(grad, list(am.named_parameters()), ARGMAX_HDIMS, am.hidden_nf, hid)
+        grads = [gd[k].contiguous().to(p.dtype) for k, p in am.named_parameters()]
         # h is the categorical data (one-hot, argmax.py:13): no gradient is returned for it
         return (None, None, None, None) + tuple(grads)

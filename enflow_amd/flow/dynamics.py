@@ -57,7 +57,8 @@ class LFIntegrator(BaseFlow):
             n._check_supported()
             if (n.hidden_nf, n.input_nf) != (h0, f0) or n.coords_weight != nets[0].coords_weight:
                 raise NotImplementedError("all EGCL layers must share hidden_nf, node_nf and coords_weight")
-        return h0, f0, float(nets[0].coords_weight)
+        # the kernels' hidden width (hidden_nf, or zero-padded to the next compiled one)
+        return nets[0].kernel_hidden, f0, float(nets[0].coords_weight)
 
     def _dequant_kind(self):
         d = self.dequantize
@@ -105,7 +106,7 @@ class LFIntegrator(BaseFlow):
         zpad = self._zpad
         pieces = []
         for n in self.networks:
-            pieces += [p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in n.raw_parameters()]
+            pieces.append(n.kernel_raw(device))
             pieces.append(n._att_raw(device) if n.attention else zpad)
         raw = torch.cat(pieces)
         stride = L.enflow_egcl_bwd_packed_size(hid, nf)
@@ -149,7 +150,7 @@ class LFIntegrator(BaseFlow):
         kind = self._dequant_kind()
         dev = h.device
         prec = self._prec() if prec is None else prec
-        dq = self.dequantize.packed(dev) if kind == _lib.DEQUANT_ARGMAX else None
+        dq = self.dequantize.packed(dev, hid) if kind == _lib.DEQUANT_ARGMAX else None
         scale = float(getattr(self.dequantize, "dequant_scale", 1.0)) if kind == _lib.DEQUANT_FLOOR else 0.0
         L = _lib.lib()
         # training past the fused backward's molecule size records its tape on the

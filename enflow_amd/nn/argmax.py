@@ -10,6 +10,7 @@ from torch import nn
 
 from .. import _lib
 from ..utils.helpers import one_hot, mol_ptr_from_counts
+from ._pad import ARGMAX_HDIMS, flat_padded, kernel_hidden
 
 
 class ArgMax(nn.Module):
@@ -21,16 +22,30 @@ class ArgMax(nn.Module):
         self._packed = None
         self._packed_key = None
 
-    def packed(self, device):
+    @property
+    def kernel_hidden(self):
+        """Compiled hidden width (hidden_nf zero-padded to 32 / 64 / 128, exact; nn/_pad.py)."""
+        return kernel_hidden(self.hidden_nf)
+
+    def kernel_raw(self, device, width=None):
+        """network parameters as one flat fp32 vector padded to `width` (default
+        kernel_hidden; the flow passes its layers' width)."""
+        width = width or self.kernel_hidden
+        if width is None or width < self.hidden_nf:
+            raise NotImplementedError(f"ArgMax hidden_nf {self.hidden_nf} past the kernel width {width}")
+        return flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.hidden_nf, width, device)
+
+    def packed(self, device, width=None):
+        width = width or self.kernel_hidden
         params = [p for _, p in self.named_parameters()]
-        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        key = (str(device), width) + tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is not None and self._packed_key == key:
             return self._packed
         L = _lib.lib()
-        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in params])
-        out = torch.empty(L.enflow_argmax_packed_size(self.hidden_nf, self.node_nf),
+        raw = self.kernel_raw(device, width)
+        out = torch.empty(L.enflow_argmax_packed_size(width, self.node_nf),
                           dtype=torch.float32, device=device)
-        _lib.check(L.enflow_pack_argmax_f32(_lib.ptr(raw), self.hidden_nf, self.node_nf, _lib.ptr(out),
+        _lib.check(L.enflow_pack_argmax_f32(_lib.ptr(raw), width, self.node_nf, _lib.ptr(out),
                                             _lib.stream_ptr(device)), "enflow_pack_argmax_f32")
         self._packed, self._packed_key = out, key
         return out
@@ -56,7 +71,7 @@ class ArgMax(nn.Module):
         z = torch.empty_like(hf)
         lq_mol = torch.empty(max(meta["num_mols"], 1), dtype=torch.float32, device=dev)
         lq = torch.empty(1, dtype=torch.float32, device=dev)
-        _lib.check(L.enflow_argmax_forward_f32(meta["num_mols"], n, meta["max_n"], self.node_nf, self.hidden_nf,
+        _lib.check(L.enflow_argmax_forward_f32(meta["num_mols"], n, meta["max_n"], self.node_nf, self.kernel_hidden,
                                                _lib.ptr(meta["mol_ptr"]), _lib.ptr(hf), _lib.ptr(self.packed(dev)),
                                                _lib.ptr(eps), _lib.ptr(z), _lib.ptr(lq_mol), _lib.ptr(lq),
                                                _lib.stream_ptr(dev)), "enflow_argmax_forward_f32")

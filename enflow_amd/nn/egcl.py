@@ -12,6 +12,7 @@ from torch import nn
 
 from .. import _lib
 from ..data.base import Edges
+from ._pad import EGCL_HDIMS, flat_padded, kernel_hidden
 
 
 class EGCL(nn.Module):
@@ -47,43 +48,57 @@ class EGCL(nn.Module):
         self._packed_key = None
 
     # ------------------------------------------------------------------
+    @property
+    def kernel_hidden(self):
+        """The compiled hidden width this layer runs at: hidden_nf, or the next
+        of 32 / 64 / 128 with the extra units zero-padded (exact, nn/_pad.py)."""
+        return kernel_hidden(self.hidden_nf)
+
     def hip_supported(self):
         """The HIP kernels implement every constructor flag of the reference
         (attention, norm_diff, tanh; ``clamp`` is stored and unused there too)
-        with the SiLU activation, input_nf == output_nf <= 8, hidden_nf in
-        {32, 64, 128}."""
+        with the SiLU activation, input_nf == output_nf <= 8, any hidden_nf
+        <= 128 (32 / 64 / 128 compiled, other widths zero-padded)."""
         L = _lib.lib()
+        kh = self.kernel_hidden
         return (isinstance(self.act_fn, nn.SiLU) and self.input_nf == self.output_nf
                 and 1 <= self.input_nf <= L.enflow_max_node_nf()
-                and bool(L.enflow_supports_hidden(self.hidden_nf)))
+                and kh is not None and bool(L.enflow_supports_hidden(kh)))
 
     def _check_supported(self):
         if not self.hip_supported():
             raise NotImplementedError(
                 "enflow_amd EGCL kernels implement the SiLU activation, input_nf == output_nf <= 8 "
-                "and hidden_nf in {32, 64, 128}")
+                "and hidden_nf <= 128")
 
     def variant_flags(self):
         """ENFLOW_EGCL_* flags of this layer's constructor variants (0 = defaults)."""
         return ((_lib.EGCL_ATTENTION if self.attention else 0) | (_lib.EGCL_NORM_DIFF if self.norm_diff else 0)
                 | (_lib.EGCL_TANH if self.tanh else 0))
 
+    def raw_named(self):
+        """(name, parameter) in the default-flag named_parameters() order the C
+        ABI expects (att_nn, present with attention=True, travels separately)."""
+        return [(k, p) for k, p in self.named_parameters() if not k.startswith("att_nn.")]
+
     def raw_parameters(self):
-        """Parameters in the default-flag named_parameters() order the C ABI
-        expects (att_nn, present with attention=True, travels separately)."""
-        return [p for k, p in self.named_parameters() if not k.startswith("att_nn.")]
+        return [p for _, p in self.raw_named()]
+
+    def kernel_raw(self, device):
+        """The raw parameters as one flat fp32 vector at the kernel width."""
+        return flat_padded(self.raw_named(), EGCL_HDIMS, self.hidden_nf, self.kernel_hidden, device)
 
     def _att_raw(self, device):
+        """att_nn.0 weight [kernel width] + bias [1] (None without attention)."""
         if not self.attention:
             return None
-        lin = self.att_nn[0]
-        return torch.cat([lin.weight.detach().reshape(-1), lin.bias.detach().reshape(-1)]).to(
-            device=device, dtype=torch.float32)
+        return flat_padded([(k, p) for k, p in self.named_parameters() if k.startswith("att_nn.")],
+                           EGCL_HDIMS, self.hidden_nf, self.kernel_hidden, device)
 
     def _pack(self, raw, dst, device):
         L = _lib.lib()
         att = self._att_raw(device)
-        _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.hidden_nf, self.input_nf, self.variant_flags(),
+        _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.kernel_hidden, self.input_nf, self.variant_flags(),
                                              _lib.ptr(att), _lib.ptr(dst), _lib.stream_ptr(device)),
                    "enflow_pack_egcl_ex_f32")
 
@@ -95,9 +110,8 @@ class EGCL(nn.Module):
         if self._packed is not None and self._packed_key == key:
             return self._packed
         L = _lib.lib()
-        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
-                         for p in self.raw_parameters()])
-        size = L.enflow_egcl_packed_size(self.hidden_nf, self.input_nf)
+        raw = self.kernel_raw(device)
+        size = L.enflow_egcl_packed_size(self.kernel_hidden, self.input_nf)
         out = torch.empty(size, dtype=torch.float32, device=device)
         self._pack(raw, out, device)
         self._packed, self._packed_key = out, key
@@ -106,9 +120,7 @@ class EGCL(nn.Module):
     def pack_into(self, dst):
         """Pack into a slice of a caller-owned buffer (used by the fused flow)."""
         device = dst.device
-        raw = torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32)
-                         for p in self.raw_parameters()])
-        self._pack(raw, dst, device)
+        self._pack(self.kernel_raw(device), dst, device)
 
     # ------------------------------------------------------------------
     def _meta(self, edges, dev):
@@ -133,12 +145,12 @@ class EGCL(nn.Module):
             ws = _lib.large_workspace(M, n, max_n, nf, dev)
             prec = _lib.PREC_F32 | (_lib.EGCL_VARIANTS if self.variant_flags() else 0)
             _lib.check(L.enflow_egcl_forward_large_f32(
-                M, n, max_n, nf, self.hidden_nf, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                M, n, max_n, nf, self.kernel_hidden, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
                 _lib.ptr(meta["box"]), _lib.ptr(hf), _lib.ptr(pos), _lib.ptr(self.packed(dev)),
                 float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F), _lib.ptr(G), _lib.ptr(err), prec,
                 _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)), "enflow_egcl_forward_large_f32")
         else:
-            _lib.check(L.enflow_egcl_forward_f32(M, n, max_n, nf, self.hidden_nf, _lib.ptr(meta["mol_ptr"]),
+            _lib.check(L.enflow_egcl_forward_f32(M, n, max_n, nf, self.kernel_hidden, _lib.ptr(meta["mol_ptr"]),
                                                  _lib.ptr(meta["r_cut"]), _lib.ptr(meta["box"]), _lib.ptr(hf),
                                                  _lib.ptr(pos), _lib.ptr(self.packed(dev)),
                                                  float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F), _lib.ptr(G),

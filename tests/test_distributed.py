@@ -32,8 +32,10 @@ def _worker(rank, world, port, q):
             p.grad = torch.randn_like(p)
         local = [p.grad.clone() for p in params]
         allreduce_gradients(params, bucket_bytes=64)   # tiny buckets: exercise bucketing
-        out["grads"] = [p.grad.clone() for p in params]
-        out["local"] = local
+        # plain lists: a tensor put on a multiprocessing queue is shared through
+        # the sender's file descriptors, which vanish if this process exits first
+        out["grads"] = [p.grad.tolist() for p in params]
+        out["local"] = [t.tolist() for t in local]
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -53,7 +55,9 @@ def test_gloo_world2():
     s0, s1 = res[0]["shard"], res[1]["shard"]
     assert s0[0] == 0 and s0[1] == s1[0] and s1[1] == 1027 and abs((s0[1] - s0[0]) - (s1[1] - s1[0])) <= 1
     assert res[0]["max"] == res[1]["max"] == 2.5
+    T = torch.tensor
     for g0, g1, l0, l1 in zip(res[0]["grads"], res[1]["grads"], res[0]["local"], res[1]["local"]):
+        g0, g1, l0, l1 = T(g0), T(g1), T(l0), T(l1)
         torch.testing.assert_close(g0, (l0 + l1) / 2)
         torch.testing.assert_close(g1, (l0 + l1) / 2)
 

@@ -151,3 +151,34 @@ def test_bench_flop_accounting():
     assert abs(r["frac"] - iss / 1e-3 / 1e12 / 2500.0) < 1e-12
     assert abs(r["frac"] - r["matrix_pipe"]["frac"]) < 1e-12
     assert bench.flops_per_launch(1000, 100, 8, 128, 5) == alg
+
+
+def test_hidden_padding_is_exact_on_cpu():
+    """Hidden widths the kernels are not compiled for run zero-padded
+    (enflow_amd/nn/_pad.py): the float64 EGCL restatement on the padded
+    parameters gives the unpadded outputs, and pad -> unpad_grads returns every
+    real parameter (CPU-only check of the padding layout)."""
+    import numpy as np
+    from oracle import enflow_oracle as O
+    from oracle import enflow_oracle_grad as OG
+    from enflow_amd.nn._pad import EGCL_HDIMS, pad, kernel_hidden, unpad_grads
+    from enflow_amd.nn import EGCL
+    from enflow_amd.data.synthetic import make_molecules
+    torch.manual_seed(3)
+    net = EGCL(5, 5, 48, attention=True, norm_diff=True, tanh=True).double()
+    H, Hp = 48, kernel_hidden(48)
+    assert Hp == 64 and kernel_hidden(100) == 128 and kernel_hidden(129) is None
+    b = make_molecules(3, [12, 7, 9], nf=5, seed=4)
+    row, col, eb = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    args = (torch.tensor(b["h"]), torch.tensor(b["pos"]), torch.as_tensor(row), torch.as_tensor(col),
+            torch.tensor(eb), 28, 1.0, (True, True, True))
+    real = {k: p.detach() for k, p in net.named_parameters()}
+    padded = {k: pad(p, EGCL_HDIMS[k], H, Hp) for k, p in real.items()}
+    for a, c in zip(OG._egcl(real, *args), OG._egcl(padded, *args)):
+        np.testing.assert_allclose(a.numpy(), c.numpy(), rtol=1e-13, atol=1e-15)
+    named = list(net.named_parameters())
+    flat = torch.cat([padded[k].reshape(-1) for k, _ in named])
+    back, off = unpad_grads(flat, named, EGCL_HDIMS, H, Hp)
+    assert off == flat.numel()
+    for k, p in named:
+        assert torch.equal(back[k], real[k]), k
