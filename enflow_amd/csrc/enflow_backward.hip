@@ -1335,6 +1335,9 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 // hi / lo split; the stage's three-product sums land in a scratch accumulator
 // that is added to the running one with the exact inverse scale.
 #define OX_LD 36   // LDS column stride (floats): 16-byte aligned operand reads
+#ifndef ENFLOW_OX_DEPTH
+#define ENFLOW_OX_DEPTH 1    // stages of rows in flight ahead of the MFMAs (A/B knob)
+#endif
 #ifndef ENFLOW_OUTER_WPS
 #define ENFLOW_OUTER_WPS 2   // outer_x3_kernel occupancy hint (A/B knob)
 #endif
@@ -1368,58 +1371,57 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
-  float rd[16], rx[16];
-  float ra = 0.f, xa = 1.f;
+  // staged rows in registers: one stage ahead (ENFLOW_OX_DEPTH 1) or two
+  // (2: twice the loads in flight; slots alternate, the loop unrolled by 2)
+  struct Stage { float rd[16], rx[16], ra, xa; };
+  Stage S0, S1;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
   // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
-  auto gload = [&](int st) {
+  auto gload = [&](int st, Stage& G) {
     const int rb = r0 + st * OB_ROWS;
     const size_t rt = (size_t)(rb >> 5);
     const float* const dblk = D.DY + ((rt * D.ldd) << 5);
     const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
     const bool pv = rb + (tid & 31) < r1;
-    if (xf_dy) ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
-    if (D.xrow) xa = pv ? D.xrow[rb + (tid & 31)] : 0.f;
+    G.ra = 0.f;
+    G.xa = 1.f;
+    if (xf_dy) G.ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
+    if (D.xrow) G.xa = pv ? D.xrow[rb + (tid & 31)] : 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int c = 8 * q + (tid >> 5);
       const unsigned e = (unsigned)(q * 256 + tid);
-      rd[q] = (pv && c < M) ? dblk[e] : 0.f;
-      rx[q] = (pv && n0 + c < N) ? xblk[e] : 0.f;
+      G.rd[q] = (pv && c < M) ? dblk[e] : 0.f;
+      G.rx[q] = (pv && n0 + c < N) ? xblk[e] : 0.f;
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, Stage& G) {
     if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        const float z = rd[q], sg = sigmoid_f(z);
-        if (fold) wacc[q] = fmaf(ra, z * sg, wacc[q]);
-        rd[q] = ra * (sg * (1.f + z * (1.f - sg)));
+        const float z = G.rd[q], sg = sigmoid_f(z);
+        if (fold) wacc[q] = fmaf(G.ra, z * sg, wacc[q]);
+        G.rd[q] = G.ra * (sg * (1.f + z * (1.f - sg)));
       }
     }
     if (xf_x) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) rx[q] = silu_f(rx[q]);
+      for (int q = 0; q < 16; ++q) G.rx[q] = silu_f(G.rx[q]);
     }
     if (D.xrow) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) rx[q] *= xa;
+      for (int q = 0; q < 16; ++q) G.rx[q] *= G.xa;
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int c = 8 * q + (tid >> 5), r = tid & 31;
-      sd[buf][c][r] = rd[q];
-      sx[buf][c][r] = rx[q];
+      sd[buf][c][r] = G.rd[q];
+      sx[buf][c][r] = G.rx[q];
     }
   };
   const bool use_m1 = mh * 64 + 32 < M, use_n0 = n0 + nh * 64 < N, use_n1 = n0 + nh * 64 + 32 < N;
   const bool live = mh * 64 < M && use_n0;
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int st = 0; st < nst; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nst) gload(st + 1);
+  auto compute = [&](int buf) {
     if (live) {
       // operands of both k-steps: A[a][ks] (DY columns), B[b][ks] (X columns)
       f32x4 av[2][2][2], bv[2][2][2];   // [tile][ks][half]
@@ -1477,9 +1479,35 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
 #pragma unroll 8
       for (int r = 0; r < OB_ROWS; ++r) bsum += sd[buf][tid][r];
     }
-    if (st + 1 < nst) lstore(buf ^ 1);
+  };
+#if ENFLOW_OX_DEPTH == 2
+  gload(0, S0);
+  lstore(0, S0);
+  if (nst > 1) gload(1, S1);
+  __syncthreads();
+  // iteration st: LDS buffer st & 1 holds stage st, slot (st + 1) & 1 stage st + 1
+  auto iter = [&](int st, Stage& cur_free, Stage& nxt) {
+    if (st + 2 < nst) gload(st + 2, cur_free);
+    compute(st & 1);
+    if (st + 1 < nst) lstore((st + 1) & 1, nxt);
+    __syncthreads();
+  };
+  for (int st = 0; st < nst; st += 2) {
+    iter(st, S0, S1);
+    if (st + 1 < nst) iter(st + 1, S1, S0);
+  }
+#else
+  gload(0, S0);
+  lstore(0, S0);
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nst) gload(st + 1, S0);
+    compute(buf);
+    if (st + 1 < nst) lstore(buf ^ 1, S0);
     __syncthreads();
   }
+#endif
   float* out = D.part + (size_t)chunk * M * NB;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
