@@ -1891,6 +1891,7 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
 // sync events.  Host-side state only; guarded by a mutex (one backward's launch
 // sequence at a time per process).
 #include <mutex>
+#include <stdlib.h>
 #include <vector>
 namespace {
 struct AuxDev {
@@ -2166,6 +2167,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
   int dev = 0;
   if ((st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev)) != hipSuccess || dev < 0 || dev >= 64) return -2;
   std::lock_guard<std::mutex> aux_lock(g_aux_mu);
+  const bool serial = getenv("ENFLOW_SERIAL_BWD") != nullptr;   // diagnostic: no overlap
   hipStream_t st2 = aux_stream(dev);
   if (!st2) return -2;
   auto ev = [&](int i) { return aux_event(dev, (size_t)i); };   // 2 l: backward of l done, 2 l + 1: outer of l done
@@ -2213,6 +2215,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
                                       num_atoms, nf, H);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
+    if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;
   }
   // join: every weight-gradient pass done before the dequantiser's (buffer 0 again) and the return
   if (n_layers > 0 && hipStreamWaitEvent(st, ev(1), 0) != hipSuccess) return -2;   // layer 0's pass (the last)
@@ -2322,6 +2325,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
   int dev = 0;
   if ((st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev)) != hipSuccess || dev < 0 || dev >= 64) return -2;
   std::lock_guard<std::mutex> aux_lock(g_aux_mu);
+  const bool serial = getenv("ENFLOW_SERIAL_BWD") != nullptr;   // diagnostic: no overlap
   hipStream_t st2 = aux_stream(dev);
   if (!st2) return -2;
   auto ev = [&](int i) { return aux_event(dev, (size_t)i); };
@@ -2377,6 +2381,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
                                       A.Rp, R, tape + T.hx + (size_t)l * num_atoms * (nf + H), num_atoms, nf, H);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
+    if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;
   }
   if (n_layers > 0 && hipStreamWaitEvent(st, ev(1), 0) != hipSuccess) return -2;
   if (dequant_kind == ENFLOW_DEQUANT_ARGMAX && num_atoms > 0) {

@@ -311,6 +311,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
           A.tape[T.vel + la * 3 + e] = sm.vel[r0 * 3 + e];
         }
         for (int a = tid; a < rb; a += BLOCK) A.tape[T.q + la + a] = sm.Q[r0 + a];
+        __syncthreads();   // every thread's copy done before the leapfrog update rewrites pos / vel / h / g
       }
       if constexpr (BLOCKED) {   // park the block's forces (egcl.py:73-74)
         for (int e = tid; e < rb * 3; e += BLOCK) {

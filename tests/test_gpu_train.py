@@ -206,3 +206,27 @@ def test_backward_error_word_is_deferred_then_checked():
     with pytest.raises(IndexError):
         _lib.check_pending()
     assert not _lib._pending
+
+
+def test_training_gradients_bitwise_reproducible_bench_scale():
+    """The bench's training batch (1024 x 64-atom molecules), 2 layers, three
+    steps: bitwise-identical gradients.  (Regression: the forward's tape copy
+    of a layer's input state once raced the same layer's leapfrog update in
+    the unblocked kernel -- a few atoms' taped positions were already updated
+    -- which only showed at this scale.)"""
+    from enflow_amd.data.synthetic import make_molecules, default_dt, default_kBT
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    b = make_molecules(1024, 64, nf=5, seed=2000, radius=4.0 * (64 / 22.0) ** (1.0 / 3.0))
+    torch.manual_seed(0)
+    model = LFIntegrator([EGCL(5, 5, 128) for _ in range(2)], ArgMax(5, 128), dt=default_dt()).cuda()
+    base = Data.from_arrays(b, device="cuda")
+    eps = torch.randn_like(base.h)
+    grads = []
+    for _ in range(3):
+        _train_step(model, base._replace(), eps, default_kBT(), 0.1)
+        grads.append([p.grad.clone() for p in model.parameters()])
+    for g in grads[1:]:
+        for a, b_ in zip(grads[0], g):
+            assert torch.equal(a, b_)

@@ -20,11 +20,12 @@ def main():
     mols = int(os.environ.get("AB_MOLS", 1024))
     b = make_molecules(mols, atoms, nf=5, seed=2000, radius=4.0 * (atoms / 22.0) ** (1.0 / 3.0))
     torch.manual_seed(0)
-    model = LFIntegrator([EGCL(5, 5, 128) for _ in range(8)], ArgMax(5, 128), dt=default_dt()).to(dev)
+    nl = int(os.environ.get("AB_LAYERS", 8))
+    model = LFIntegrator([EGCL(5, 5, 128) for _ in range(nl)], ArgMax(5, 128), dt=default_dt()).to(dev)
     nll = Alchemical_NLL(kBT=default_kBT(), softening=0.1)
     base = Data.from_arrays(b, device=dev)
     noise = torch.randn_like(base.h)
-    names = [n for n, _ in model.named_parameters()]
+    names = [n for n, _ in model.named_parameters()] + ["input.pos", "input.vel"]
 
     def run(path):
         _lib._lib = None
@@ -34,12 +35,16 @@ def main():
                 if hasattr(mod, attr):
                     setattr(mod, attr, None)
         model.zero_grad(set_to_none=True)
-        out, ldj = model(base._replace(), noise=noise)
+        d = base._replace()
+        d.pos = d.pos.clone().requires_grad_(True)
+        d.vel = d.vel.clone().requires_grad_(True)
+        pos_in, vel_in = d.pos, d.vel
+        out, ldj = model(d, noise=noise)
         loss = nll(out, ldj)
         loss.backward()
         torch.cuda.synchronize()
         _lib.check_pending()
-        return float(loss), [p.grad.clone() for p in model.parameters()]
+        return float(loss), [p.grad.clone() for p in model.parameters()] + [pos_in.grad.clone(), vel_in.grad.clone()]
 
     runs = [(p, run(p)) for p in sys.argv[1:]]
     l0, g0 = runs[0][1]
