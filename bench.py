@@ -155,7 +155,8 @@ def load_traffic(workload, sha):
     (profiles/*pmc_traffic.json, written by profiles/collect_pmc.py) -- only if
     it was collected for this workload AND this exact library build."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_traffic.json"), recursive=True),
+                       reverse=True):
         try:
             with open(path) as fh:
                 d = json.load(fh)
@@ -675,7 +676,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=30,
+                    help="untimed steps first: the first ~20 launches run while the clock ramps up")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-per-core", type=int, default=192,
                     help="cpu_baseline sample: molecules per host core (16 cores: ~15 s)")
