@@ -434,3 +434,34 @@ def test_training_forward_defers_the_index_error_to_backward():
         loss.backward()
     _lib.check_pending()
     assert not _lib._pending
+
+
+@pytest.mark.parametrize("scale", [3e4, 1e6])
+def test_f16x3_range_guard(scale):
+    """Features scaled so the hidden activations pass the fp16 range (65504):
+    the f16x3 path must either raise FloatingPointError (ENFLOW_ERR_RANGE) or
+    return the oracle's result; the f32 path returns the oracle's result."""
+    from enflow_amd.nn import EGCL, Floor
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(4, 22, nf=4, seed=13))
+    b["h"] = np.floor(np.random.default_rng(14).uniform(0, scale, size=b["h"].shape)).astype(np.float32).astype(np.float64)
+    torch.manual_seed(15)
+    model = LFIntegrator([EGCL(4, 4, 64) for _ in range(2)], Floor(), dt=default_dt()).to(DEV)
+    u = torch.rand(b["h"].shape, device=DEV, generator=torch.Generator(DEV).manual_seed(16))
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    ref, _ = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
+    outcome = {}
+    for prec in ("f16x3", "f32"):
+        model.gemm_precision = prec
+        try:
+            with torch.no_grad():
+                o, _ = model(Data.from_arrays(b, device=DEV), noise=u)
+            errs = {k: rel_err(getattr(o, k).cpu().numpy(), ref[k]) for k in ("h", "g", "pos", "vel")}
+            outcome[prec] = ("result", max(errs.values()))
+        except FloatingPointError as e:
+            outcome[prec] = ("raised", str(e)[:60])
+    print(f"range guard, features up to {scale:g}:", outcome)
+    assert outcome["f32"][0] == "result" and outcome["f32"][1] < TOL, outcome
+    assert outcome["f16x3"][0] == "raised" or outcome["f16x3"][1] < TOL, outcome
