@@ -183,6 +183,7 @@ struct BwdArgs {
   float* colc;                // [pair rows][CSTR] out
   long long prb;              // pair rows allocated
 };
+__host__ __device__ inline int xin_width(int nf) { return 2 * nf + 1 > 16 ? 32 : 16; }
 constexpr int CSTR = 12;      // colc row: d h_j [NFMAX], d pos_j [3], pad
 
 // <= 80 KB at (H, NMAX) = (128, 64): two workgroups per CU.  The node-MLP
@@ -673,7 +674,9 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const rsrc_t rp0 = rows_rsrc(B.p0 + prow0 * H, nrow * H), rpe = rows_rsrc(B.pe + prow0 * H, nrow * H);
     const rsrc_t rpc = rows_rsrc(B.pc + prow0 * H, nrow * H);
     const rsrc_t rdp0 = rows_rsrc(B.dp0 + prow0 * H, nrow * H), rdpe = rows_rsrc(B.dpe + prow0 * H, nrow * H);
-    const rsrc_t rxin = rows_rsrc(B.xin + prow0 * 16, nrow * 16);
+    // edge_nn.0 input rows [h_i, h_j, radial]: 16 wide, 32 when 2 nf + 1 > 16 (nf = 8)
+    const int XW = xin_width(nf);
+    const rsrc_t rxin = rows_rsrc(B.xin + prow0 * XW, nrow * XW);
     const int lob = (hh * 128 + j) * 4;   // lane bytes: (feature 4hh, row j)
     // d h / d pos of the edge part: each wave adds into its own [atom][nf + 3]
     // slab (one wave's LDS atomics apply in a fixed order), summed over the
@@ -748,8 +751,10 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
         if (q < nf) v = sm.h[i * NFP + q];
         else if (q < 2 * nf) v = colh(q - nf);
         else if (q == 2 * nf) v = radial;
-        ST_OUT(rxin, (hh * 256 + j) * 4, gt * 2048 + u * 128, valid ? v : 0.f);
+        ST_OUT(rxin, (hh * 256 + j) * 4, gt * XW * 128 + u * 128, valid ? v : 0.f);
       }
+      if (XW > 16 && hh == 0)   // q = 16 = 2 nf: the radial of an nf = 8 layer
+        ST_OUT(rxin, j * 4, gt * XW * 128 + 16 * 128, valid ? radial : 0.f);
 
       // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1
       f32x16 x0[NT];
@@ -1859,7 +1864,7 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   const size_t P = (size_t)prb, A = (size_t)num_atoms;
   W.offs = 0;
   W.buf0 = al64((size_t)n_layers * (num_mols + 1));
-  W.xin = o; o += al64(P * 16);
+  W.xin = o; o += al64(P * xin_width(nf));
   W.p0 = o; o += al64(P * H);
   W.pe = o; o += al64(P * H);
   W.pc = o; o += al64(P * H);
@@ -2017,7 +2022,8 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     ob.nd = 0;
     int wg = 0;
     float* part = wb + Wl.part;
-    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, 16, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1, PAIR_OUTER);
+    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, xin_width(nf), 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1,
+             PAIR_OUTER);
     add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
     ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
     add_desc(ob, wg, wb + Wl.pc, H, H, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);

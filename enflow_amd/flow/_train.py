@@ -135,7 +135,7 @@ class _FlowFunction(torch.autograd.Function):
             grads += layer_grads(net, grad_layers[li * rstride:(li + 1) * rstride])
         if kind == _lib.DEQUANT_ARGMAX:
             am = flow.dequantize
-            gd, _ = unpad_grads(grad_dq, list(am.named_parameters()), ARGMAX_HDIMS, am.hidden_nf, hid)
+            gd, _ = unpad_grads(grad_dq, list(am.named_parameters()), ARGMAX_HDIMS, am.pad_geom(hid))
             grads += [gd[k].contiguous().to(p.dtype) for k, p in am.named_parameters()]
         # d h of the data only exists without a learned dequantiser (z = h + noise)
         gh_in = ah if kind != _lib.DEQUANT_ARGMAX else None
@@ -224,11 +224,11 @@ def layer_grads(net, flat):
     default-flag parameters in named order, then att_nn.0 weight / bias in the
     width + 1 slots) into the module's parameters, in named_parameters() order
     (the real block of each zero-padded tensor, nn/_pad.py)."""
-    H, Hp = net.hidden_nf, net.kernel_hidden
-    g, off = unpad_grads(flat, net.raw_named(), EGCL_HDIMS, H, Hp)
+    geom = net.pad_geom()
+    g, off = unpad_grads(flat, net.raw_named(), EGCL_HDIMS, geom)
     att = [(k, p) for k, p in net.named_parameters() if k.startswith("att_nn.")]
     if att:
-        ga, _ = unpad_grads(flat[off:], att, EGCL_HDIMS, H, Hp)
+        ga, _ = unpad_grads(flat[off:], att, EGCL_HDIMS, geom)
         g.update(ga)
     return [g[name].contiguous().to(p.dtype) for name, p in net.named_parameters()]
 
@@ -242,7 +242,7 @@ class _EGCLFunction(torch.autograd.Function):
     def forward(ctx, net, meta, h, pos, *params):
         q, f, g = net._infer(h.detach(), pos.detach(), meta)
         ctx.net, ctx.meta = net, meta
-        ctx.save_for_backward(h.detach().to(torch.float32).contiguous(), pos.detach().to(torch.float32).contiguous())
+        ctx.save_for_backward(net.pad_h(h.detach()), pos.detach().to(torch.float32).contiguous())
         return q, f, g
 
     @staticmethod
@@ -252,7 +252,7 @@ class _EGCLFunction(torch.autograd.Function):
         large = meta["max_n"] > _lib.TRAIN_MAX_ATOMS
         L = _lib.lib()
         dev = h.device
-        A, nf, hid = h.shape[0], net.input_nf, net.kernel_hidden
+        A, nf, hid = h.shape[0], net.kernel_nf, net.kernel_hidden
         M = meta["mol_ptr"].numel() - 1
         st = _lib.stream_ptr(dev)
         prec = _lib.PREC_F16X3 | (_lib.EGCL_VARIANTS if net.variant_flags() else 0)
@@ -298,7 +298,10 @@ class _EGCLFunction(torch.autograd.Function):
                 return torch.zeros(shape, dtype=torch.float32, device=dev)
             return t.detach().to(dtype=torch.float32).reshape(shape).contiguous()
 
-        aq, af, ag = adj(gq, (A,)), adj(gf, (A, 3)), adj(gg, (A, nf))
+        aq, af = adj(gq, (A,)), adj(gf, (A, 3))
+        ag = torch.zeros((A, nf), dtype=torch.float32, device=dev)   # G's padded columns: no adjoint
+        if gg is not None:
+            ag[:, :net.output_nf] = gg.detach().to(torch.float32).reshape(A, net.output_nf)
         dh = torch.empty((A, nf), dtype=torch.float32, device=dev)
         dpos = torch.empty((A, 3), dtype=torch.float32, device=dev)
         grad = torch.empty_like(raw)
@@ -317,7 +320,7 @@ class _EGCLFunction(torch.autograd.Function):
                 _lib.ptr(ag), _lib.ptr(dh), _lib.ptr(dpos), _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
                 st), "enflow_egcl_backward_f32")
         _lib.raise_on_err(err)
-        return (None, None, dh, dpos) + tuple(layer_grads(net, grad))
+        return (None, None, dh[:, :net.input_nf], dpos) + tuple(layer_grads(net, grad))
 
 
 class _ArgMaxFunction(torch.autograd.Function):
@@ -347,7 +350,7 @@ class _ArgMaxFunction(torch.autograd.Function):
             meta["mol_ptr"].numel() - 1, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(h),
             _lib.ptr(raw), _lib.ptr(noise), _lib.ptr(az), _lib.ptr(alq), _lib.ptr(grad), _lib.ptr(ws), wsb,
             _lib.stream_ptr(dev)), "enflow_argmax_backward_f32")
-        gd, _ = unpad_grads(grad, list(am.named_parameters()), ARGMAX_HDIMS, am.hidden_nf, hid)
+        gd, _ = unpad_grads(grad, list(am.named_parameters()), ARGMAX_HDIMS, am.pad_geom())
         grads = [gd[k].contiguous().to(p.dtype) for k, p in am.named_parameters()]
         # h is the categorical data (one-hot, argmax.py:13): no gradient is returned for it
         return (None, None, None, None) + tuple(grads)

@@ -55,6 +55,8 @@ class LFIntegrator(BaseFlow):
         h0, f0 = nets[0].hidden_nf, nets[0].input_nf
         for n in nets:
             n._check_supported()
+            if n.input_nf != n.output_nf:   # dynamics.py:17-18 adds G to g
+                raise NotImplementedError("LFIntegrator needs EGCL layers with input_nf == output_nf")
             if (n.hidden_nf, n.input_nf) != (h0, f0) or n.coords_weight != nets[0].coords_weight:
                 raise NotImplementedError("all EGCL layers must share hidden_nf, node_nf and coords_weight")
         # the kernels' hidden width (hidden_nf, or zero-padded to the next compiled one)

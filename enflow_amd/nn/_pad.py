@@ -1,31 +1,41 @@
-"""Hidden widths the kernels are not compiled for run zero-padded to the next
-compiled width (32, 64, 128).
+"""Shapes the kernels are not compiled for run zero-padded to compiled ones.
 
-The reference accepts any ``hidden_nf`` (enflow/nn/egcl.py:11,
-enflow/nn/argmax.py:6).  Padding every hidden dimension with zero weights and
-zero biases is exact: a padded hidden unit has pre-activation 0, SiLU(0) = 0,
-and its outgoing weights are 0, so every output (and every gradient of a real
-parameter) equals the unpadded network's.  The real parameters occupy the
-leading block of each padded tensor: for node_nn.0.weight the columns are
-[h (nf) | messages (H)], so the messages' padding is appended at the tail too.
+The reference accepts any ``hidden_nf`` and any ``input_nf`` / ``output_nf``
+(enflow/nn/egcl.py:11, enflow/nn/argmax.py:6).  The kernels are compiled for
+hidden widths 32 / 64 / 128 and one node-feature width ``nf`` (<= 8) for both
+the input and the output features.  Other shapes are embedded in the next
+compiled one with zero weights and biases, which is exact:
+
+* a padded hidden unit has pre-activation 0, SiLU(0) = 0, and zero outgoing
+  weights;
+* a padded input feature is a zero column of h with zero incoming weights;
+* a padded output feature of node_nn.2 has zero weights and bias (G's extra
+  columns are 0 and are sliced away).
+
+So every output, and the gradient of every real parameter, equals the
+unpadded network's.  Each parameter's real entries sit at fixed indices of the
+padded tensor (`Geom` index maps): for edge_nn.0's input [h_i | h_j | radial]
+and node_nn.0's input [h | messages] the blocks move to the padded offsets.
 """
 import torch
 
 KERNEL_HIDDEN = (32, 64, 128)
 
-# per parameter: the dims that have the hidden width ("H") or end with it ("xH")
+# per parameter and dim: None (kept), "H" hidden, "E" edge_nn.0 input
+# [h_i (in) | h_j (in) | radial], "xH" node_nn.0 input [h (in) | messages (H)],
+# "I" input features, "O" output features
 EGCL_HDIMS = {
-    "edge_nn.0.weight": ("H", None), "edge_nn.0.bias": ("H",),
+    "edge_nn.0.weight": ("H", "E"), "edge_nn.0.bias": ("H",),
     "edge_nn.2.weight": ("H", "H"), "edge_nn.2.bias": ("H",),
     "node_nn.0.weight": ("H", "xH"), "node_nn.0.bias": ("H",),
-    "node_nn.2.weight": (None, "H"), "node_nn.2.bias": (None,),
+    "node_nn.2.weight": ("O", "H"), "node_nn.2.bias": ("O",),
     "coord_nn.0.weight": ("H", "H"), "coord_nn.0.bias": ("H",), "coord_nn.2.weight": (None, "H"),
-    "vel_scaling_nn.0.weight": ("H", None), "vel_scaling_nn.0.bias": ("H",),
+    "vel_scaling_nn.0.weight": ("H", "I"), "vel_scaling_nn.0.bias": ("H",),
     "vel_scaling_nn.2.weight": (None, "H"), "vel_scaling_nn.2.bias": (None,),
     "att_nn.0.weight": (None, "H"), "att_nn.0.bias": (None,),
 }
 ARGMAX_HDIMS = {
-    "network.0.weight": ("H", None), "network.0.bias": ("H",),
+    "network.0.weight": ("H", "I"), "network.0.bias": ("H",),
     "network.2.weight": (None, "H"), "network.2.bias": (None,),
 }
 
@@ -35,35 +45,72 @@ def kernel_hidden(hidden_nf):
     return next((k for k in KERNEL_HIDDEN if k >= hidden_nf), None)
 
 
-def padded_shape(spec, shape, H, Hp):
-    return tuple(Hp if s == "H" else (d - H + Hp if s == "xH" else d) for s, d in zip(spec, shape))
+class Geom:
+    """Real (H, fin, fout) -> kernel (Hp, F) shape of one module."""
+
+    def __init__(self, H, Hp, fin, fout, F):
+        self.H, self.Hp, self.fin, self.fout, self.F = H, Hp, fin, fout, F
+
+    @property
+    def identity(self):
+        return self.H == self.Hp and self.fin == self.F and self.fout == self.F
+
+    def index(self, kind, size):
+        """(padded size, indices of the real entries along this dim)."""
+        a = torch.arange
+        if kind is None:
+            return size, a(size)
+        if kind == "H":
+            return self.Hp, a(self.H)
+        if kind == "I":
+            return self.F, a(self.fin)
+        if kind == "O":
+            return self.F, a(self.fout)
+        if kind == "E":
+            return 2 * self.F + 1, torch.cat([a(self.fin), self.F + a(self.fin), torch.tensor([2 * self.F])])
+        if kind == "xH":
+            return self.F + self.Hp, torch.cat([a(self.fin), self.F + a(self.H)])
+        raise ValueError(kind)
 
 
-def pad(t, spec, H, Hp):
-    """t (real parameter) -> zero-padded fp32 tensor of the kernel width."""
-    if H == Hp:
+def _indices(spec, shape, g, device):
+    dims = [g.index(k, d) for k, d in zip(spec, shape)]
+    sizes = tuple(s for s, _ in dims)
+    idx = [i.to(device) for _, i in dims]
+    if len(idx) == 2:
+        idx = (idx[0][:, None], idx[1][None, :])
+    else:
+        idx = (idx[0],)
+    return sizes, idx
+
+
+def pad(t, spec, g):
+    """t (real parameter) -> zero-padded tensor of the kernel shape."""
+    if g.identity:
         return t
-    out = torch.zeros(padded_shape(spec, t.shape, H, Hp), dtype=t.dtype, device=t.device)
-    out[tuple(slice(0, d) for d in t.shape)] = t
+    sizes, idx = _indices(spec, t.shape, g, t.device)
+    out = torch.zeros(sizes, dtype=t.dtype, device=t.device)
+    out[idx] = t
     return out
 
 
-def flat_padded(named, table, H, Hp, device):
+def flat_padded(named, table, g, device):
     """Concatenated flat fp32 padded parameters, in the given (name, param) order."""
-    return torch.cat([pad(p.detach().to(device=device, dtype=torch.float32), table[k], H, Hp).reshape(-1)
+    return torch.cat([pad(p.detach().to(device=device, dtype=torch.float32), table[k], g).reshape(-1)
                       for k, p in named])
 
 
-def unpad_grads(flat, named, table, H, Hp):
+def unpad_grads(flat, named, table, g):
     """Split a flat gradient in the padded layout of `named` into the real
-    parameters' shapes (the leading block of each padded tensor)."""
+    parameters' shapes (their entries of each padded tensor).  Returns
+    ({name: grad}, floats consumed)."""
     out, off = {}, 0
     for k, p in named:
-        ps = padded_shape(table[k], p.shape, H, Hp)
+        sizes, idx = _indices(table[k], p.shape, g, flat.device)
         n = 1
-        for d in ps:
+        for d in sizes:
             n *= d
-        g = flat[off:off + n].view(ps)
-        out[k] = g[tuple(slice(0, d) for d in p.shape)]
+        gp = flat[off:off + n].view(sizes)
+        out[k] = gp if g.identity else gp[idx]
         off += n
     return out, off

@@ -10,7 +10,7 @@ from torch import nn
 
 from .. import _lib
 from ..utils.helpers import one_hot, mol_ptr_from_counts
-from ._pad import ARGMAX_HDIMS, flat_padded, kernel_hidden
+from ._pad import ARGMAX_HDIMS, Geom, flat_padded, kernel_hidden
 
 
 class ArgMax(nn.Module):
@@ -33,7 +33,11 @@ class ArgMax(nn.Module):
         width = width or self.kernel_hidden
         if width is None or width < self.hidden_nf:
             raise NotImplementedError(f"ArgMax hidden_nf {self.hidden_nf} past the kernel width {width}")
-        return flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.hidden_nf, width, device)
+        return flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.pad_geom(width), device)
+
+    def pad_geom(self, width=None):
+        nf = self.node_nf
+        return Geom(self.hidden_nf, width or self.kernel_hidden, nf, nf, nf)
 
     def packed(self, device, width=None):
         width = width or self.kernel_hidden

@@ -12,7 +12,7 @@ from torch import nn
 
 from .. import _lib
 from ..data.base import Edges
-from ._pad import EGCL_HDIMS, flat_padded, kernel_hidden
+from ._pad import EGCL_HDIMS, Geom, flat_padded, kernel_hidden
 
 
 class EGCL(nn.Module):
@@ -54,21 +54,31 @@ class EGCL(nn.Module):
         of 32 / 64 / 128 with the extra units zero-padded (exact, nn/_pad.py)."""
         return kernel_hidden(self.hidden_nf)
 
+    @property
+    def kernel_nf(self):
+        """The kernels' node-feature width: max(input_nf, output_nf), the
+        narrower side zero-padded (exact, nn/_pad.py)."""
+        return max(self.input_nf, self.output_nf)
+
+    def pad_geom(self):
+        return Geom(self.hidden_nf, self.kernel_hidden, self.input_nf, self.output_nf, self.kernel_nf)
+
     def hip_supported(self):
         """The HIP kernels implement every constructor flag of the reference
         (attention, norm_diff, tanh; ``clamp`` is stored and unused there too)
-        with the SiLU activation, input_nf == output_nf <= 8, any hidden_nf
-        <= 128 (32 / 64 / 128 compiled, other widths zero-padded)."""
+        with the SiLU activation, input_nf and output_nf <= 8 and any hidden_nf
+        <= 128 (hidden 32 / 64 / 128 and one feature width compiled, other
+        shapes zero-padded)."""
         L = _lib.lib()
         kh = self.kernel_hidden
-        return (isinstance(self.act_fn, nn.SiLU) and self.input_nf == self.output_nf
-                and 1 <= self.input_nf <= L.enflow_max_node_nf()
+        return (isinstance(self.act_fn, nn.SiLU) and min(self.input_nf, self.output_nf) >= 1
+                and self.kernel_nf <= L.enflow_max_node_nf()
                 and kh is not None and bool(L.enflow_supports_hidden(kh)))
 
     def _check_supported(self):
         if not self.hip_supported():
             raise NotImplementedError(
-                "enflow_amd EGCL kernels implement the SiLU activation, input_nf == output_nf <= 8 "
+                "enflow_amd EGCL kernels implement the SiLU activation, input_nf / output_nf <= 8 "
                 "and hidden_nf <= 128")
 
     def variant_flags(self):
@@ -86,19 +96,19 @@ class EGCL(nn.Module):
 
     def kernel_raw(self, device):
         """The raw parameters as one flat fp32 vector at the kernel width."""
-        return flat_padded(self.raw_named(), EGCL_HDIMS, self.hidden_nf, self.kernel_hidden, device)
+        return flat_padded(self.raw_named(), EGCL_HDIMS, self.pad_geom(), device)
 
     def _att_raw(self, device):
         """att_nn.0 weight [kernel width] + bias [1] (None without attention)."""
         if not self.attention:
             return None
         return flat_padded([(k, p) for k, p in self.named_parameters() if k.startswith("att_nn.")],
-                           EGCL_HDIMS, self.hidden_nf, self.kernel_hidden, device)
+                           EGCL_HDIMS, self.pad_geom(), device)
 
     def _pack(self, raw, dst, device):
         L = _lib.lib()
         att = self._att_raw(device)
-        _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.kernel_hidden, self.input_nf, self.variant_flags(),
+        _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.kernel_hidden, self.kernel_nf, self.variant_flags(),
                                              _lib.ptr(att), _lib.ptr(dst), _lib.stream_ptr(device)),
                    "enflow_pack_egcl_ex_f32")
 
@@ -111,7 +121,7 @@ class EGCL(nn.Module):
             return self._packed
         L = _lib.lib()
         raw = self.kernel_raw(device)
-        size = L.enflow_egcl_packed_size(self.kernel_hidden, self.input_nf)
+        size = L.enflow_egcl_packed_size(self.kernel_hidden, self.kernel_nf)
         out = torch.empty(size, dtype=torch.float32, device=device)
         self._pack(raw, out, device)
         self._packed, self._packed_key = out, key
@@ -133,8 +143,8 @@ class EGCL(nn.Module):
         L = _lib.lib()
         dev = h.device
         n = h.shape[0]
-        nf = self.input_nf
-        hf = h.to(torch.float32).contiguous()
+        nf = self.kernel_nf
+        hf = self.pad_h(h)
         pos = pos.to(torch.float32).contiguous()
         Q = torch.empty(n, dtype=torch.float32, device=dev)
         F = torch.empty((n, 3), dtype=torch.float32, device=dev)
@@ -156,7 +166,14 @@ class EGCL(nn.Module):
                                                  float(self.coords_weight), _lib.ptr(Q), _lib.ptr(F), _lib.ptr(G),
                                                  _lib.ptr(err), _lib.stream_ptr(dev)), "enflow_egcl_forward_f32")
         _lib.raise_on_err(err)
-        return Q.reshape(n, 1), F, G
+        return Q.reshape(n, 1), F, G[:, :self.output_nf]
+
+    def pad_h(self, h):
+        """h [n][input_nf] -> fp32 [n][kernel_nf] (zero columns past input_nf)."""
+        hf = h.to(torch.float32)
+        if self.kernel_nf > self.input_nf:
+            hf = torch.cat([hf, hf.new_zeros((hf.shape[0], self.kernel_nf - self.input_nf))], 1)
+        return hf.contiguous()
 
     def forward(self, h, edges):
         """egcl.py:76-92.  Differentiable (w.r.t. the parameters, h and, through

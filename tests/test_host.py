@@ -161,7 +161,7 @@ def test_hidden_padding_is_exact_on_cpu():
     import numpy as np
     from oracle import enflow_oracle as O
     from oracle import enflow_oracle_grad as OG
-    from enflow_amd.nn._pad import EGCL_HDIMS, pad, kernel_hidden, unpad_grads
+    from enflow_amd.nn._pad import EGCL_HDIMS, Geom, pad, kernel_hidden, unpad_grads
     from enflow_amd.nn import EGCL
     from enflow_amd.data.synthetic import make_molecules
     torch.manual_seed(3)
@@ -173,12 +173,43 @@ def test_hidden_padding_is_exact_on_cpu():
     args = (torch.tensor(b["h"]), torch.tensor(b["pos"]), torch.as_tensor(row), torch.as_tensor(col),
             torch.tensor(eb), 28, 1.0, (True, True, True))
     real = {k: p.detach() for k, p in net.named_parameters()}
-    padded = {k: pad(p, EGCL_HDIMS[k], H, Hp) for k, p in real.items()}
+    g = Geom(H, Hp, 5, 5, 5)
+    padded = {k: pad(p, EGCL_HDIMS[k], g) for k, p in real.items()}
     for a, c in zip(OG._egcl(real, *args), OG._egcl(padded, *args)):
         np.testing.assert_allclose(a.numpy(), c.numpy(), rtol=1e-13, atol=1e-15)
     named = list(net.named_parameters())
     flat = torch.cat([padded[k].reshape(-1) for k, _ in named])
-    back, off = unpad_grads(flat, named, EGCL_HDIMS, H, Hp)
+    back, off = unpad_grads(flat, named, EGCL_HDIMS, g)
     assert off == flat.numel()
     for k, p in named:
         assert torch.equal(back[k], real[k]), k
+
+
+@pytest.mark.parametrize("fin,fout", [(3, 5), (6, 2)])
+def test_feature_padding_is_exact_on_cpu(fin, fout):
+    """EGCL(input_nf != output_nf) runs at the kernel width max(in, out):
+    zero input columns / zero output rows (enflow_amd/nn/_pad.py).  The float64
+    restatement on the padded parameters and padded h gives the real outputs."""
+    import numpy as np
+    from oracle import enflow_oracle as O
+    from oracle import enflow_oracle_grad as OG
+    from enflow_amd.nn._pad import EGCL_HDIMS, pad
+    from enflow_amd.nn import EGCL
+    from enflow_amd.data.synthetic import make_molecules
+    torch.manual_seed(5)
+    net = EGCL(fin, fout, 40).double()
+    g = net.pad_geom()
+    assert (g.Hp, g.F) == (64, max(fin, fout))
+    b = make_molecules(2, [11, 8], nf=fin, seed=6)
+    row, col, eb = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    h = torch.tensor(np.random.default_rng(7).normal(size=(19, fin)))
+    hp = torch.cat([h, h.new_zeros((19, g.F - fin))], 1)
+    common = (torch.tensor(b["pos"]), torch.as_tensor(row), torch.as_tensor(col), torch.tensor(eb), 19, 1.0)
+    real = {k: p.detach() for k, p in net.named_parameters()}
+    padded = {k: pad(p, EGCL_HDIMS[k], g) for k, p in real.items()}
+    q, f, gg = OG._egcl(real, h, *common)
+    qp, fp, ggp = OG._egcl(padded, hp, *common)
+    np.testing.assert_allclose(q.numpy(), qp.numpy(), rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(f.numpy(), fp.numpy(), rtol=1e-13, atol=1e-15)
+    np.testing.assert_allclose(gg.numpy(), ggp[:, :fout].numpy(), rtol=1e-13, atol=1e-15)
+    assert float(ggp[:, fout:].abs().max()) == 0.0 if g.F > fout else True
