@@ -205,7 +205,9 @@ class FlowRunner:
         self.noise = torch.empty_like(inp["h"])
         self.ldj_mol = torch.empty(max(mols, 1), dtype=torch.float32, device=device)
         self.ldj = torch.empty(1, dtype=torch.float32, device=device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.status = torch.zeros(2, dtype=torch.int32, device=device)   # error word, ldj ticket
+        self.err = self.status[:1]
+        self.calls = 0
         self.idx = torch.empty(max(n_atoms, 1), dtype=torch.int32, device=device)
         self.mx = torch.zeros(1, dtype=torch.int32, device=device)
         self.onehot = torch.empty((n_atoms, NF), dtype=torch.float32, device=device)
@@ -218,22 +220,29 @@ class FlowRunner:
             self.src = {k: self.work[k].clone() for k in self.work}
 
     def forward_once(self, stats=None):
-        for k in self.work:
-            self.work[k].copy_(self.inp[k])
-        torch.randn(self.noise.shape, generator=self.gen, out=self.noise)
+        # one launch: reads the input batch, writes the work buffers, draws the
+        # ArgMax noise in the kernel (fresh Philox counters every call) and
+        # reduces log|detJ| in the same launch (enflow_lf_forward_io_f32)
         i, w = self.inp, self.work
+        self.calls += 1
         self.model.forward_buffers(w["h"], w["g"], w["pos"], w["vel"], i["box"], i["r_cut"], i["mol_ptr"],
-                                   self.atoms, self.noise, self.ldj_mol, self.ldj, self.err, stats)
+                                   self.atoms, None, self.ldj_mol, self.ldj, self.err, stats,
+                                   src=(i["h"], i["g"], i["pos"], i["vel"]),
+                                   noise_key=(self.seed, self.calls * self.noise.numel()),
+                                   ticket=self.status[1:])
+
+    @property
+    def seed(self):
+        return 0x5eed0000 + int(self.gen.initial_seed())
 
     def step(self):
         if not self.reverse:
             return self.forward_once()
         from enflow_amd import _lib as L_
-        for k in self.work:
-            self.work[k].copy_(self.src[k])
-        i, w = self.inp, self.work
+        i, w, s = self.inp, self.work, self.src
         self.model.reverse_buffers(w["h"], w["g"], w["pos"], w["vel"], i["box"], i["r_cut"], i["mol_ptr"],
-                                   self.atoms, self.idx, self.mx, self.err)
+                                   self.atoms, self.idx, self.mx, self.err,
+                                   src=(s["h"], s["g"], s["pos"], s["vel"]))
         n = w["h"].shape[0]
         L_.check(L_.lib().enflow_one_hot_f32(L_.ptr(self.idx), n, NF, L_.ptr(self.onehot),
                                              L_.stream_ptr(self.dev)), "one_hot")

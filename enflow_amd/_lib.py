@@ -22,6 +22,7 @@ EGCL_ATTENTION, EGCL_NORM_DIFF, EGCL_TANH = 1, 2, 4   # ENFLOW_EGCL_* (include/e
 EGCL_VARIANTS = 0x100                                  # OR into gemm_precision
 
 _i, _i64, _f, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
+_u64 = ctypes.c_uint64
 
 # name -> (restype, argtypes); mirrors include/enflow_hip.h one to one
 SIGNATURES = {
@@ -38,6 +39,10 @@ SIGNATURES = {
                                    _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p, _p, _i, _p]),
     "enflow_lf_reverse_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                    _i, _f, _f, _p, _p, _p, _i, _p]),
+    "enflow_lf_forward_io_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                      _i, _p, _p, _u64, _u64, _f, _f, _f, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
+    "enflow_lf_reverse_io_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                      _i, _f, _f, _p, _p, _p, _i, _p]),
     "enflow_lf_large_workspace_size": (_i64, [_i, _i, _i, _i]),
     "enflow_lf_forward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                          _i, _p, _p, _f, _f, _f, _p, _p, _p, _i, _p, _p, _p, _i64, _p]),
@@ -98,6 +103,8 @@ def lib():
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
         handle = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if not hasattr(handle, name):    # an older build (A/B tools): calling it raises
+                continue
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
@@ -214,10 +221,30 @@ def check_pending():
         _raise_code(int(host.item()))
 
 
-def raise_on_err(err_flag):
-    """Read the device error word (synchronises) and raise like the reference."""
+def raise_on_err(err_flag, reset=False):
+    """Read the device error word (synchronises) and raise like the reference;
+    reset: zero a non-zero word first (a cached status_word stays reusable)."""
     check_pending()
-    _raise_code(int(err_flag.item()))
+    e = int(err_flag.item())
+    if e and reset:
+        err_flag.zero_()
+    _raise_code(e)
+
+
+_status = {}
+
+
+def status_word(device):
+    """int32[2] device words per (device, stream), zero between calls: [0] the
+    error word (read synchronously and re-zeroed by raise_on_err(reset=True)),
+    [1] the in-launch log|detJ| reduction ticket (the kernel resets it).  Saves
+    a fill launch per inference call."""
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    st = _status.get(key)
+    if st is None:
+        st = torch.zeros(2, dtype=torch.int32, device=device)
+        _status[key] = st
+    return st
 
 
 def _raise_code(e):

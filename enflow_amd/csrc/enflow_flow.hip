@@ -200,6 +200,33 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
 #ifndef ENFLOW_BLOCKED_WPS
 #define ENFLOW_BLOCKED_WPS ENFLOW_WAVES_PER_SIMD   // row-blocked (> 64-atom) instances
 #endif
+// batch log|detJ| in the same launch: every workgroup publishes its ldj_mol
+// entry and takes a ticket; the last one sums ldj_mol in reduce_ldj_kernel's
+// fixed order (per-thread strided double sums, then a tree over the block) --
+// bitwise the separate reduction's result -- and resets the ticket for the
+// next launch on the stream.  `red` is BLOCK doubles of LDS scratch.
+__device__ __forceinline__ void ticket_reduce_ldj(const FlowArgs& A, double* red, int* last) {
+  const int tid = threadIdx.x;
+  __threadfence();                       // this block's ldj_mol entry visible device-wide
+  __syncthreads();
+  if (tid == 0) *last = atomicAdd(A.ticket, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!*last) return;
+  __threadfence();                       // acquire: every block's entry
+  double s = 0.0;
+  for (int m = tid; m < A.num_mols; m += BLOCK) s += (double)__builtin_nontemporal_load(&A.ldj_mol[m]);
+  red[tid] = s;
+  __syncthreads();
+  for (int off = BLOCK / 2; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    A.ldj_total[0] = (float)(red[0] + A.ldj_cst);
+    atomicExch(A.ticket, 0u);
+  }
+}
+
 template <int H, int NMAX, bool REV, int PREC, int RB, bool VAR>
 __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLOW_WAVES_PER_SIMD))
     lf_flow_kernel(FlowArgs A) {
@@ -216,7 +243,13 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       for (int i = 0; i < ENFLOW_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
     }
 #endif
-  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) return;
+  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) {   // error raised; keep the ticket count
+    if (!REV && A.ticket) {
+      if (threadIdx.x == 0) A.ldj_mol[blockIdx.x] = 0.f;
+      ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
+    }
+    return;
+  }
   STAMP(0);
   const int tid = threadIdx.x;
   const int n = M.n, nf = A.nf;
@@ -231,11 +264,11 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
 
   if (!REV) {
     if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-      ldj += argmax_dequant(sm, A.dequant, A.noise, M.a0, n, nf);
+      ldj += argmax_dequant(sm, A.dequant, A.noise_src(), M.a0, n, nf);
     } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
       for (int e = tid; e < n * nf; e += BLOCK) {
         const int a = e / nf, q = e - a * nf;
-        sm.h[a * NFP + q] += A.dequant_scale * A.noise[(size_t)M.a0 * nf + e];
+        sm.h[a * NFP + q] += A.dequant_scale * A.noise_src().uniform((size_t)M.a0 * nf + e);
       }
       __syncthreads();
     }
@@ -404,6 +437,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
     if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
   }
   if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
+  if (!REV && A.ticket) ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
   STAMP(7);
   STAMP_FLUSH
 }
@@ -453,7 +487,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float
   if (!load_molecule(sm, A, M, LOAD_H)) return;
   const int tid = threadIdx.x;
   const int n = M.n, nf = A.nf;
-  const float lq = argmax_dequant(sm, A.dequant, A.noise, M.a0, n, nf);
+  const float lq = argmax_dequant(sm, A.dequant, A.noise_src(), M.a0, n, nf);
   for (int e = tid; e < n * nf; e += BLOCK) {
     const int a = e / nf, q = e - a * nf;
     z[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
@@ -727,6 +761,47 @@ static int check_common(int num_mols, int max_mol_atoms, int nf, int H) {
   return 0;
 }
 
+int enflow_lf_forward_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                             float* h, float* g, float* pos, float* vel,
+                             const float* layers, int n_layers,
+                             int dequant_kind, const float* dequant, const float* noise,
+                             uint64_t noise_seed, uint64_t noise_offset,
+                             float dequant_scale, float dt, float cw,
+                             float* ldj_mol, float* ldj_total, uint32_t* ticket, int32_t* err_flag,
+                             uint64_t* pair_stats, float* tape, int32_t* pair_counts, int gemm_precision,
+                             void* stream) {
+  int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
+      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
+  if (rc) return rc;
+  if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
+  if (!h || !g || !pos || !vel || !ldj_mol || !ldj_total || !err_flag) return -1;
+  // training tape: the backward handles molecules of <= 64 atoms (unblocked pair lists)
+  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr || max_mol_atoms > 64)) return -1;
+  // the tape feeds the fp32-accurate backward: it must come from an fp32-accurate forward
+  if (tape != nullptr && (gemm_precision & 0xff) == ENFLOW_PREC_BF16) return -1;
+  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
+             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
+             reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
+  A.h_in = h_in; A.g_in = g_in; A.pos_in = pos_in; A.vel_in = vel_in;
+  A.seed = noise_seed; A.offset = noise_offset;
+  const double cst = dequant_kind == ENFLOW_DEQUANT_ARGMAX ? -0.5 * kLog2Pi : 0.0;
+  A.ticket = num_mols > 0 ? ticket : nullptr;
+  A.ldj_total = ldj_total;
+  A.ldj_cst = cst;
+  if (num_mols > 0) {
+#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, false>(gemm_precision, num_mols, S(stream), A)
+    DISPATCH_HN(H, max_mol_atoms, CALL);
+#undef CALL
+  }
+  if (A.ticket == nullptr)
+    ENFLOW_TIMED("reduce_ldj_kernel", S(stream),
+                 hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
                           const int32_t* mol_ptr, const float* r_cut, const float* box,
                           float* h, float* g, float* pos, float* vel,
@@ -735,27 +810,38 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           float dequant_scale, float dt, float cw,
                           float* ldj_mol, float* ldj_total, int32_t* err_flag, uint64_t* pair_stats,
                           float* tape, int32_t* pair_counts, int gemm_precision, void* stream) {
+  const int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if (rc) return rc;
+  if (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) return -1;   // ABI <= 7: the caller's draws
+  return enflow_lf_forward_io_f32(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, nullptr, nullptr,
+                                  nullptr, nullptr, h, g, pos, vel, layers, n_layers, dequant_kind, dequant, noise,
+                                  0, 0, dequant_scale, dt, cw, ldj_mol, ldj_total, nullptr, err_flag, pair_stats, tape,
+                                  pair_counts, gemm_precision, stream);
+}
+
+int enflow_lf_reverse_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                             float* h, float* g, float* pos, float* vel,
+                             const float* layers, int n_layers,
+                             int dequant_kind, float dt, float cw,
+                             int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
+                             void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
   if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
       (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
-  if (n_layers < 0 || (dequant_kind != ENFLOW_DEQUANT_NONE && !noise) ||
-      (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
-  // training tape: the backward handles molecules of <= 64 atoms (unblocked pair lists)
-  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr || max_mol_atoms > 64)) return -1;
-  // the tape feeds the fp32-accurate backward: it must come from an fp32-accurate forward
-  if (tape != nullptr && (gemm_precision & 0xff) == ENFLOW_PREC_BF16) return -1;
-  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
-             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
-             reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
+  if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
+  if (!h || !g || !pos || !vel || !err_flag) return -1;
+  (void)num_atoms;
+  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
+             0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag, nullptr};
+  A.h_in = h_in; A.g_in = g_in; A.pos_in = pos_in; A.vel_in = vel_in;
   if (num_mols > 0) {
-#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, false>(gemm_precision, num_mols, S(stream), A)
+#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, true>(gemm_precision, num_mols, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
-  const double cst = dequant_kind == ENFLOW_DEQUANT_ARGMAX ? -0.5 * kLog2Pi : 0.0;
-  ENFLOW_TIMED("reduce_ldj_kernel", S(stream),
-               hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total));
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
@@ -766,20 +852,9 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                           int dequant_kind, float dt, float cw,
                           int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
                           void* stream) {
-  int rc = check_common(num_mols, max_mol_atoms, nf, H);
-  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
-      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
-  if (rc) return rc;
-  if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
-  (void)num_atoms;
-  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
-             0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag, nullptr};
-  if (num_mols > 0) {
-#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, true>(gemm_precision, num_mols, S(stream), A)
-    DISPATCH_HN(H, max_mol_atoms, CALL);
-#undef CALL
-  }
-  return hipGetLastError() == hipSuccess ? 0 : -2;
+  return enflow_lf_reverse_io_f32(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, nullptr, nullptr,
+                                  nullptr, nullptr, h, g, pos, vel, layers, n_layers, dequant_kind, dt, cw, argmax_idx,
+                                  max_idx, err_flag, gemm_precision, stream);
 }
 
 int enflow_one_hot_f32(const int32_t* idx, int num_atoms, int width, float* out, void* stream) {

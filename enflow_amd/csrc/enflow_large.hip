@@ -446,7 +446,7 @@ __global__ void __launch_bounds__(BLOCK) lg_dequant_kernel(LgArgs B, int kind, c
       sm.h[e] = (a < rb && q < nf) ? B.h[(size_t)(g0 + a) * nf + q] : 0.f;
     }
     __syncthreads();
-    lq = argmax_dequant(sm, dq, noise, g0, rb, nf);
+    lq = argmax_dequant(sm, dq, NoiseSrc{noise, 0, 0}, g0, rb, nf);
     for (int e = tid; e < rb * nf; e += BLOCK) {
       const int a = e / nf, q = e - a * nf;
       B.h[(size_t)g0 * nf + e] = sm.h[a * NFP + q];

@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 7
+#define ENFLOW_ABI 8
 #define WAVES 4
 #define BLOCK 256
 #define NFMAX 8
@@ -1653,8 +1653,42 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
 
 // ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
 // returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
+// The dequantiser's draws made in the kernel (noise == NULL): Philox4x32-10
+// (Salmon et al., SC'11) keyed by the caller's 64-bit seed, counter = (element
+// index, 0, 64-bit offset); N(0,1) by Box-Muller (argmax.py:16's torch.randn),
+// U[0,1) for Floor (floor.py's torch.rand).  Element index = atom * nf + q.
+__device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+  }
+  return c;
+}
+struct NoiseSrc {
+  const float* buf;              // caller's draws, or NULL: drawn here
+  unsigned long long seed, offset;
+  __device__ __forceinline__ uint4 bits(size_t e) const {
+    return philox4x32_10(make_uint4((uint32_t)e, (uint32_t)(e >> 32), (uint32_t)offset, (uint32_t)(offset >> 32)),
+                         (uint32_t)seed, (uint32_t)(seed >> 32));
+  }
+  __device__ __forceinline__ float normal(size_t e) const {
+    if (buf) return buf[e];
+    const uint4 r = bits(e);
+    const float u1 = (float)((r.x >> 8) + 1u) * 5.9604644775390625e-8f;   // (0, 1]
+    const float u2 = (float)(r.y >> 8) * 5.9604644775390625e-8f;          // [0, 1)
+    return sqrtf(-2.f * logf(u1)) * cosf(6.2831853071795865f * u2);
+  }
+  __device__ __forceinline__ float uniform(size_t e) const {
+    if (buf) return buf[e];
+    return (float)(bits(e).x >> 8) * 5.9604644775390625e-8f;
+  }
+};
+
 template <int H, int NMAX, int RB>
-__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const float* __restrict__ noise,
+__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const NoiseSrc noise,
                                 int a0, int n, int nf) {
   using S = Smem<H, NMAX, RB>;
   constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
@@ -1713,7 +1747,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
       for (int q = 0; q < NFMAX; ++q) {
         if (q < nf) {
           const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
-          u[q] = tr + noise[(size_t)(a0 + ag) * nf + q] * expf(ls);
+          u[q] = tr + noise.normal((size_t)(a0 + ag) * nf + q) * expf(ls);
           hv[q] = sm.h[ag * NFP + q];
           T += hv[q] * u[q];
           lq += -0.5f * u[q] * u[q] - ls;
@@ -1771,6 +1805,19 @@ struct FlowArgs {
   float* tape;                 // optional (training): TapeLayout block
   int32_t* pair_counts;        // optional (training): [n_layers][num_mols] unique pairs
   int num_mols, num_atoms;
+  // ABI 8 (out-of-place, self-contained forward): inputs read from *_in when set
+  // (the outputs h / g / pos / vel are then written only); noise == NULL draws
+  // in the kernel (NoiseSrc); ticket != NULL: the last workgroup to finish
+  // reduces ldj_mol into ldj_total (+ ldj_cst) and resets the ticket
+  const float* h_in = nullptr;
+  const float* g_in = nullptr;
+  const float* pos_in = nullptr;
+  const float* vel_in = nullptr;
+  unsigned long long seed = 0, offset = 0;
+  uint32_t* ticket = nullptr;
+  float* ldj_total = nullptr;
+  double ldj_cst = 0.0;
+  __device__ __forceinline__ NoiseSrc noise_src() const { return NoiseSrc{noise, seed, offset}; }
 };
 
 enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
@@ -1791,19 +1838,21 @@ __device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowA
   if (what & LOAD_POS) {
     M.rc = A.r_cut[m];
     for (int e = tid; e < n * 3; e += BLOCK) {
-      sm.pos[e] = A.pos[(size_t)M.a0 * 3 + e];
+      sm.pos[e] = (A.pos_in ? A.pos_in : A.pos)[(size_t)M.a0 * 3 + e];
       // blocked images keep only the first atom's box (the edge box); the
       // per-atom pbc boxes are read from global memory in the update
       if (!Smem<H, NMAX, RB>::BLOCKED || e < 3) sm.boxa[e] = A.box[(size_t)M.a0 * 3 + e];
     }
   }
   if (what & LOAD_VELG)
-    for (int e = tid; e < n * 3; e += BLOCK) sm.vel[e] = A.vel[(size_t)M.a0 * 3 + e];
+    for (int e = tid; e < n * 3; e += BLOCK) sm.vel[e] = (A.vel_in ? A.vel_in : A.vel)[(size_t)M.a0 * 3 + e];
+  const float* const hin = A.h_in ? A.h_in : A.h;
+  const float* const gin = A.g_in ? A.g_in : A.g;
   for (int e = tid; e < n * NFP; e += BLOCK) {   // rows zero-padded past nf
     const int a = e / NFP, q = e - a * NFP;
     const size_t src = (size_t)(M.a0 + a) * nf + q;
-    if (what & LOAD_H) sm.h[e] = q < nf ? A.h[src] : 0.f;
-    if (what & LOAD_VELG) sm.g[e] = q < nf ? A.g[src] : 0.f;
+    if (what & LOAD_H) sm.h[e] = q < nf ? hin[src] : 0.f;
+    if (what & LOAD_VELG) sm.g[e] = q < nf ? gin[src] : 0.f;
   }
   if (tid == 0) sm.err = 0;
   __syncthreads();

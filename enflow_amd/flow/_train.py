@@ -31,14 +31,18 @@ class _FlowFunction(torch.autograd.Function):
         n_layers = len(flow.networks)
         A = h.shape[0]
         M = meta["mol_ptr"].numel() - 1
-        h_in = h.detach().clone()
-        hw, gw, pw, vw = (t.detach().clone() for t in (h, g, pos, vel))
+        # out of place: the kernel reads the inputs and writes fresh outputs (the
+        # input h is kept for the dequantiser's backward as is, no copy)
+        src = tuple(t.detach().contiguous() for t in (h, g, pos, vel))
+        h_in = src[0]
+        hw, gw, pw, vw = (torch.empty_like(t) for t in src)
         tape = torch.empty(max(L.enflow_lf_tape_size(A, nf, hid, n_layers), 1), dtype=torch.float32, device=dev)
         # fused: unique pairs [n_layers][M]; large: the backward's pair rows per layer
         counts = torch.zeros(max(n_layers * (1 if meta["large"] else M), 1), dtype=torch.int32, device=dev)
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        st = torch.zeros(2, dtype=torch.int32, device=dev)   # error word, ldj reduction ticket
+        err = st[:1]
         prec = flow._prec()
         if (prec & 0xff) == _lib.PREC_BF16:
             # the tape feeds the fp32-accurate backward: record it from an fp32-accurate forward
@@ -49,7 +53,8 @@ class _FlowFunction(torch.autograd.Function):
                 warnings.warn("enflow_amd: gemm_precision='bf16' is a generate-path setting; the training "
                               "forward runs f16x3", RuntimeWarning, stacklevel=2)
         flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"], meta["max_n"],
-                             meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts, prec=prec)
+                             meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts, prec=prec,
+                             src=src, ticket=st[1:])
         # queue the backward's weight packing (cached on the parameters' versions,
         # which cannot change before this graph's backward) and the dequantiser's
         # flat parameters behind the forward kernel, ahead of the error check's sync

@@ -141,13 +141,18 @@ class LFIntegrator(BaseFlow):
 
     # ------------------------------------------------------------------
     def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
-                        ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None, prec=None):
-        """In-place fused forward on preallocated fp32 device buffers (no
-        host sync, no allocation): the entry point the benchmark times.
-        Molecules past the fused kernel's LDS image (> enflow_max_atoms())
-        go through the layer-by-layer large-system kernels
-        (enflow_lf_forward_large_f32; needs a workspace, allocated once per
-        shape)."""
+                        ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None, prec=None,
+                        src=None, noise_key=(0, 0), ticket=None):
+        """Fused forward on preallocated fp32 device buffers (no host sync, no
+        allocation): the entry point the benchmark times.  ``src`` = (h, g,
+        pos, vel) inputs read by the kernel (None: h, g, pos, vel are updated
+        in place); ``noise`` None draws the dequantiser's noise in the kernel
+        (Philox keyed by ``noise_key`` = (seed, offset)); ``ticket`` (uint32
+        device word, zero) reduces log|detJ| in the same launch
+        (enflow_lf_forward_io_f32).  Molecules past the fused kernel's LDS
+        image (> enflow_max_atoms()) go through the layer-by-layer
+        large-system kernels (enflow_lf_forward_large_f32; needs a workspace,
+        allocated once per shape)."""
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         dev = h.device
@@ -158,6 +163,12 @@ class LFIntegrator(BaseFlow):
         # training past the fused backward's molecule size records its tape on the
         # large-system path (pair_counts then holds the per-layer pair rows)
         if _lib.is_large(max_mol_atoms) or (tape is not None and max_mol_atoms > _lib.TRAIN_MAX_ATOMS):
+            if src is not None:      # the layer-by-layer path updates its state in place
+                for o, i in zip((h, g, pos, vel), src):
+                    if o.data_ptr() != i.data_ptr():
+                        o.copy_(i)
+            if noise is None and kind != _lib.DEQUANT_NONE:
+                noise = _host_noise(kind, h.shape, dev)
             ws = _lib.large_workspace(mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, dev)
             _lib.check(L.enflow_lf_forward_large_f32(
                 mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
@@ -168,22 +179,30 @@ class LFIntegrator(BaseFlow):
                 _lib.ptr(ws), ws.numel(), _lib.stream_ptr(dev)),
                 "enflow_lf_forward_large_f32")
             return
-        _lib.check(L.enflow_lf_forward_f32(
+        si = (None,) * 4 if src is None else tuple(_lib.ptr(t) for t in src)
+        _lib.check(L.enflow_lf_forward_io_f32(
             mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
-            _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
+            _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
             _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
-            _lib.ptr(noise), scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total),
+            _lib.ptr(noise), int(noise_key[0]) & 0xFFFFFFFFFFFFFFFF, int(noise_key[1]) & 0xFFFFFFFFFFFFFFFF,
+            scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total), _lib.ptr(ticket),
             _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), prec,
-            _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
+            _lib.stream_ptr(dev)), "enflow_lf_forward_io_f32")
 
-    def reverse_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, argmax_idx, max_idx, err):
-        """In-place fused reverse on preallocated fp32 device buffers (no host
-        sync, no allocation); with ArgMax, argmax_idx / max_idx receive the
-        dequantiser's indices (enflow_one_hot_f32 materialises the one-hot)."""
+    def reverse_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, argmax_idx, max_idx, err,
+                        src=None):
+        """Fused reverse on preallocated fp32 device buffers (no host sync, no
+        allocation); ``src`` = (h, g, pos, vel) inputs (None: in place); with
+        ArgMax, argmax_idx / max_idx receive the dequantiser's indices
+        (enflow_one_hot_f32 materialises the one-hot)."""
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         L = _lib.lib()
         if _lib.is_large(max_mol_atoms):
+            if src is not None:
+                for o, i in zip((h, g, pos, vel), src):
+                    if o.data_ptr() != i.data_ptr():
+                        o.copy_(i)
             ws = _lib.large_workspace(mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, h.device)
             _lib.check(L.enflow_lf_reverse_large_f32(
                 mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
@@ -192,20 +211,25 @@ class LFIntegrator(BaseFlow):
                 _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), self._prec(), _lib.ptr(ws), ws.numel(),
                 _lib.stream_ptr(h.device)), "enflow_lf_reverse_large_f32")
             return
-        _lib.check(L.enflow_lf_reverse_f32(
+        si = (None,) * 4 if src is None else tuple(_lib.ptr(t) for t in src)
+        _lib.check(L.enflow_lf_reverse_io_f32(
             mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
-            _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
+            _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
             _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
             _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), self._prec(), _lib.stream_ptr(h.device)),
-            "enflow_lf_reverse_f32")
+            "enflow_lf_reverse_io_f32")
 
     def _state(self, data):
+        """Kernel inputs (fp32, contiguous, on the device: views of the data's
+        tensors when they already are) and fresh output buffers."""
         _lib.require_gpu(data.pos)
         dev = data.pos.device
-        f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous().clone()  # noqa: E731
+        f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
         rc = torch.as_tensor(data.r_cut, device=dev).to(torch.float32).reshape(-1).contiguous()
         ptr, max_n = batch_meta(data, dev)
-        return dict(h=f(data.h), g=f(data.g), pos=f(data.pos), vel=f(data.vel),
+        src = tuple(f(t) for t in (data.h, data.g, data.pos, data.vel))
+        h, g, pos, vel = (torch.empty_like(t) for t in src)
+        return dict(h=h, g=g, pos=pos, vel=vel, src=src,
                     box=data.box.detach().to(device=dev, dtype=torch.float32).contiguous(), r_cut=rc,
                     mol_ptr=ptr, max_n=max_n, dev=dev)
 
@@ -222,22 +246,23 @@ class LFIntegrator(BaseFlow):
             return flow_forward_train(self, data, noise, check_errors)
         s = self._state(data)
         dev = s["dev"]
-        kind = self._dequant_kind()
+        key = (0, 0)
         if noise is None:
-            if kind == _lib.DEQUANT_ARGMAX:
-                noise = torch.randn(s["h"].shape, device=dev, dtype=torch.float32)
-            elif kind == _lib.DEQUANT_FLOOR:
-                noise = torch.rand(s["h"].shape, device=dev, dtype=torch.float32)
+            # the dequantiser's draws are made in the kernel (N(0,1) / U[0,1),
+            # argmax.py:16 / floor.py), keyed from torch's generator so that
+            # torch.manual_seed makes runs reproducible
+            key = (int(torch.randint(0, 2 ** 62, (1,)).item()), 0)
         else:
             noise = noise.to(device=dev, dtype=torch.float32).contiguous()
         M = s["mol_ptr"].numel() - 1
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
-        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        st = _lib.status_word(dev) if check_errors else torch.zeros(2, dtype=torch.int32, device=dev)
         self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
-                             s["max_n"], noise, ldj_mol, ldj, err)
+                             s["max_n"], noise, ldj_mol, ldj, st[:1], src=s["src"], noise_key=key,
+                             ticket=st[1:])
         if check_errors:
-            _lib.raise_on_err(err)
+            _lib.raise_on_err(st[:1], reset=True)
         dt = data.h.dtype
         data.h, data.g = s["h"].to(dt), s["g"].to(dt)
         data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
@@ -256,7 +281,7 @@ class LFIntegrator(BaseFlow):
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         L = _lib.lib()
         self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"], s["max_n"],
-                             idx, mx, err)
+                             idx, mx, err, src=s["src"])
         if check_errors:
             _lib.raise_on_err(err)
         dt = data.h.dtype
@@ -271,3 +296,10 @@ class LFIntegrator(BaseFlow):
         data.g = s["g"].to(dt)
         data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
         return data
+
+
+def _host_noise(kind, shape, dev):
+    """Draws for the large-system path (it takes the caller's noise)."""
+    if kind == _lib.DEQUANT_ARGMAX:
+        return torch.randn(shape, device=dev, dtype=torch.float32)
+    return torch.rand(shape, device=dev, dtype=torch.float32)

@@ -73,7 +73,16 @@ class Geom:
         raise ValueError(kind)
 
 
+_IDX_CACHE = {}
+
+
 def _indices(spec, shape, g, device):
+    """(padded sizes, index tuple on `device`); cached per shape, so a training
+    step does no host-to-device index copies (they would stall the stream)."""
+    key = (tuple(spec), tuple(shape), g.H, g.Hp, g.fin, g.fout, g.F, str(device))
+    hit = _IDX_CACHE.get(key)
+    if hit is not None:
+        return hit
     dims = [g.index(k, d) for k, d in zip(spec, shape)]
     sizes = tuple(s for s, _ in dims)
     idx = [i.to(device) for _, i in dims]
@@ -81,6 +90,7 @@ def _indices(spec, shape, g, device):
         idx = (idx[0][:, None], idx[1][None, :])
     else:
         idx = (idx[0],)
+    _IDX_CACHE[key] = (sizes, idx)
     return sizes, idx
 
 
@@ -106,11 +116,14 @@ def unpad_grads(flat, named, table, g):
     ({name: grad}, floats consumed)."""
     out, off = {}, 0
     for k, p in named:
-        sizes, idx = _indices(table[k], p.shape, g, flat.device)
+        if g.identity:
+            sizes, idx = tuple(p.shape), None
+        else:
+            sizes, idx = _indices(table[k], p.shape, g, flat.device)
         n = 1
         for d in sizes:
             n *= d
         gp = flat[off:off + n].view(sizes)
-        out[k] = gp if g.identity else gp[idx]
+        out[k] = gp if idx is None else gp[idx]
         off += n
     return out, off

@@ -53,7 +53,9 @@ extern "C" {
 /* ABI version of this header; bump on any signature or error-semantics change (6: ENFLOW_ERR_RANGE,
  * bf16 + tape rejected, NaN-poisoned gradients on a backward error, enflow_timing_*; 7: training
  * on large systems -- tape / pair_rows of enflow_lf_forward_large_f32, enflow_lf_backward_large_f32,
- * enflow_alchemical_nll_backward_f32 for any molecule size). */
+ * enflow_alchemical_nll_backward_f32 for any molecule size; 8: out-of-place, self-contained
+ * forward / reverse -- enflow_lf_forward_io_f32 (in-kernel dequantiser draws, in-launch
+ * log|detJ| reduction), enflow_lf_reverse_io_f32). */
 int enflow_abi_version(void);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept. */
@@ -152,6 +154,48 @@ int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int no
                           int dequant_kind, float dt, float coords_weight,
                           int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
                           int gemm_precision, void* stream);
+
+/*
+ * enflow_lf_forward_f32 as one self-contained launch (the reference's
+ * LFIntegrator.forward returns new tensors, dynamics.py:10-24; nothing here
+ * needs a copy, a separate noise draw or a separate reduction):
+ *   h_in, g_in, pos_in, vel_in : inputs, read only (NULL: the corresponding
+ *                 output buffer is read, i.e. in place); outputs h, g, pos, vel
+ *   noise       : the caller's draws as in enflow_lf_forward_f32, or NULL with
+ *                 ARGMAX / FLOOR: drawn in the kernel, Philox4x32-10 keyed by
+ *                 noise_seed, counter (atom * node_nf + q, offset noise_offset);
+ *                 N(0,1) by Box-Muller for ARGMAX, U[0,1) for FLOOR.  A caller
+ *                 advances noise_offset (or the seed) between calls.
+ *   ticket      : device uint32, zero before the first call on it; the last
+ *                 workgroup to finish reduces ldj_mol into ldj_total (same
+ *                 fixed-order double sum as the separate reduction) and resets
+ *                 it to zero.  One ticket per concurrently running call; NULL:
+ *                 a second launch reduces, as enflow_lf_forward_f32.
+ * Everything else as enflow_lf_forward_f32 (enflow_lf_forward_f32 is this call
+ * with the inputs NULL, the caller's noise and no ticket).
+ */
+int enflow_lf_forward_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                             float* h, float* g, float* pos, float* vel,
+                             const float* layers, int n_layers,
+                             int dequant_kind, const float* dequant, const float* noise,
+                             uint64_t noise_seed, uint64_t noise_offset,
+                             float dequant_scale, float dt, float coords_weight,
+                             float* ldj_mol, float* ldj_total, uint32_t* ticket, int32_t* err_flag,
+                             uint64_t* pair_stats, float* tape, int32_t* pair_counts,
+                             int gemm_precision, void* stream);
+
+/* enflow_lf_reverse_f32 out of place (LFIntegrator.reverse, dynamics.py:26-37):
+ * inputs h_in, g_in, pos_in, vel_in (NULL: in place), outputs h, g, pos, vel. */
+int enflow_lf_reverse_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                             float* h, float* g, float* pos, float* vel,
+                             const float* layers, int n_layers,
+                             int dequant_kind, float dt, float coords_weight,
+                             int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
+                             int gemm_precision, void* stream);
 
 /* ------------------------------------------------------------------------
  * Large systems: molecules / periodic boxes with more than enflow_max_atoms()

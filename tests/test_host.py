@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 7
+    assert L.enflow_abi_version() == 8
     assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
@@ -57,6 +57,15 @@ def test_argument_errors_launch_nothing():
     args[3] = 5
     args[-2] = 7    # unknown GEMM precision
     assert L.enflow_lf_forward_f32(*args) == -1
+    # the out-of-place entry (ABI 8): same checks, and NULL outputs / ldj / error word are rejected
+    io = [1, 300, 300, 5, 128] + [None] * 12 + [1, 1, None, None, 0, 0, 0.0, 0.1, 1.0] + [None] * 7 + [1, None]
+    assert L.enflow_lf_forward_io_f32(*io) == -3
+    io[2] = 20
+    assert L.enflow_lf_forward_io_f32(*io) == -1
+    rev = [1, 300, 300, 5, 128] + [None] * 12 + [1, 0, 0.1, 1.0, None, None, None, 1, None]
+    assert L.enflow_lf_reverse_io_f32(*rev) == -3
+    rev[2] = 20
+    assert L.enflow_lf_reverse_io_f32(*rev) == -1
 
 
 def test_backward_sizes_and_argument_errors():

@@ -42,8 +42,15 @@ def main():
                 work[k].copy_(inp[k])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
-                                  inp["mol_ptr"], atoms, noise, ldj_mol, ldj, err)
+            # the ABI-7 entry (in place, caller's noise): present in every build compared
+            hid, nf, cw = model._geometry()
+            _lib.check(_lib.lib().enflow_lf_forward_f32(
+                mols, work["h"].shape[0], atoms, nf, hid, _lib.ptr(inp["mol_ptr"]), _lib.ptr(inp["r_cut"]),
+                _lib.ptr(inp["box"]), _lib.ptr(work["h"]), _lib.ptr(work["g"]), _lib.ptr(work["pos"]),
+                _lib.ptr(work["vel"]), _lib.ptr(model.packed_layers(dev)), len(model.networks), _lib.DEQUANT_ARGMAX,
+                _lib.ptr(model.dequantize.packed(dev, hid)), _lib.ptr(noise), 0.0, float(model.dt), cw,
+                _lib.ptr(ldj_mol), _lib.ptr(ldj), _lib.ptr(err), None, None, None, model._prec(),
+                _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
             e1.record()
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
