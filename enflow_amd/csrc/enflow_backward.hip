@@ -25,6 +25,7 @@
 
 #define ENFLOW_BACKWARD_TU   // -DENFLOW_STAMPS_BWD stamps this file's kernels only (tools/stamps_bwd.py)
 #include "enflow_large.h"
+#include <stdlib.h>
 
 // ---------------------------------------------------------------------------
 // packing of the backward weight section
@@ -144,13 +145,15 @@ struct BwdArgs {
   float* apos;       // [A][3]
   float* avel;
   const int32_t* pair_off;   // this layer's [num_mols + 1] row offsets (32-aligned)
-  // pair rows, tile-blocked (trow).  The pre-activations are stored, not their
-  // SiLUs: outer_acc_kernel applies silu (X operands) and aphi * wc2 * silu'
-  // (coord_nn.0's DY) on load, and this kernel re-reads p0 / pe for silu'.
+  // pair rows, tile-blocked (trow).  pre(edge_nn.0) and pre(coord_nn.0) are not
+  // stored: this kernel recomputes pre0 for silu', outer_x3_kernel recomputes
+  // pre0 from xin (X of edge_nn.2) and pre(coord_nn.0) from the message (DY of
+  // coord_nn.0, X of coord_nn.2), bitwise as here.  pe is stored as the
+  // pre-activation: outer_x3_kernel applies silu on load, this kernel re-reads it.
   float* xin;        // [P][16] h_i, h_j, radial                     (X of edge_nn.0)
-  float* p0;         // [P][H] pre(edge_nn.0)           silu -> X of edge_nn.2
+  float* p0;         // unused (ABI <= 7 layout)
   float* pe;         // [P][H] pre(edge_nn.2)           silu -> X of coord_nn.0 (the message)
-  float* pc;         // [P][H] pre(coord_nn.0)          silu -> X of coord_nn.2; DY of coord_nn.0
+  float* pc;         // unused
   float* dp0;        // [P][H] d pre(edge_nn.0)                      (DY of edge_nn.0)
   float* dpe;        // [P][H] d pre(edge_nn.2)                      (DY of edge_nn.2)
   float* aphi;       // [P]    d phi                                 (DY of coord_nn.2)
@@ -671,8 +674,11 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     // the molecule's tile-blocked rows (trow): buffer resources on its first
     // row, per element a wave-uniform byte offset (tile, feature) + the lane's
     const size_t nrow = (size_t)TT_all * 32;
-    const rsrc_t rp0 = rows_rsrc(B.p0 + prow0 * H, nrow * H), rpe = rows_rsrc(B.pe + prow0 * H, nrow * H);
-    const rsrc_t rpc = rows_rsrc(B.pc + prow0 * H, nrow * H);
+    const rsrc_t rpe = rows_rsrc(B.pe + prow0 * H, nrow * H);
+    const bool store_pc = B.pc != nullptr;   // A/B diagnostic (ENFLOW_STORE_PC): the pass reads pc rows
+    const bool store_p0 = B.p0 != nullptr;   // A/B diagnostic (ENFLOW_STORE_P0): the pass reads p0 rows
+    const rsrc_t rp0 = rows_rsrc((store_p0 ? B.p0 : B.pe) + prow0 * H, nrow * H);
+    const rsrc_t rpc = rows_rsrc((store_pc ? B.pc : B.pe) + prow0 * H, nrow * H);
     const rsrc_t rdp0 = rows_rsrc(B.dp0 + prow0 * H, nrow * H), rdpe = rows_rsrc(B.dpe + prow0 * H, nrow * H);
     // edge_nn.0 input rows [h_i, h_j, radial]: 16 wide, 32 when 2 nf + 1 > 16 (nf = 8)
     const int XW = xin_width(nf);
@@ -756,8 +762,11 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       if (XW > 16 && hh == 0)   // q = 16 = 2 nf: the radial of an nf = 8 layer
         ST_OUT(rxin, j * 4, gt * XW * 128 + 16 * 128, valid ? radial : 0.f);
 
-      // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1
-      f32x16 x0[NT];
+      // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1.  Run twice per
+      // tile (here, and again for silu'(pre0) after GEMM4) instead of parking pre0
+      // in HBM: the same instruction sequence on the same operands, so both are
+      // bitwise the forward's pre0 (outer_x3_kernel recomputes it from xin, too)
+      auto gemm0 = [&](f32x16 (&x0)[NT]) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
       if constexpr (PREC == PREC_F16X3) {
@@ -805,8 +814,11 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
             x0[t] = mfma32(bload(W, lane * 4, (L.we1f + (t * (NFMAX + 1) + s) * 64) * 4), b, x0[t]);
         }
       }
+      };
+      f32x16 x0[NT];
+      gemm0(x0);
       STAMP(4);
-      // x1 = silu(pre0) (kept: B operand of GEMM1); pre0 stored
+      // x1 = silu(pre0) (kept: B operand of GEMM1)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -816,7 +828,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float z = x0[t][4 * g4 + u] + b[u];
-            ST_PARK(rp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
+            if (store_p0) ST_PARK(rp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
             x0[t][4 * g4 + u] = silu_f(z);
           }
         }
@@ -827,7 +839,6 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) ev[t] = (f32x16)0.f;
       chain_prec_fill<PREC, NT, 1>(W, L.we2f, L.we2x, L.we2b, x0, ev, lane, nofill);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pre0 rows landed (drained by the chain anyway)
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -876,8 +887,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(cv[t][4 * g4 + u], inv2, b[u]);
             const float s = sigmoid_f(z);
-            part = fmaf(w2[u], z * s, part);
-            ST_OUT(rpc, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
+            part = fmaf(w2[u], z * s, part);   // pc: recomputed by outer_x3_kernel (unless ENFLOW_STORE_PC)
+            if (store_pc) ST_OUT(rpc, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
             cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
           }
         }
@@ -960,21 +971,19 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       for (int t = 0; t < NT; ++t) ax[t] = (f32x16)0.f;
       float sc4 = 1.f;
       if constexpr (PREC == PREC_F16X3) sc4 = tile_pow2_scale(ae);   // ae already stored unscaled
-      chain_prec_fill<PREC, NT, 1>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, [&](int i) {
-        const int t = i >> 2, g4 = i & 3;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) rl[t][4 * g4 + u] = bload(rp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7));
-      });
+      chain_prec_fill<PREC, NT, 1>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, nofill);
       STAMP(10);
+      gemm0(rl);   // pre0 again (bitwise the first pass's)
       const float u4 = inv1 * sc4;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(sm.bias + f0);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            ax[t][4 * g4 + u] = ax[t][4 * g4 + u] * u4 * dsilu_f(rl[t][4 * g4 + u]);
+            ax[t][4 * g4 + u] = ax[t][4 * g4 + u] * u4 * dsilu_f(rl[t][4 * g4 + u] + b[u]);
             ST_OUT(rdp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), ax[t][4 * g4 + u]);
           }
         }
@@ -1150,7 +1159,15 @@ struct OuterDesc {
   const float* colv;
   int chunk;                 // rows per workgroup / partial
   float* part2;              // outer_x3_kernel with xf_dy: partials of sum_rows rowv * silu(DY source)
+  int recomp;                // outer_x3_kernel operands recomputed instead of read (RECOMP_*)
+  const float* Lp;           // RECOMP_*: the layer's packed forward weights
+  int nf;                    // RECOMP_X0: node features (xin row layout)
 };
+// RECOMP_X0: X = silu(pre0), pre0 = edge_nn.0 . xin + be1 (the X source is xin, width ldx);
+// RECOMP_PC: DY = rowv * silu'(pc), pc = coord_nn.0 . X + bc1 (X read; no DY source), and
+//            part2 gets coord_nn.2's sum_rows rowv * silu(pc).
+// Both are the layer backward's instruction sequences on the same operands: bitwise its values.
+enum { RECOMP_NONE = 0, RECOMP_X0 = 1, RECOMP_PC = 2 };
 #define OUTER_MAX 10
 struct OuterBatch {
   OuterDesc d[OUTER_MAX];
@@ -1339,47 +1356,59 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 // (max |x| -> [2^12, 2^13), as the layer backward's adjoint tiles) before the
 // hi / lo split; the stage's three-product sums land in a scratch accumulator
 // that is added to the running one with the exact inverse scale.
+//
+// Recomputed operands (OuterDesc::recomp) trade HBM bytes for MFMAs: the layer
+// backward stores neither pre(edge_nn.0) nor pre(coord_nn.0) (2 x H floats per
+// pair row written and read back), wave w rebuilds output tile w (features
+// 32 w .. 32 w + 31) of the stage's 32 rows in the forward's "weights = A"
+// orientation (lane = row, registers = features) from the packed forward
+// fragments, and writes it to the LDS stage.
 #define OX_LD 36   // LDS column stride (floats): 16-byte aligned operand reads
-#ifndef ENFLOW_OX_DEPTH
-#define ENFLOW_OX_DEPTH 1    // stages of rows in flight ahead of the MFMAs (A/B knob)
-#endif
 #ifndef ENFLOW_OUTER_WPS
 #define ENFLOW_OUTER_WPS 2   // outer_x3_kernel occupancy hint (A/B knob)
 #endif
-__global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBatch ob) {
-  const int bid = blockIdx.x;
-  const int k = find_desc(ob, bid);
-  const OuterDesc& D = ob.d[k];
-  const int local = bid - ob.start[k];
-  const int chunk = local / D.nb, nbi = local - chunk * D.nb;
-  const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
-  const int r0 = chunk * D.chunk;
-  if (r0 >= rows) return;
-  const int r1 = min(rows, r0 + D.chunk);
+static_assert(ENFLOW_OUTER_X3 == 1, "pair-row weight gradients run on outer_x3_kernel (recomputed operands)");
+
+template <int H, int RCM>
+__device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int nbi, int r0, int r1,
+                                              float (*sd)[128][OX_LD], float (*sx)[128][OX_LD]) {
+  constexpr int NT = H / 32;
   const int NB = D.N + (D.outB ? 1 : 0);
   const int n0 = nbi * 128;
   const int M = D.M, N = D.N;
-  __shared__ float sd[2][128][OX_LD];
-  __shared__ float sx[2][128][OX_LD];
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int j = lane & 31, hh = lane >> 5;
   const int mh = w & 1, nh = w >> 1;
+  constexpr int rcm = RCM;
   const bool do_bias = D.outB != nullptr && nbi == 0 && tid < M;
   const bool xf_dy = D.xf_dy != 0, xf_x = D.xf_x != 0;
   const bool fold = xf_dy && D.part2 != nullptr && nbi == 0;   // coord_nn.2's gradient rides along
+  // recompute: the layer's packed forward weights
+  const int nf = rcm ? D.nf : 1;
+  const EgclLayout L = egcl_layout(H, nf);
+  const rsrc_t W = weights_rsrc(rcm ? D.Lp : nullptr, rcm ? L.total : 0);
   float wacc[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) wacc[q] = 0.f;
   float bsum = 0.f;
+  // edge_nn.0's fragments of output tile w (hi / lo per k-step): loop invariant,
+  // loaded once per workgroup and kept in registers (RECOMP_X0)
+  // (the first k-step's; nf = 8's second k-step is read when used)
+  f32x4 wfh = (f32x4)0.f, wfl = (f32x4)0.f;
+  if constexpr (rcm == RECOMP_X0) {
+    if (w < NT) {
+      wfh = bload4(W, lane * 32, (L.we1x + (w * 2) * 512) * 4);
+      wfl = bload4(W, lane * 32 + 16, (L.we1x + (w * 2) * 512) * 4);
+    }
+  }
   f32x16 acc[2][2];
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
-  // staged rows in registers: one stage ahead (ENFLOW_OX_DEPTH 1) or two
-  // (2: twice the loads in flight; slots alternate, the loop unrolled by 2)
-  struct Stage { float rd[16], rx[16], ra, xa; };
-  Stage S0, S1;
+  // staged rows in registers, one stage ahead
+  struct Stage { float rd[16], rx[16], ra, xa; bool pv; };
+  Stage S0;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
   // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
   auto gload = [&](int st, Stage& G) {
@@ -1388,40 +1417,143 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
     const float* const dblk = D.DY + ((rt * D.ldd) << 5);
     const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
     const bool pv = rb + (tid & 31) < r1;
+    G.pv = pv;
     G.ra = 0.f;
     G.xa = 1.f;
     if (xf_dy) G.ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
     if (D.xrow) G.xa = pv ? D.xrow[rb + (tid & 31)] : 0.f;
+    if constexpr (rcm != RECOMP_PC) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int c = 8 * q + (tid >> 5);
-      const unsigned e = (unsigned)(q * 256 + tid);
-      G.rd[q] = (pv && c < M) ? dblk[e] : 0.f;
-      G.rx[q] = (pv && n0 + c < N) ? xblk[e] : 0.f;
+      for (int q = 0; q < 16; ++q) {
+        const int c = 8 * q + (tid >> 5);
+        G.rd[q] = (pv && c < M) ? dblk[(unsigned)(q * 256 + tid)] : 0.f;
+      }
+    }
+    if constexpr (rcm == RECOMP_X0) {
+      // GEMM0's B operand of lane (row j, half hh), as the layer backward builds it:
+      // half 0 = h_i's row, half 1 = h_j's (+ radial in slot 7 for nf <= 7); rx[8] =
+      // radial (the second k-step of nf = 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = hh ? nf + u : u;
+        G.rx[u] = (pv && u < nf) ? xblk[q * 32 + j] : 0.f;
+      }
+      if (hh && nf <= 7) G.rx[7] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
+      G.rx[8] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = 8 * q + (tid >> 5);
+        G.rx[q] = (pv && n0 + c < N) ? xblk[(unsigned)(q * 256 + tid)] : 0.f;
+      }
     }
   };
   auto lstore = [&](int buf, Stage& G) {
-    if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
+    if constexpr (rcm != RECOMP_PC) {
+      if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float z = G.rd[q], sg = sigmoid_f(z);
-        if (fold) wacc[q] = fmaf(G.ra, z * sg, wacc[q]);
-        G.rd[q] = G.ra * (sg * (1.f + z * (1.f - sg)));
+        for (int q = 0; q < 16; ++q) {
+          const float z = G.rd[q], sg = sigmoid_f(z);
+          if (fold) wacc[q] = fmaf(G.ra, z * sg, wacc[q]);
+          G.rd[q] = G.ra * (sg * (1.f + z * (1.f - sg)));
+        }
       }
-    }
-    if (xf_x) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) G.rx[q] = silu_f(G.rx[q]);
+      for (int q = 0; q < 16; ++q) sd[buf][8 * q + (tid >> 5)][tid & 31] = G.rd[q];
     }
-    if (D.xrow) {
+    if constexpr (rcm == RECOMP_X0) {
+      if (w < NT) {   // output tile w of pre0 -> silu -> X
+        const int ks_n = gemm0_ksteps(nf);
+        f32x16 x = (f32x16)0.f;
+        for (int ks = 0; ks < ks_n; ++ks) {
+          f32x16 in;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) G.rx[q] *= G.xa;
+          for (int u = 0; u < 8; ++u) in[u] = ks == 0 ? G.rx[u] : 0.f;
+          if (ks == 1 && hh == 0) in[0] = G.rx[8];
+          f16x8 bh, bl;
+          split_f16(in, 0, bh, bl);
+          f32x4 ah = wfh, al = wfl;
+          if (ks == 1) {
+            ah = bload4(W, lane * 32, (L.we1x + (w * 2 + 1) * 512) * 4);
+            al = bload4(W, lane * 32 + 16, (L.we1x + (w * 2 + 1) * 512) * 4);
+          }
+          x = mfma_f16(ah, bh, x);
+          x = mfma_f16(ah, bl, x);
+          x = mfma_f16(al, bh, x);
+        }
+        x *= D.Lp[L.scl + 5];
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * w + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(D.Lp + L.be1 + f0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sx[buf][f0 + u][j] = G.pv ? silu_f(x[4 * g4 + u] + b[u]) : 0.f;
+        }
+      }
+    } else {
+      if (xf_x) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) G.rx[q] = silu_f(G.rx[q]);
+      }
+      if (D.xrow) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) G.rx[q] *= G.xa;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sx[buf][8 * q + (tid >> 5)][tid & 31] = G.rx[q];
     }
+  };
+  // RECOMP_PC, after the stage's X is in LDS: pc = coord_nn.0 . X + bc1 (output
+  // tile w), DY = aphi * silu'(pc) into LDS, d wc2 partial += aphi * silu(pc)
+  float (&wacc2)[16] = wacc;   // RECOMP_PC's d wc2 partials (lane = row, registers = features)
+  auto recomp_pc = [&](int buf, const Stage& G) {
+    if (w < NT) {
+      // coord_nn.0's fragments of output tile w, requested half a chain at a time
+      // (two L2 round trips per stage; resident they would cost 64 VGPRs across
+      // the stage)
+      constexpr int HALF = NT > 1 ? NT : 2;   // k-steps per request group
+      f32x16 cacc = (f32x16)0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int c = 8 * q + (tid >> 5), r = tid & 31;
-      sd[buf][c][r] = G.rd[q];
-      sx[buf][c][r] = G.rx[q];
+      for (int g = 0; g < 2 * NT; g += HALF) {
+        f32x4 ch[HALF], cl[HALF];
+#pragma unroll
+        for (int q = 0; q < HALF; ++q) {
+          const int ts = g + q;
+          const int so = (L.wc1x + ((w * NT + (ts >> 1)) * 2 + (ts & 1)) * 512) * 4;
+          ch[q] = bload4(W, lane * 32, so);
+          cl[q] = bload4(W, lane * 32 + 16, so);
+        }
+        // chain_x3_fill's per-tile order: k-steps ascending, hi.hi, hi.lo, lo.hi
+#pragma unroll
+        for (int q = 0; q < HALF; q += 2) {
+          const int t = (g + q) >> 1;
+          f32x16 X;   // input tile t in the accumulator layout (lane = row, registers = features)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) X[r] = sx[buf][32 * t + rho(r, hh)][j];
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            f16x8 bh, bl;
+            split_f16(X, s2, bh, bl);
+            cacc = mfma_f16(ch[q + s2], bh, cacc);
+            cacc = mfma_f16(ch[q + s2], bl, cacc);
+            cacc = mfma_f16(cl[q + s2], bh, cacc);
+          }
+        }
+      }
+      const float inv2 = D.Lp[L.scl + 3];
+      const float ra = G.ra;   // row j's aphi (gload's row is tid % 32 = j)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int f0 = 32 * w + 8 * g4 + 4 * hh;
+        const f32x4 b = ld4(D.Lp + L.bc1 + f0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float z = fmaf(cacc[4 * g4 + u], inv2, b[u]);
+          const float sg = sigmoid_f(z);
+          wacc2[4 * g4 + u] = fmaf(ra, z * sg, wacc2[4 * g4 + u]);
+          sd[buf][f0 + u][j] = ra * (sg * (1.f + z * (1.f - sg)));
+        }
+      }
     }
   };
   const bool use_m1 = mh * 64 + 32 < M, use_n0 = n0 + nh * 64 < N, use_n1 = n0 + nh * 64 + 32 < N;
@@ -1441,10 +1573,12 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
             const float* pb = &sx[buf][nh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2];
             av[a][ks][h2] = *reinterpret_cast<const f32x4*>(pa);
             bv[a][ks][h2] = *reinterpret_cast<const f32x4*>(pb);
+            // the scales see only the tiles that are multiplied: a recomputed stage
+            // writes rows < H only, the rest of the LDS image is stale
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              ma = fmaxf(ma, fabsf(av[a][ks][h2][u]));
-              mb = fmaxf(mb, fabsf(bv[a][ks][h2][u]));
+              if (a == 0 || use_m1) ma = fmaxf(ma, fabsf(av[a][ks][h2][u]));
+              if (a == 0 || use_n1) mb = fmaxf(mb, fabsf(bv[a][ks][h2][u]));
             }
           }
       ma = wave_max(ma);
@@ -1485,34 +1619,24 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
       for (int r = 0; r < OB_ROWS; ++r) bsum += sd[buf][tid][r];
     }
   };
-#if ENFLOW_OX_DEPTH == 2
   gload(0, S0);
   lstore(0, S0);
-  if (nst > 1) gload(1, S1);
   __syncthreads();
-  // iteration st: LDS buffer st & 1 holds stage st, slot (st + 1) & 1 stage st + 1
-  auto iter = [&](int st, Stage& cur_free, Stage& nxt) {
-    if (st + 2 < nst) gload(st + 2, cur_free);
-    compute(st & 1);
-    if (st + 1 < nst) lstore((st + 1) & 1, nxt);
+  if constexpr (rcm == RECOMP_PC) {
+    recomp_pc(0, S0);
     __syncthreads();
-  };
-  for (int st = 0; st < nst; st += 2) {
-    iter(st, S0, S1);
-    if (st + 1 < nst) iter(st + 1, S1, S0);
   }
-#else
-  gload(0, S0);
-  lstore(0, S0);
-  __syncthreads();
   for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
     if (st + 1 < nst) gload(st + 1, S0);
     compute(buf);
     if (st + 1 < nst) lstore(buf ^ 1, S0);
     __syncthreads();
+    if (rcm == RECOMP_PC && st + 1 < nst) {
+      recomp_pc(buf ^ 1, S0);
+      __syncthreads();
+    }
   }
-#endif
   float* out = D.part + (size_t)chunk * M * NB;
 #pragma unroll
   for (int a = 0; a < 2; ++a)
@@ -1524,7 +1648,17 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
         if (mm < M && nn < N) out[(size_t)mm * NB + nn] = xf_dy ? acc[a][b][r] * D.colv[mm] : acc[a][b][r];
       }
   if (do_bias) out[(size_t)tid * NB + N] = xf_dy ? bsum * D.colv[tid] : bsum;
-  if (fold) {   // fixed-order sum over the 32 rows a half-wave holds
+  if (fold && rcm == RECOMP_PC) {   // fixed-order sum over the 32 rows of each half-wave
+    if (w < NT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float v = wacc2[r];
+#pragma unroll
+        for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (j == 0) D.part2[(size_t)chunk * M + 32 * w + rho(r, hh)] = v;
+      }
+    }
+  } else if (fold) {   // fixed-order sum over the 32 rows a half-wave holds
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       float v = wacc[q];
@@ -1532,6 +1666,33 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
       for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
       if ((tid & 31) == 0 && 8 * q + (tid >> 5) < M) D.part2[(size_t)chunk * M + 8 * q + (tid >> 5)] = v;
     }
+  }
+}
+
+__global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBatch ob) {
+  const int bid = blockIdx.x;
+  const int k = find_desc(ob, bid);
+  const OuterDesc& D = ob.d[k];
+  const int local = bid - ob.start[k];
+  const int chunk = local / D.nb, nbi = local - chunk * D.nb;
+  const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
+  const int r0 = chunk * D.chunk;
+  if (r0 >= rows) return;
+  const int r1 = min(rows, r0 + D.chunk);
+  __shared__ float sd[2][128][OX_LD];
+  __shared__ float sx[2][128][OX_LD];
+  // recomputed operands need the layer's hidden width at compile time
+  // (one register allocation per branch: the modes' staged operands differ)
+  if (D.recomp == RECOMP_X0) {
+    if (D.N == 128) outer_x3_body<128, RECOMP_X0>(D, chunk, nbi, r0, r1, sd, sx);
+    else if (D.N == 64) outer_x3_body<64, RECOMP_X0>(D, chunk, nbi, r0, r1, sd, sx);
+    else outer_x3_body<32, RECOMP_X0>(D, chunk, nbi, r0, r1, sd, sx);
+  } else if (D.recomp == RECOMP_PC) {
+    if (D.N == 128) outer_x3_body<128, RECOMP_PC>(D, chunk, nbi, r0, r1, sd, sx);
+    else if (D.N == 64) outer_x3_body<64, RECOMP_PC>(D, chunk, nbi, r0, r1, sd, sx);
+    else outer_x3_body<32, RECOMP_PC>(D, chunk, nbi, r0, r1, sd, sx);
+  } else {
+    outer_x3_body<128, RECOMP_NONE>(D, chunk, nbi, r0, r1, sd, sx);
   }
 }
 
@@ -1858,6 +2019,10 @@ struct BwdWs {
   size_t part_floats;
 };
 
+// ENFLOW_STORE_PC=1 (diagnostic, A/B): the layer backward stores pre(coord_nn.0)
+// rows and coord_nn.0's weight-gradient pass reads them instead of recomputing
+static bool store_pc_env() { return getenv("ENFLOW_STORE_PC") != nullptr; }
+static bool store_p0_env() { return getenv("ENFLOW_STORE_P0") != nullptr; }
 static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, long long prb) {
   BwdWs W;
   size_t o = 0;
@@ -1865,9 +2030,10 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.offs = 0;
   W.buf0 = al64((size_t)n_layers * (num_mols + 1));
   W.xin = o; o += al64(P * xin_width(nf));
-  W.p0 = o; o += al64(P * H);
+  W.p0 = W.pc = 0;   // not stored (recomputed, see BwdArgs)
   W.pe = o; o += al64(P * H);
-  W.pc = o; o += al64(P * H);
+  if (store_pc_env()) { W.pc = o; o += al64(P * H); }
+  if (store_p0_env()) { W.p0 = o; o += al64(P * H); }
   W.dp0 = o; o += al64(P * H);
   W.dpe = o; o += al64(P * H);
   W.aphi = o; o += al64(P);
@@ -1937,6 +2103,9 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.rowv = nullptr;
   D.colv = nullptr;
   D.part2 = nullptr;
+  D.recomp = RECOMP_NONE;
+  D.Lp = nullptr;
+  D.nf = 0;
   D.chunk = tiled ? OA_CHUNK : OA_CHUNK_ATOM;
   D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
   D.rows_dev = rows_dev; D.rows_static = rows_static;
@@ -2017,27 +2186,40 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
 // rows) and atom rows, straight into the torch parameter layout G.
 static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const int32_t* prow, int prb,
                               bool variants, float* G, const float* Rp, const RawEgcl& R, const float* hx,
-                              int num_atoms, int nf, int H) {
+                              int num_atoms, int nf, int H, const float* Lp) {
     OuterBatch ob;
     ob.nd = 0;
     int wg = 0;
     float* part = wb + Wl.part;
-    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, xin_width(nf), 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1,
+    const int XW = xin_width(nf);
+    add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, XW, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1,
              PAIR_OUTER);
-    add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
-    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre0)
-    add_desc(ob, wg, wb + Wl.pc, H, H, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.Wc1, G + R.bc1, PAIR_OUTER);
-    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pre_e) = the message
-    ob.d[ob.nd - 1].xf_dy = 1;                                  // DY = aphi * wc2 * silu'(pc)
+    // edge_nn.2: X = silu(pre0), pre0 recomputed from the xin rows
+    if (store_p0_env()) {
+      add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
+      ob.d[ob.nd - 1].xf_x = 1;
+    } else {
+      add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.xin, XW, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
+      ob.d[ob.nd - 1].recomp = RECOMP_X0;
+    }
+    ob.d[ob.nd - 1].Lp = Lp;
+    ob.d[ob.nd - 1].nf = nf;
+    // coord_nn.0: X = silu(pre_e) = the message; DY = aphi * wc2 * silu'(pc), pc recomputed from X
+    const bool spc = store_pc_env();
+    add_desc(ob, wg, spc ? wb + Wl.pc : nullptr, H, H, wb + Wl.pe, H, H, prow, 0, prb, part,
+             G + R.Wc1, G + R.bc1, PAIR_OUTER);
+    ob.d[ob.nd - 1].xf_x = 1;
+    ob.d[ob.nd - 1].xf_dy = 1;
     ob.d[ob.nd - 1].rowv = wb + Wl.aphi;
     if (variants) ob.d[ob.nd - 1].xrow = wb + Wl.patt;          // the message is e * att
     ob.d[ob.nd - 1].colv = Rp + R.wc2;
-    // coord_nn.2: d wc2 = sum_rows aphi silu(pc); aphi is one value per row (its "tile-blocked"
-    // layout is row-major with width 1)
-    add_desc(ob, wg, wb + Wl.aphi, 1, 1, wb + Wl.pc, H, H, prow, 0, prb, part, G + R.wc2, nullptr,
-             ENFLOW_OUTER_X3 ? 3 : 1);
-    ob.d[ob.nd - 1].xf_x = 1;                                   // X = silu(pc)
-    if (ENFLOW_OUTER_X3) ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;   // folded into coord_nn.0's pass
+    ob.d[ob.nd - 1].recomp = spc ? RECOMP_NONE : RECOMP_PC;
+    ob.d[ob.nd - 1].Lp = Lp;
+    ob.d[ob.nd - 1].nf = nf;
+    // coord_nn.2: d wc2 = sum_rows aphi silu(pc), folded into coord_nn.0's pass (its partials
+    // written there; this descriptor only sizes them and feeds the reduction)
+    add_desc(ob, wg, wb + Wl.aphi, 1, 1, nullptr, H, H, prow, 0, prb, part, G + R.wc2, nullptr, 3);
+    ob.d[ob.nd - 2].part2 = ob.d[ob.nd - 1].part;
     if (variants) {   // att_nn.0: d w = sum_rows dlogit e, d b = sum_rows dlogit (0 rows without attention)
       add_desc(ob, wg, wb + Wl.dlogit, 1, 1, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
       ob.d[ob.nd - 1].xf_x = 1;                                 // X = silu(pre_e) = e
@@ -2196,7 +2378,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
     A.pair_off = offs + (size_t)l * (num_mols + 1);
-    A.xin = wb + Wl.xin; A.p0 = wb + Wl.p0; A.pe = wb + Wl.pe; A.pc = wb + Wl.pc;
+    A.xin = wb + Wl.xin; A.p0 = store_p0_env() ? wb + Wl.p0 : nullptr; A.pe = wb + Wl.pe; A.pc = store_pc_env() ? wb + Wl.pc : nullptr;
     A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
     A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
@@ -2218,7 +2400,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
                                       grad_layers + (size_t)l * R.total_bwd, A.Rp, R,
                                       tape + tape_layout(num_atoms, nf, H, n_layers).hx +
                                           (size_t)l * num_atoms * (nf + H),
-                                      num_atoms, nf, H);
+                                      num_atoms, nf, H, A.Lp);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
     if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;
@@ -2357,7 +2539,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
     A.Rp = layers_raw + (size_t)l * R.total_bwd;
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
-    A.xin = wb + Wl.xin; A.p0 = wb + Wl.p0; A.pe = wb + Wl.pe; A.pc = wb + Wl.pc;
+    A.xin = wb + Wl.xin; A.p0 = store_p0_env() ? wb + Wl.p0 : nullptr; A.pe = wb + Wl.pe; A.pc = store_pc_env() ? wb + Wl.pc : nullptr;
     A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
     A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
@@ -2384,7 +2566,8 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
     if (hipEventRecord(ev(2 * l), st) != hipSuccess || hipStreamWaitEvent(st2, ev(2 * l), 0) != hipSuccess)
       return -2;
     const int rc = layer_weight_grads(st2, Wl, wb, tot_l, prb, variants, grad_layers + (size_t)l * R.total_bwd,
-                                      A.Rp, R, tape + T.hx + (size_t)l * num_atoms * (nf + H), num_atoms, nf, H);
+                                      A.Rp, R, tape + T.hx + (size_t)l * num_atoms * (nf + H), num_atoms, nf, H,
+                                      A.Lp);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
     if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;

@@ -3,6 +3,7 @@
 step time and the backward kernels' share (events around loss.backward()).
 
     python tools/ab_train.py path/to/libA.so path/to/libB.so ...
+    python tools/ab_train.py lib.so lib.so@ENFLOW_STORE_PC=1     # same build, a runtime knob set
 """
 import os
 import statistics
@@ -33,9 +34,21 @@ def main():
     noise = torch.randn_like(base.h)
     grads = {}
 
-    def run(path, reps):
-        _lib._lib = None
-        _lib.LIB_PATH = path
+    def run(spec, reps):
+        path, _, env = spec.partition("@")
+        for kv in [e for e in env.split(",") if e]:
+            k, _, v = kv.partition("=")
+            os.environ[k] = v
+        try:
+            return _run(spec, path, reps)
+        finally:
+            for kv in [e for e in env.split(",") if e]:
+                os.environ.pop(kv.partition("=")[0], None)
+
+    def _run(spec, path, reps):
+        if _lib.LIB_PATH != path or _lib._lib is None:
+            _lib._lib = None
+            _lib.LIB_PATH = path
         for mod in model.modules():
             for attr in ("_packed_key", "_layers_key", "_train_key"):
                 if hasattr(mod, attr):
@@ -52,7 +65,7 @@ def main():
             e2.record()
             torch.cuda.synchronize()
             ts.append((e0.elapsed_time(e1), e1.elapsed_time(e2)))
-        grads[path] = [p.grad.clone() for p in model.parameters()]
+        grads[spec] = [p.grad.clone() for p in model.parameters()]
         return ts
 
     res = {p: [] for p in libs}
@@ -66,7 +79,7 @@ def main():
         fw = statistics.median(t[0] for t in res[p])
         bw = statistics.median(t[1] for t in res[p])
         rel = max(float((a - b).norm() / (b.norm() + 1e-30)) for a, b in zip(grads[p], g0))
-        print(f"{os.path.basename(p):28s} fwd+nll {fw:7.3f} ms  backward {bw:7.3f} ms  "
+        print(f"{os.path.basename(p):40s} fwd+nll {fw:7.3f} ms  backward {bw:7.3f} ms  "
               f"max grad rel diff vs first {rel:.2e}", flush=True)
 
 
