@@ -1651,8 +1651,6 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
   node_partials_reduce(sm, Lp, L, nf, tid, r0, rb);
 }
 
-// ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
-// returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
 // The dequantiser's draws made in the kernel (noise == NULL): Philox4x32-10
 // (Salmon et al., SC'11) keyed by the caller's 64-bit seed, counter = (element
 // index, 0, 64-bit offset); N(0,1) by Box-Muller (argmax.py:16's torch.randn),
@@ -1687,6 +1685,8 @@ struct NoiseSrc {
   }
 };
 
+// ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
+// returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
 template <int H, int NMAX, int RB>
 __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const NoiseSrc noise,
                                 int a0, int n, int nf) {
