@@ -1364,6 +1364,9 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 // orientation (lane = row, registers = features) from the packed forward
 // fragments, and writes it to the LDS stage.
 #define OX_LD 36   // LDS column stride (floats): 16-byte aligned operand reads
+#ifndef ENFLOW_OX_VEC
+#define ENFLOW_OX_VEC 1   // 16-B row staging (A/B knob: 0 = one dword per row)
+#endif
 #ifndef ENFLOW_OUTER_WPS
 #define ENFLOW_OUTER_WPS 2   // outer_x3_kernel occupancy hint (A/B knob)
 #endif
@@ -1407,7 +1410,11 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
   // staged rows in registers, one stage ahead
-  struct Stage { float rd[16], rx[16], ra, xa; bool pv; };
+  // ENFLOW_OX_VEC: a thread stages 4 consecutive rows of a column per 16-B load /
+  // ds_write_b128 (float4 e4 = q * 256 + tid: column e4 / 8, rows 4 (e4 % 8) ..),
+  // 4x fewer memory instructions than one dword per row; ra4 / xa4 the 4 rows'
+  // factors, raj row j's (the recompute's lane row)
+  struct Stage { float rd[16], rx[16], ra, xa; bool pv; f32x4 ra4, xa4; float raj; };
   Stage S0;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
   // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
@@ -1420,9 +1427,45 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
     G.pv = pv;
     G.ra = 0.f;
     G.xa = 1.f;
+#if ENFLOW_OX_VEC
+    if (rcm == RECOMP_PC) G.raj = pv ? D.rowv[rb + j] : 0.f;
+    if constexpr (rcm != RECOMP_X0) {
+      // stage rows are whole 32-row tiles (pair rows are 32-aligned), so a float4
+      // of rows is valid or not as a whole
+      const int r4 = (tid & 7) * 4;
+      const bool pv4 = rb + r4 + 3 < r1;
+      G.ra4 = (f32x4)0.f;
+      G.xa4 = (f32x4)1.f;
+      if (xf_dy) G.ra4 = pv4 ? ld4(D.rowv + rb + r4) : (f32x4)0.f;
+      if (D.xrow) G.xa4 = pv4 ? ld4(D.xrow + rb + r4) : (f32x4)0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e4 = q * 256 + tid, c = e4 >> 3;
+        f32x4 d = (f32x4)0.f, x = (f32x4)0.f;
+        if (rcm != RECOMP_PC && pv4 && c < M) d = ld4(dblk + 4 * e4);
+        if (pv4 && n0 + c < N) x = ld4(xblk + 4 * e4);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          G.rd[4 * q + u] = d[u];
+          G.rx[4 * q + u] = x[u];
+        }
+      }
+      return;
+    } else {   // RECOMP_X0: DY as float4 rows here, the X operand (xin) below
+      const int r4 = (tid & 7) * 4;
+      const bool pv4 = rb + r4 + 3 < r1;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e4 = q * 256 + tid, c = e4 >> 3;
+        const f32x4 d = (pv4 && c < M) ? ld4(dblk + 4 * e4) : (f32x4)0.f;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) G.rd[4 * q + u] = d[u];
+      }
+    }
+#endif
     if (xf_dy) G.ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
     if (D.xrow) G.xa = pv ? D.xrow[rb + (tid & 31)] : 0.f;
-    if constexpr (rcm != RECOMP_PC) {
+    if constexpr (rcm != RECOMP_PC && !ENFLOW_OX_VEC) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int c = 8 * q + (tid >> 5);
@@ -1449,7 +1492,46 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
     }
   };
   auto lstore = [&](int buf, Stage& G) {
-    if constexpr (rcm != RECOMP_PC) {
+#if ENFLOW_OX_VEC
+    if constexpr (rcm != RECOMP_X0) {
+      const int r4 = (tid & 7) * 4;
+      if constexpr (rcm != RECOMP_PC) {
+        if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float z = G.rd[4 * q + u], sg = sigmoid_f(z);
+              if (fold) wacc[q] = fmaf(G.ra4[u], z * sg, wacc[q]);
+              G.rd[4 * q + u] = G.ra4[u] * (sg * (1.f + z * (1.f - sg)));
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          st4(&sd[buf][(q * 256 + tid) >> 3][r4],
+              (f32x4){G.rd[4 * q], G.rd[4 * q + 1], G.rd[4 * q + 2], G.rd[4 * q + 3]});
+      }
+      if (xf_x) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) G.rx[q] = silu_f(G.rx[q]);
+      }
+      if (D.xrow) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) G.rx[q] *= G.xa4[q & 3];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(&sx[buf][(q * 256 + tid) >> 3][r4], (f32x4){G.rx[4 * q], G.rx[4 * q + 1], G.rx[4 * q + 2], G.rx[4 * q + 3]});
+      return;
+    } else {   // RECOMP_X0: DY rows as float4 (no transform on edge_nn.2's DY)
+      const int r4 = (tid & 7) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(&sd[buf][(q * 256 + tid) >> 3][r4],
+            (f32x4){G.rd[4 * q], G.rd[4 * q + 1], G.rd[4 * q + 2], G.rd[4 * q + 3]});
+    }
+#endif
+    if constexpr (rcm != RECOMP_PC && !(ENFLOW_OX_VEC && rcm == RECOMP_X0)) {
       if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
@@ -1541,7 +1623,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         }
       }
       const float inv2 = D.Lp[L.scl + 3];
-      const float ra = G.ra;   // row j's aphi (gload's row is tid % 32 = j)
+      const float ra = ENFLOW_OX_VEC ? G.raj : G.ra;   // row j's aphi
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int f0 = 32 * w + 8 * g4 + 4 * hh;
@@ -1586,19 +1668,21 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
       const int ea = pow2_exp(ma), eb = pow2_exp(mb);
       const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb), un = ldexpf(1.f, -(ea + eb));
       f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
+      // scaled hi / lo split: hi = f16(x s) by v_cvt_pk_f16_f32, lo = f16(x s - hi) by
+      // v_fma_mix (split_f16; x s - hi is exact in fp32, so bitwise the plain form)
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks) {
+          f32x16 xa, xb;
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) {
-            const float xa = av[a][ks][jj >> 2][jj & 3] * sa, xb = bv[a][ks][jj >> 2][jj & 3] * sbs;
-            const _Float16 ha = (_Float16)xa, hb = (_Float16)xb;
-            ah[a][ks][jj] = ha;
-            al[a][ks][jj] = (_Float16)(xa - (float)ha);
-            bh[a][ks][jj] = hb;
-            bl[a][ks][jj] = (_Float16)(xb - (float)hb);
+            xa[jj] = av[a][ks][jj >> 2][jj & 3] * sa;
+            xb[jj] = bv[a][ks][jj >> 2][jj & 3] * sbs;
           }
+          split_f16(xa, 0, ah[a][ks], al[a][ks]);
+          split_f16(xb, 0, bh[a][ks], bl[a][ks]);
+        }
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1657,6 +1741,15 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
         if (j == 0) D.part2[(size_t)chunk * M + 32 * w + rho(r, hh)] = v;
       }
+    }
+  } else if (fold && ENFLOW_OX_VEC) {   // fixed-order sum over the 8 row groups of each column
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float v = wacc[q];
+#pragma unroll
+      for (int off = 1; off < 8; off <<= 1) v += __shfl_xor(v, off, 64);
+      const int c = (q * 256 + tid) >> 3;
+      if ((tid & 7) == 0 && c < M) D.part2[(size_t)chunk * M + c] = v;
     }
   } else if (fold) {   // fixed-order sum over the 32 rows a half-wave holds
 #pragma unroll
