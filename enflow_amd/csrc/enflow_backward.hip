@@ -1789,6 +1789,11 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
   }
 }
 
+// Four fp64 sums per output (chunk mod 4, the leftover chunks into the first),
+// one per thread of a 4-lane group, combined in the fixed order (s0 + s1) +
+// (s2 + s3): 64 outputs per workgroup, so the partials stream through 4x as
+// many workgroups with a quarter of the serial loads each
+#define RP_OUT 64
 __global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
@@ -1796,25 +1801,24 @@ __global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
   const int rows = D.rows_dev ? D.rows_dev[0] : D.rows_static;
   const int nch = (rows + D.chunk - 1) / D.chunk;
   const int NB = D.N + (D.outB ? 1 : 0);
-  const int idx = (bid - ob.start[k]) * 256 + threadIdx.x;
-  if (idx >= D.M * NB) return;
-  // four interleaved fp64 sums (chunk mod 4), combined in a fixed order: the
-  // loads stream, the result does not depend on timing
+  const int sub = threadIdx.x & 3;
+  const int idx = (bid - ob.start[k]) * RP_OUT + (threadIdx.x >> 2);
+  const bool live = idx < D.M * NB;   // (the whole 4-lane group agrees)
   const size_t cs = (size_t)D.M * NB;
-  const float* src = D.part + idx;
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  int ch = 0;
-  for (; ch + 3 < nch; ch += 4) {
-    s0 += (double)src[(size_t)ch * cs];
-    s1 += (double)src[(size_t)(ch + 1) * cs];
-    s2 += (double)src[(size_t)(ch + 2) * cs];
-    s3 += (double)src[(size_t)(ch + 3) * cs];
+  const float* src = D.part + (live ? idx : 0);
+  double s = 0.0;
+  const int G = nch >> 2;
+  if (live) {
+    for (int g = 0; g < G; ++g) s += (double)src[(size_t)(4 * g + sub) * cs];
+    if (sub == 0)
+      for (int ch = 4 * G; ch < nch; ++ch) s += (double)src[(size_t)ch * cs];
   }
-  for (; ch < nch; ++ch) s0 += (double)src[(size_t)ch * cs];
-  const double s = (s0 + s1) + (s2 + s3);
+  const double pair = s + __shfl_xor(s, 1, 64);      // lane 0: s0 + s1, lane 2: s2 + s3
+  const double tot = pair + __shfl_xor(pair, 2, 64);  // lane 0: (s0 + s1) + (s2 + s3)
+  if (!live || sub != 0) return;
   const int mm = idx / NB, nn = idx - mm * NB;
-  if (nn < D.N) D.outW[(size_t)mm * D.N + nn] = (float)s;
-  else D.outB[mm] = (float)s;
+  if (nn < D.N) D.outW[(size_t)mm * D.N + nn] = (float)tot;
+  else D.outB[mm] = (float)tot;
 }
 
 // ---------------------------------------------------------------------------
@@ -2255,7 +2259,7 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
   for (int k = 0; k < ob.nd; ++k) {
     rb.start[k] = rw;
     const int NB = ob.d[k].N + (ob.d[k].outB ? 1 : 0);
-    rw += cdiv((long long)ob.d[k].M * NB, 256);
+    rw += cdiv((long long)ob.d[k].M * NB, RP_OUT);
   }
   rb.start[ob.nd] = rw;
   if (rw > 0) ENFLOW_TIMED("reduce_part_kernel", st, hipLaunchKernelGGL(reduce_part_kernel, dim3(rw), dim3(256), 0, st, rb));
