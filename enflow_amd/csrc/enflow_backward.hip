@@ -675,10 +675,6 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     // row, per element a wave-uniform byte offset (tile, feature) + the lane's
     const size_t nrow = (size_t)TT_all * 32;
     const rsrc_t rpe = rows_rsrc(B.pe + prow0 * H, nrow * H);
-    const bool store_pc = B.pc != nullptr;   // A/B diagnostic (ENFLOW_STORE_PC): the pass reads pc rows
-    const bool store_p0 = B.p0 != nullptr;   // A/B diagnostic (ENFLOW_STORE_P0): the pass reads p0 rows
-    const rsrc_t rp0 = rows_rsrc((store_p0 ? B.p0 : B.pe) + prow0 * H, nrow * H);
-    const rsrc_t rpc = rows_rsrc((store_pc ? B.pc : B.pe) + prow0 * H, nrow * H);
     const rsrc_t rdp0 = rows_rsrc(B.dp0 + prow0 * H, nrow * H), rdpe = rows_rsrc(B.dpe + prow0 * H, nrow * H);
     // edge_nn.0 input rows [h_i, h_j, radial]: 16 wide, 32 when 2 nf + 1 > 16 (nf = 8)
     const int XW = xin_width(nf);
@@ -771,6 +767,15 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
       if constexpr (PREC == PREC_F16X3) {
         const int ks_n = gemm0_ksteps(nf);
+        // the first k-step's fragments requested before the operand build, so
+        // their L2 round trip overlaps it (they are the only loads the chain waits on)
+        f32x4 fh0[NT], fl0[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int so = (L.we1x + (t * 2) * 512) * 4;
+          fh0[t] = bload4(W, lane * 32, so);
+          fl0[t] = bload4(W, lane * 32 + 16, so);
+        }
         for (int ks = 0; ks < ks_n; ++ks) {   // k order gemm0_col (as the forward)
           f32x16 in;
           if (ks == 0) {
@@ -792,8 +797,12 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           split_f16(in, 0, bh, bl);
 #pragma unroll
           for (int t = 0; t < NT; ++t) {
-            const int so = (L.we1x + (t * 2 + ks) * 512) * 4;
-            const f32x4 ah = bload4(W, lane * 32, so), al = bload4(W, lane * 32 + 16, so);
+            f32x4 ah = fh0[t], al = fl0[t];
+            if (ks) {
+              const int so = (L.we1x + (t * 2 + 1) * 512) * 4;
+              ah = bload4(W, lane * 32, so);
+              al = bload4(W, lane * 32 + 16, so);
+            }
             x0[t] = mfma_f16(ah, bh, x0[t]);
             x0[t] = mfma_f16(ah, bl, x0[t]);
             x0[t] = mfma_f16(al, bh, x0[t]);
@@ -826,11 +835,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
           const f32x4 b = ld4(sm.bias + f0);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const float z = x0[t][4 * g4 + u] + b[u];
-            if (store_p0) ST_PARK(rp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
-            x0[t][4 * g4 + u] = silu_f(z);
-          }
+          for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = silu_f(x0[t][4 * g4 + u] + b[u]);
         }
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(5);
@@ -887,8 +892,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(cv[t][4 * g4 + u], inv2, b[u]);
             const float s = sigmoid_f(z);
-            part = fmaf(w2[u], z * s, part);   // pc: recomputed by outer_x3_kernel (unless ENFLOW_STORE_PC)
-            if (store_pc) ST_OUT(rpc, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
+            part = fmaf(w2[u], z * s, part);   // pc is not stored: outer_x3_kernel recomputes it
             cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
           }
         }
@@ -2116,10 +2120,6 @@ struct BwdWs {
   size_t part_floats;
 };
 
-// ENFLOW_STORE_PC=1 (diagnostic, A/B): the layer backward stores pre(coord_nn.0)
-// rows and coord_nn.0's weight-gradient pass reads them instead of recomputing
-static bool store_pc_env() { return getenv("ENFLOW_STORE_PC") != nullptr; }
-static bool store_p0_env() { return getenv("ENFLOW_STORE_P0") != nullptr; }
 static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, long long prb) {
   BwdWs W;
   size_t o = 0;
@@ -2129,8 +2129,6 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.xin = o; o += al64(P * xin_width(nf));
   W.p0 = W.pc = 0;   // not stored (recomputed, see BwdArgs)
   W.pe = o; o += al64(P * H);
-  if (store_pc_env()) { W.pc = o; o += al64(P * H); }
-  if (store_p0_env()) { W.p0 = o; o += al64(P * H); }
   W.dp0 = o; o += al64(P * H);
   W.dpe = o; o += al64(P * H);
   W.aphi = o; o += al64(P);
@@ -2292,25 +2290,19 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, XW, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1,
              PAIR_OUTER);
     // edge_nn.2: X = silu(pre0), pre0 recomputed from the xin rows
-    if (store_p0_env()) {
-      add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.p0, H, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
-      ob.d[ob.nd - 1].xf_x = 1;
-    } else {
-      add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.xin, XW, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
-      ob.d[ob.nd - 1].recomp = RECOMP_X0;
-    }
+    add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.xin, XW, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
+    ob.d[ob.nd - 1].recomp = RECOMP_X0;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
     // coord_nn.0: X = silu(pre_e) = the message; DY = aphi * wc2 * silu'(pc), pc recomputed from X
-    const bool spc = store_pc_env();
-    add_desc(ob, wg, spc ? wb + Wl.pc : nullptr, H, H, wb + Wl.pe, H, H, prow, 0, prb, part,
+    add_desc(ob, wg, nullptr, H, H, wb + Wl.pe, H, H, prow, 0, prb, part,
              G + R.Wc1, G + R.bc1, PAIR_OUTER);
     ob.d[ob.nd - 1].xf_x = 1;
     ob.d[ob.nd - 1].xf_dy = 1;
     ob.d[ob.nd - 1].rowv = wb + Wl.aphi;
     if (variants) ob.d[ob.nd - 1].xrow = wb + Wl.patt;          // the message is e * att
     ob.d[ob.nd - 1].colv = Rp + R.wc2;
-    ob.d[ob.nd - 1].recomp = spc ? RECOMP_NONE : RECOMP_PC;
+    ob.d[ob.nd - 1].recomp = RECOMP_PC;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
     // coord_nn.2: d wc2 = sum_rows aphi silu(pc), folded into coord_nn.0's pass (its partials
@@ -2475,7 +2467,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
     A.pair_off = offs + (size_t)l * (num_mols + 1);
-    A.xin = wb + Wl.xin; A.p0 = store_p0_env() ? wb + Wl.p0 : nullptr; A.pe = wb + Wl.pe; A.pc = store_pc_env() ? wb + Wl.pc : nullptr;
+    A.xin = wb + Wl.xin; A.p0 = nullptr; A.pe = wb + Wl.pe; A.pc = nullptr;
     A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
     A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
@@ -2636,7 +2628,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
     A.Rp = layers_raw + (size_t)l * R.total_bwd;
     A.dt = dt; A.cw = cw; A.adj_ldj = adj_ldj;
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
-    A.xin = wb + Wl.xin; A.p0 = store_p0_env() ? wb + Wl.p0 : nullptr; A.pe = wb + Wl.pe; A.pc = store_pc_env() ? wb + Wl.pc : nullptr;
+    A.xin = wb + Wl.xin; A.p0 = nullptr; A.pe = wb + Wl.pe; A.pc = nullptr;
     A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
     A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
