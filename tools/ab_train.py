@@ -3,7 +3,7 @@
 step time and the backward kernels' share (events around loss.backward()).
 
     python tools/ab_train.py path/to/libA.so path/to/libB.so ...
-    python tools/ab_train.py lib.so lib.so@ENFLOW_STORE_PC=1     # same build, a runtime knob set
+    python tools/ab_train.py lib.so lib.so@ENFLOW_SERIAL_BWD=1   # same build, a runtime knob set
 """
 import os
 import statistics
