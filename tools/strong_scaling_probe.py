@@ -1,0 +1,42 @@
+"""Per-rank time of the forward under strong scaling, measured on one GPU:
+the 1024-molecule batch of BASELINE configs[1] split N ways is, on each rank,
+a 1024/N-molecule forward with no data-path collective, so its step time IS
+the N-rank strong-scaling time (max over ranks = the slowest shard).
+
+    python tools/strong_scaling_probe.py > profiles/r02/strong_scaling_probe.json
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import bench
+    from enflow_amd.data.synthetic import make_molecules
+    dev = torch.device("cuda", 0)
+    model = bench.build_model(dev, bench.LAYERS)
+    model.gemm_precision = "f16x3"
+    g = make_molecules(1024, bench.ATOMS, nf=bench.NF, seed=1000)
+    out = {"workload": bench.workload_name("forward"), "rows": []}
+    t1 = None
+    for n in (1, 2, 4, 8):
+        m1 = 1024 // n
+        run = bench.FlowRunner(model, bench.batch_tensors(bench.sub_batch(g, 0, m1), dev), bench.ATOMS, False, dev,
+                               torch.Generator(dev).manual_seed(0))
+        el = bench.timed(run.step, 40, 30, None, dev)
+        run.check()
+        ms = el / 40 * 1e3
+        t1 = ms if n == 1 else t1
+        out["rows"].append({"ranks": n, "molecules_per_rank": m1, "workgroups": m1, "ms_per_step": ms,
+                            "global_molecule_transforms_per_s": 1024 / (ms * 1e-3),
+                            "strong_scaling_efficiency": t1 / (n * ms)})
+        print(json.dumps(out["rows"][-1]), file=sys.stderr, flush=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
