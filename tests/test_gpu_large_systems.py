@@ -167,6 +167,26 @@ def test_generate_example_box_2944():
         assert bad.mean() < 0.01, (k, int(bad.sum()))
 
 
+def test_generate_example_box_2944_grad_enabled():
+    """The reference's Main.generate calls self.model(out) outside no_grad
+    (main.py:275): with autograd on, the 2944-atom box goes through the taped
+    training forward and returns the inference kernels' state (fp32 round-off)."""
+    from enflow_amd.data import Data
+    b = _boxes([2944], 21, nf=5)
+    b["pos"] = O.apply_pbc(b["pos"], b["box"]).astype(np.float32).astype(np.float64)
+    b["h"] = np.eye(5)[np.random.default_rng(0).integers(0, 5, 2944)]
+    model = _model(128, 5, 8, 22)
+    noise = torch.randn((2944, 5), device=DEV, generator=torch.Generator(DEV).manual_seed(23))
+    with torch.no_grad():
+        ref, lref = model(Data.from_arrays(b, device=DEV), noise=noise)
+    o, ldj = model(Data.from_arrays(b, device=DEV), noise=noise)
+    assert ldj.requires_grad
+    for k in ("h", "g", "pos", "vel"):
+        got, want = getattr(o, k).detach().cpu().numpy(), getattr(ref, k).cpu().numpy()
+        assert np.linalg.norm(got - want) <= 1e-5 * np.linalg.norm(want), k
+    assert abs(float(ldj.detach()) - float(lref)) <= 1e-5 * abs(float(lref))
+
+
 def _large_train_step(model, b, eps, kBT=1.0, softening=0.1):
     from enflow_amd.data import Data
     from enflow_amd.flow import Alchemical_NLL
