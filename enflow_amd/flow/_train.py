@@ -75,8 +75,6 @@ class _FlowFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gh, gg, gpos, gvel, gldj):
         flow, meta, kind = ctx.flow, ctx.meta, ctx.kind
-        if meta["check_errors"]:
-            _lib.check_pending()          # the forward's deferred word (the reference's IndexError)
         h_in, tape, counts = ctx.saved_tensors
         hid, nf, cw = flow._geometry()
         dev = h_in.device
@@ -130,8 +128,12 @@ class _FlowFunction(torch.autograd.Function):
                 _lib.ptr(grad_layers), _lib.ptr(grad_dq), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
                 _lib.stream_ptr(dev)), "enflow_lf_backward_f32")
         if meta["check_errors"]:
-            # the forward already validated this batch's geometry; the backward's
-            # word is read at the next check instead of stalling the host here
+            # the forward's deferred word (the reference's IndexError), read once the
+            # backward is queued behind it, so the device never drains while the host
+            # prepares the backward; raised before any gradient is returned (the
+            # backward kernels validate their own geometry and only compute on a
+            # failed batch's state).  The backward's own word is read at the next check.
+            _lib.check_pending()
             _lib.defer_err(err)
         # split the flat gradients into the parameters' shapes (inputs order)
         grads = []
