@@ -2108,15 +2108,22 @@ static inline int hid_ok_b(int H) { return H == 32 || H == 64 || H == 128; }
 static inline size_t al64(size_t x) { return (x + 63) & ~(size_t)63; }
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-// Workspace: the per-layer pair-row / atom-row / partial sections are double
-// buffered (BWD_NBUF copies, `span` floats apart): layer l's weight-gradient pass
-// (outer kernels, on an auxiliary stream) reads buffer l & 1 while layer l-1's
-// backward writes the other one.
-#define BWD_NBUF 2
+// Workspace: the per-layer pair-row / atom-row / partial sections come in
+// BWD_NBUF copies (`span` floats apart): layer l's weight-gradient pass (outer
+// kernels, on an auxiliary stream) reads buffer l % BWD_NBUF while the layer
+// backwards of l-1, l-2 write the others.  Three buffers let the layer chain
+// run two layers ahead of the weight-gradient passes instead of waiting on
+// each one (backward -2.7 %, profiles/r02/r02y_ab_nbuf.txt; +6.6 GB at the
+// bench batch); the large-system path and single layers use two.
+#ifndef BWD_NBUF
+#define BWD_NBUF 3
+#endif
+static_assert(BWD_NBUF >= 2, "at least double buffered");
 struct BwdWs {
   size_t offs, buf0, span;   // shared offsets section; first buffer; buffer stride
   // offsets within a buffer (floats)
   size_t xin, p0, pe, pc, dp0, dpe, aphi, patt, dlogit, su, au, sn, an, aq, agr, anet, part, total;
+  int nbuf;                  // buffers rotated by the layer chain (BWD_NBUF or 2)
   size_t part_floats;
 };
 
@@ -2149,7 +2156,10 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   if (am > W.part_floats) W.part_floats = am;
   W.part = o; o += al64(W.part_floats);
   W.span = o;
-  W.total = W.buf0 + BWD_NBUF * W.span;
+  // fused layer chains of >= BWD_NBUF layers rotate BWD_NBUF buffers; the
+  // large-system path (n_layers 0 here) and single-layer callers use two
+  W.nbuf = n_layers >= BWD_NBUF ? BWD_NBUF : 2;
+  W.total = W.buf0 + (size_t)W.nbuf * W.span;
   return W;
 }
 
@@ -2455,9 +2465,10 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     hipLaunchKernelGGL(pair_offsets_kernel, dim3(n_layers), dim3(BLOCK), 0, st, pair_counts, num_mols, offs);
 
   for (int l = n_layers - 1; l >= 0; --l) {
-    float* const wb = ws + Wl.buf0 + (size_t)(l & 1) * Wl.span;   // this layer's buffer
-    // the buffer was last read by layer l + 2's weight-gradient pass
-    if (l + 2 < n_layers && hipStreamWaitEvent(st, ev(2 * (l + 2) + 1), 0) != hipSuccess) return -2;
+    float* const wb = ws + Wl.buf0 + (size_t)(l % Wl.nbuf) * Wl.span;   // this layer's buffer
+    // the buffer was last read by layer l + nbuf's weight-gradient pass
+    if (l + Wl.nbuf < n_layers && hipStreamWaitEvent(st, ev(2 * (l + Wl.nbuf) + 1), 0) != hipSuccess)
+      return -2;
     BwdArgs A{};
     A.mol_ptr = mol_ptr; A.r_cut = r_cut; A.box = box; A.tape = tape;
     A.num_atoms = num_atoms; A.num_mols = num_mols; A.n_layers = n_layers; A.layer = l; A.nf = nf;
