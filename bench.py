@@ -316,7 +316,10 @@ def cpu_baseline(per_core=192):
         avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         avail = os.cpu_count() or 1
-    cores = max(1, min(avail, BOX_CPU_SHARE))
+    # the GPU box's affinity set shows the whole machine (shared with other jobs);
+    # a one-GPU job is granted BOX_CPU_SHARE of them, exported as OMP_NUM_THREADS
+    grant = int(os.environ.get("OMP_NUM_THREADS") or BOX_CPU_SHARE)
+    cores = max(1, min(avail, grant))
     torch.manual_seed(0)
     nets = [EGCL(NF, NF, HID) for _ in range(LAYERS)]
     am = ArgMax(NF, HID)
@@ -342,11 +345,37 @@ def cpu_baseline(per_core=192):
     except (OSError, KeyError, ValueError):
         pass
     return {"value": total / wall, "unit": "molecule-transforms/s", "cores": cores, "kind": "port",
+            "cores_note": (f"{cores} single-thread worker processes = the host CPUs this job is granted "
+                           f"(OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')}); the affinity set "
+                           f"lists {avail} logical CPUs of the whole machine, shared with other jobs"),
+            "host_cpu": host_cpu_info(),
             "reference_torch": ref,
             "sample": f"{total} molecules x {ATOMS} atoms ({per_core} per core), {LAYERS} layers, hidden {HID}: "
                       f"numpy float64 oracle (oracle/enflow_oracle.py), one single-thread process per core, "
                       f"{wall:.1f} s wall (per-core {min(per):.1f}-{max(per):.1f} s); host CPUs visible "
                       f"{avail}, used {cores}"}
+
+
+def host_cpu_info():
+    """Model, logical CPUs and physical cores (distinct (package, core) pairs) of the host."""
+    info = {"logical": os.cpu_count()}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["model"] = line.split(":", 1)[1].strip()
+                    break
+        cores = set()
+        base = "/sys/devices/system/cpu"
+        for d in os.listdir(base):
+            if d.startswith("cpu") and d[3:].isdigit():
+                t = os.path.join(base, d, "topology")
+                with open(os.path.join(t, "physical_package_id")) as a, open(os.path.join(t, "core_id")) as b:
+                    cores.add((a.read().strip(), b.read().strip()))
+        info["physical_cores"] = len(cores)
+    except OSError:
+        pass
+    return info
 
 
 def run_cpu_baseline_child(per_core):

@@ -27,6 +27,8 @@ _u64 = ctypes.c_uint64
 # name -> (restype, argtypes); mirrors include/enflow_hip.h one to one
 SIGNATURES = {
     "enflow_abi_version": (_i, []),
+    "enflow_set_latency_threshold": (_i, [_i]),
+    "enflow_latency_threshold": (_i, []),
     "enflow_max_atoms": (_i, []),
     "enflow_max_node_nf": (_i, []),
     "enflow_supports_hidden": (_i, [_i]),
@@ -91,6 +93,12 @@ _lib = None
 
 class HipPathError(RuntimeError):
     pass
+
+
+class RangeError(FloatingPointError):
+    """ENFLOW_ERR_RANGE: a split-precision (f16x3 / bf16) GEMM operand left the
+    fp16 / bf16 range.  Inference calls catch it and re-run the same launch
+    with fp32 GEMMs; the training path raises it."""
 
 
 def lib():
@@ -223,11 +231,13 @@ def check_pending():
 
 def raise_on_err(err_flag, reset=False):
     """Read the device error word (synchronises) and raise like the reference;
-    reset: zero a non-zero word first (a cached status_word stays reusable)."""
-    check_pending()
+    reset: zero a non-zero word (a cached status_word stays reusable).  The
+    word is read and reset BEFORE any queued (deferred) error is raised, so a
+    stale bit never outlives this call; the first error found is raised."""
     e = int(err_flag.item())
     if e and reset:
         err_flag.zero_()
+    check_pending()      # an older queued error is raised first
     _raise_code(e)
 
 
@@ -256,5 +266,5 @@ def _raise_code(e):
     if e & ERR_TOO_MANY_FEATURES:
         raise HipPathError(f"node_nf larger than {lib().enflow_max_node_nf()}")
     if e & ERR_RANGE:
-        raise FloatingPointError("the split-precision (f16x3 / bf16) GEMMs produced a non-finite result: an "
+        raise RangeError("the split-precision (f16x3 / bf16) GEMMs produced a non-finite result: an "
                                  "operand is past the fp16 / bf16 range; run with gemm_precision='f32'")

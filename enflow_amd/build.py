@@ -5,16 +5,18 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-SRCS = [os.path.join(CSRC, f) for f in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip", "enflow_timing.hip")
+SRCS = [os.path.join(CSRC, f) for f in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip", "enflow_timing.hip",
+                                              "enflow_latency.hip")
         if os.path.exists(os.path.join(CSRC, f))]
+HDRS = [os.path.join(CSRC, h) for h in ("flow_device.h", "flow_kernel.h", "enflow_timing.h", "enflow_large.h",
+                                         "enflow_latency.h")] + [os.path.join(ROOT, "include", "enflow_hip.h")]
 OUT = os.path.join(HERE, "libenflow_hip.so")
 ARCH = os.environ.get("ENFLOW_OFFLOAD_ARCH", "gfx950")
 
 
 def build(force=False, verbose=False, out=OUT, defines=()):
     """defines: extra -D flags (A/B and ablation variants built to another `out`)."""
-    deps = SRCS + [os.path.join(CSRC, "flow_device.h"), os.path.join(CSRC, "enflow_timing.h"), os.path.join(CSRC, "enflow_large.h"),
-                   os.path.join(ROOT, "include", "enflow_hip.h")]
+    deps = SRCS + HDRS
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
         return out
     # one hipcc per source, in parallel, then one link
@@ -26,8 +28,7 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     stamp = out + ".flags"
     flags = " ".join(base)
     same_flags = os.path.exists(stamp) and open(stamp).read() == flags
-    hdrs = [os.path.join(CSRC, "flow_device.h"), os.path.join(CSRC, "enflow_timing.h"), os.path.join(CSRC, "enflow_large.h"),
-            os.path.join(ROOT, "include", "enflow_hip.h")]
+    hdrs = HDRS
     procs = []
     for src, obj in zip(SRCS, objs):
         if (not force and same_flags and os.path.exists(obj) and

@@ -26,6 +26,7 @@
 // All arithmetic is float32; MFMA f32 is an exact fmaf chain.
 
 #include "enflow_large.h"
+#include "enflow_latency.h"
 
 // ---------------------------------------------------------------------------
 // packing kernels
@@ -194,253 +195,7 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
   }
 }
 
-// ---------------------------------------------------------------------------
-// the fused flow kernel (forward or reverse)
-// ---------------------------------------------------------------------------
-#ifndef ENFLOW_BLOCKED_WPS
-#define ENFLOW_BLOCKED_WPS ENFLOW_WAVES_PER_SIMD   // row-blocked (> 64-atom) instances
-#endif
-// batch log|detJ| in the same launch: every workgroup publishes its ldj_mol
-// entry and takes a ticket; the last one sums ldj_mol in reduce_ldj_kernel's
-// fixed order (per-thread strided double sums, then a tree over the block) --
-// bitwise the separate reduction's result -- and resets the ticket for the
-// next launch on the stream.  `red` is BLOCK doubles of LDS scratch.
-__device__ __forceinline__ void ticket_reduce_ldj(const FlowArgs& A, double* red, int* last) {
-  const int tid = threadIdx.x;
-  __threadfence();                       // this block's ldj_mol entry visible device-wide
-  __syncthreads();
-  if (tid == 0) *last = atomicAdd(A.ticket, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (!*last) return;
-  __threadfence();                       // acquire: every block's entry
-  double s = 0.0;
-  for (int m = tid; m < A.num_mols; m += BLOCK) s += (double)__builtin_nontemporal_load(&A.ldj_mol[m]);
-  red[tid] = s;
-  __syncthreads();
-  for (int off = BLOCK / 2; off > 0; off >>= 1) {
-    if (tid < off) red[tid] += red[tid + off];
-    __syncthreads();
-  }
-  if (tid == 0) {
-    A.ldj_total[0] = (float)(red[0] + A.ldj_cst);
-    atomicExch(A.ticket, 0u);
-  }
-}
-
-template <int H, int NMAX, bool REV, int PREC, int RB, bool VAR>
-__global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLOW_WAVES_PER_SIMD))
-    lf_flow_kernel(FlowArgs A) {
-  __shared__ Smem<H, NMAX, RB> sm;
-  constexpr bool BLOCKED = RB < NMAX;
-  MolRef M;
-  STAMP_DECL
-#ifdef ENFLOW_SKEW
-  // A/B experiment: offset the second resident workgroup of a CU so the two
-  // molecules' serial phases (pair build, node phase) overlap the other's tiles
-  if (blockIdx.x & ENFLOW_SKEW_BIT)
-    {
-#pragma unroll
-      for (int i = 0; i < ENFLOW_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
-    }
-#endif
-  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) {   // error raised; keep the ticket count
-    if (!REV && A.ticket) {
-      if (threadIdx.x == 0) A.ldj_mol[blockIdx.x] = 0.f;
-      ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
-    }
-    return;
-  }
-  STAMP(0);
-  const int tid = threadIdx.x;
-  const int n = M.n, nf = A.nf;
-  const EgclLayout L = egcl_layout(H, nf);
-  constexpr int AST = Smem<H, NMAX, RB>::AST;
-  float ldj = 0.f;
-  // per-atom pbc box (Data.pbc, base.py): LDS image, or global memory when blocked
-  auto pbox = [&](int a, int d) {
-    if constexpr (BLOCKED) return A.box[((size_t)M.a0 + a) * 3 + d];
-    else return sm.boxa[a * 3 + d];
-  };
-
-  if (!REV) {
-    if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-      ldj += argmax_dequant(sm, A.dequant, A.noise_src(), M.a0, n, nf);
-    } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
-      for (int e = tid; e < n * nf; e += BLOCK) {
-        const int a = e / nf, q = e - a * nf;
-        sm.h[a * NFP + q] += A.dequant_scale * A.noise_src().uniform((size_t)M.a0 * nf + e);
-      }
-      __syncthreads();
-    }
-  }
-  STAMP(1);
-
-  for (int it = 0; it < A.n_layers; ++it) {
-    // Opaque per-layer copies: stop hipcc from hoisting every nf / molecule
-    // derived predicate and address out of the layer loop (SGPR/VGPR spills).
-    int nf = __builtin_amdgcn_readfirstlane(A.nf), n = __builtin_amdgcn_readfirstlane(M.n), tid_l = tid;
-    asm volatile("" : "+s"(nf), "+s"(n), "+v"(tid_l));
-    MolRef Ml = M;
-    Ml.n = n;
-    const EgclLayout L = egcl_layout(H, nf);
-    const int l = REV ? A.n_layers - 1 - it : it;
-    const float* Lp = A.layers + (size_t)l * L.total;
-    if (REV) {   // dynamics.py:28-30
-      for (int a = tid; a < n; a += BLOCK) {
-        for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] -= sm.g[a * NFP + q] * A.dt;
-        for (int d = 0; d < 3; ++d)
-          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, pbox(a, d));
-      }
-      __syncthreads();
-    }
-    if (!(ENFLOW_ABLATE & 1) || it == 0) build_images(sm, Ml, tid_l);
-    STAMP(3);
-    int npairs_layer = 0;
-    auto block_pass = [&](const int r0, const int rb) {
-      int tot;
-      if constexpr (BLOCKED) {
-        block_counts(sm, Ml, tid_l, r0, rb);
-        tot = block_compact(sm, n, tid_l, rb, 0);
-      } else {
-        if (!(ENFLOW_ABLATE & 1) || it == 0) build_block_pairs(sm, Ml, tid_l, r0, rb);
-        tot = sm.npairs;
-      }
-      STAMP(2);
-      npairs_layer += tot;
-      if (A.stats != nullptr && tid == 0) {
-        unsigned long long edges = 0;
-        for (int a = 0; a < rb; ++a) edges += (unsigned long long)sm.cntrow[r0 + a];
-        atomicAdd(&A.stats[0], (unsigned long long)tot);
-        atomicAdd(&A.stats[1], edges);
-      }
-      edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS);
-      if constexpr (BLOCKED) {   // blocks with more pairs than the buffer: further passes
-        constexpr int PC = Smem<H, NMAX, RB>::PC;
-        for (int p0 = PC; p0 < tot; p0 += PC) {
-          block_compact(sm, n, tid_l, rb, p0);
-          edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, false STAMP_PASS);
-        }
-      }
-      STAMP(4);
-      if (!(ENFLOW_ABLATE & 2)) {
-        if constexpr (PREC != PREC_F32) node_phase_x3(sm, Lp, L, n, nf, tid_l, r0, rb);   // fp32-accurate
-        else node_phase(sm, Lp, L, n, nf, tid_l, r0, rb);
-      }
-      STAMP(5);
-      if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q
-        const TapeLayout T = tape_layout(A.num_atoms, nf, H, A.n_layers);
-        const size_t la = (size_t)l * A.num_atoms + M.a0 + r0;
-        float* hx = A.tape + T.hx + la * T.ldhx;
-        for (int e = tid; e < rb * T.ldhx; e += BLOCK) {
-          const int a = e / T.ldhx, c = e - a * T.ldhx;
-          hx[e] = c < nf ? sm.h[(r0 + a) * NFP + c] : sm.agg[a * AST + (c - nf)];
-        }
-        for (int e = tid; e < rb * nf; e += BLOCK) {
-          const int a = e / nf, q = e - a * nf;
-          A.tape[T.g + la * nf + e] = sm.g[(r0 + a) * NFP + q];
-        }
-        for (int e = tid; e < rb * 3; e += BLOCK) {
-          A.tape[T.pos + la * 3 + e] = sm.pos[r0 * 3 + e];
-          A.tape[T.vel + la * 3 + e] = sm.vel[r0 * 3 + e];
-        }
-        for (int a = tid; a < rb; a += BLOCK) A.tape[T.q + la + a] = sm.Q[r0 + a];
-        __syncthreads();   // every thread's copy done before the leapfrog update rewrites pos / vel / h / g
-      }
-      if constexpr (BLOCKED) {   // park the block's forces (egcl.py:73-74)
-        for (int e = tid; e < rb * 3; e += BLOCK) {
-          const int a = e / 3, d = e - a * 3;
-          const float inv = 1.f / fmaxf((float)sm.cntrow[r0 + a], 1.f);
-          sm.F[(r0 + a) * 3 + d] = sm.agg[a * AST + H + d] * inv * A.cw;
-        }
-        __syncthreads();
-      }
-    };
-    if constexpr (BLOCKED) {
-      for (int r0 = 0; r0 < n; r0 += RB) block_pass(r0, min(RB, n - r0));
-    } else {
-      block_pass(0, n);   // the whole molecule in one pass
-    }
-    if (!REV && A.tape != nullptr && tid == 0 && A.pair_counts != nullptr)
-      A.pair_counts[(size_t)l * A.num_mols + blockIdx.x] = npairs_layer;
-    for (int a = tid; a < n; a += BLOCK) {
-      const float q = sm.Q[a];
-      const float eq = expf(q);
-      const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);   // helpers.py:63-70
-      auto force = [&](int d) {
-        if constexpr (BLOCKED) return sm.F[a * 3 + d];
-        else return sm.agg[a * AST + H + d] * inv * A.cw;
-      };
-      if (!REV) {  // dynamics.py:15-22
-        for (int d = 0; d < 3; ++d) {
-          const float F = force(d);
-          const float v = eq * sm.vel[a * 3 + d] + F * A.dt;
-          sm.vel[a * 3 + d] = v;
-          sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, pbox(a, d));
-        }
-        for (int qf = 0; qf < nf; ++qf) {
-          const float gn = sm.g[a * NFP + qf] + sm.G[a * NFP + qf] * A.dt;
-          sm.g[a * NFP + qf] = gn;
-          sm.h[a * NFP + qf] += gn * A.dt;
-        }
-        ldj += q;
-      } else {     // dynamics.py:32-35
-        for (int qf = 0; qf < nf; ++qf) sm.g[a * NFP + qf] -= sm.G[a * NFP + qf] * A.dt;
-        for (int d = 0; d < 3; ++d) {
-          const float F = force(d);
-          sm.vel[a * 3 + d] = (sm.vel[a * 3 + d] - F * A.dt) / eq;
-        }
-      }
-    }
-    __syncthreads();
-    STAMP(6);
-  }
-
-  if (REV) {   // dequantize.reverse (argmax.py:27-28 / floor.py:13)
-    for (int a = tid; a < n; a += BLOCK) {
-      if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-        int best = 0;
-        float bv = sm.h[a * NFP];
-        for (int q = 1; q < nf; ++q)
-          if (sm.h[a * NFP + q] > bv) { bv = sm.h[a * NFP + q]; best = q; }
-        A.argmax_idx[M.a0 + a] = best;
-        atomicMax(A.max_idx, best);
-      } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
-        for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] = floorf(sm.h[a * NFP + q]);
-      }
-    }
-    __syncthreads();   // the write-back below maps threads to elements differently
-  }
-  // write back.  Split-precision GEMMs (f16x3 / bf16) cannot represent operands
-  // past the fp16 / bf16 range: a non-finite output they produce is flagged
-  // (ENFLOW_ERR_RANGE) instead of returned silently; the f32 path returns
-  // whatever the arithmetic gives, as the reference does.
-  bool bad = false;
-  for (int e = tid; e < n * 3; e += BLOCK) {
-    const float p = sm.pos[e], v = sm.vel[e];
-    A.pos[(size_t)M.a0 * 3 + e] = p;
-    A.vel[(size_t)M.a0 * 3 + e] = v;
-    bad |= !__builtin_isfinite(p) || !__builtin_isfinite(v);
-  }
-  for (int e = tid; e < n * nf; e += BLOCK) {
-    const int a = e / nf, q = e - a * nf;
-    const float hv = sm.h[a * NFP + q], gv = sm.g[a * NFP + q];
-    A.h[(size_t)M.a0 * nf + e] = hv;
-    A.g[(size_t)M.a0 * nf + e] = gv;
-    bad |= (!REV && !__builtin_isfinite(hv)) || !__builtin_isfinite(gv);
-  }
-  if (!REV) {
-    const float s = block_sum(sm, ldj);
-    if (tid == 0) A.ldj_mol[blockIdx.x] = s;
-    bad |= tid == 0 && !__builtin_isfinite(s);
-  }
-  if constexpr (PREC != PREC_F32) {
-    if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
-  }
-  if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
-  if (!REV && A.ticket) ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
-  STAMP(7);
-  STAMP_FLUSH
-}
+#include "flow_kernel.h"
 
 // one EGCL.forward: Q, F, G to global
 template <int H, int NMAX, int RB>
@@ -655,6 +410,11 @@ static const double kLog2Pi = 1.8378770664093453;
 // molecule-size classes: <= 32 and <= 64 atoms unblocked, <= 256 atoms in
 // row blocks of 32 (BASELINE configs[4]: 256-atom chains)
 #define MAX_ATOMS 256
+#ifdef ENFLOW_DEV_ONLY
+// development build (tools/dev_asm.sh, never the product): only the headline
+// instance (H = 128, <= 32 atoms, f16x3, default flags) is compiled
+#define DISPATCH_HN(H, NMAXSEL, CALL) do { CALL(128, 32, 32); } while (0)
+#else
 #define DISPATCH_HN(H, NMAXSEL, CALL)                        \
   do {                                                        \
     if (NMAXSEL <= 32) {                                      \
@@ -671,6 +431,7 @@ static const double kLog2Pi = 1.8378770664093453;
       else { CALL(128, 256, 32); }                            \
     }                                                         \
   } while (0)
+#endif
 
 template <int HH, int NN, int RBB, bool REV, bool VAR>
 static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
@@ -684,6 +445,9 @@ static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs
     return;
   }
 #endif
+#ifdef ENFLOW_DEV_ONLY
+  if constexpr (REV || VAR) return;
+#endif
   if (prec == ENFLOW_PREC_F16X3)
     ENFLOW_TIMED(REV ? "lf_flow_kernel<rev>" : "lf_flow_kernel<fwd>", st,
                  hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A));
@@ -696,8 +460,22 @@ static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs
 }
 // gemm_precision may carry ENFLOW_EGCL_VARIANTS: layers packed with
 // enflow_pack_egcl_ex_f32 flags run on the variant-capable kernels
+// Latency instance (enflow_latency.hip, 8 waves per molecule, one workgroup per
+// CU) for <= 32-atom molecules when the batch has at most `threshold`
+// molecules; -1 (default): the device's CU count, i.e. whenever the 256-thread
+// kernel's two-per-CU slots would not all be busy for one round.
+static int g_lat_threshold = -1;
+static int lat_threshold_now() {
+  if (g_lat_threshold >= 0) return g_lat_threshold;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  return cus;
+}
+
 template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
+  if (NN == 32 && num_mols <= lat_threshold_now() && enflow_lat_launch(HH, REV, prec, num_mols, st, &A)) return;
   if (prec & ENFLOW_EGCL_VARIANTS) launch_flow_v<HH, NN, RBB, REV, true>(prec & 0xff, num_mols, st, A);
   else launch_flow_v<HH, NN, RBB, REV, false>(prec, num_mols, st, A);
 }
@@ -717,6 +495,12 @@ int enflow_read_stamps(unsigned long long* host_out, int reset) {
 #endif
 
 int enflow_abi_version(void) { return ENFLOW_ABI; }
+int enflow_set_latency_threshold(int max_mols) {
+  const int prev = g_lat_threshold;
+  g_lat_threshold = max_mols < 0 ? -1 : max_mols;
+  return prev;
+}
+int enflow_latency_threshold(void) { return lat_threshold_now(); }
 int enflow_max_atoms(void) { return MAX_ATOMS; }
 int enflow_max_node_nf(void) { return NFMAX; }
 int enflow_supports_hidden(int hidden_nf) { return hid_ok(hidden_nf); }

@@ -333,6 +333,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   }
   if (tid < 32) sm.cntrow[tid] = tid < rb ? B.cntrow[g0 + tid] : 0;
   if (tid == 0) {
+    sm.err = 0;
     int acc = 0;
     for (int a = 0; a < rb; ++a) { roff[a] = acc; acc += B.npairs[g0 + a]; }
     for (int a = rb; a <= 32; ++a) roff[a] = acc;
@@ -361,6 +362,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   }
   if constexpr (PREC != PREC_F32) node_phase_x3(sm, B.layer, L, rb, nf, tid, 0, rb);
   else node_phase(sm, B.layer, L, rb, nf, tid, 0, rb);
+  if (tid == 0 && sm.err) atomicOr(B.err, sm.err);   // edge tiles' range check (split precision)
 
   const bool tape = mode == 0 && B.tape != nullptr;
   if (tape) {   // training tape (as the fused kernel's): layer-input h / pos, message sums, Q

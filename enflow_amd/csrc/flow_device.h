@@ -11,17 +11,13 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 8
-#define WAVES 4
-#define BLOCK 256
+#define ENFLOW_ABI 9
+#ifndef WAVES
+#define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
+#endif
+#define BLOCK (64 * WAVES)
 #define NFMAX 8
 #define NFP 9  // LDS row stride of h / g / G (odd -> conflict-free across atoms)
-// ENFLOW_ABLATE (diagnostic builds only, outputs wrong): bit 1 = build pairs
-// only in layer 0, 2 = skip node phase, 4 = skip segment sums, 8 = SiLU -> identity,
-// 16 = skip GEMM2
-#ifndef ENFLOW_ABLATE
-#define ENFLOW_ABLATE 0
-#endif
 #ifndef ENFLOW_WAVES_PER_SIMD
 #define ENFLOW_WAVES_PER_SIMD 2   // workgroups of 4 waves per CU (VGPR budget 256 / 168 for 2 / 3)
 #endif
@@ -290,11 +286,7 @@ __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<
 
 __device__ __forceinline__ float sigm_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 __device__ __forceinline__ float silu_f(float x) {
-#if ENFLOW_ABLATE & 8
-  return x;
-#else
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x));   // v_rcp_f32 (1 ulp), not an IEEE divide
-#endif
 }
 
 // silu of 4 independent values in lock-step (mul, exp, add, rcp, mul x 4): every
@@ -305,7 +297,7 @@ __device__ __forceinline__ float silu_f(float x) {
 #define ENFLOW_SILU4_ASM 1
 #endif
 __device__ __forceinline__ f32x4 silu4(f32x4 z) {
-#if ENFLOW_SILU4_ASM && !(ENFLOW_ABLATE & 8)
+#if ENFLOW_SILU4_ASM
   float t0, t1, t2, t3;
   f32x4 y;
   asm("v_mul_f32 %4, 0xbfb8aa3b, %8\n\t"
@@ -340,7 +332,54 @@ __device__ __forceinline__ f32x4 silu4_fma(float x0, float x1, float x2, float x
   return silu4((f32x4){fmaf(x0, s, b[0]), fmaf(x1, s, b[1]), fmaf(x2, s, b[2]), fmaf(x3, s, b[3])});
 }
 
+// silu(z) of a scaled pre-activation a = K z (bias already inside a): with
+// c = -log2(e) / K,  silu(z) = a / (K + K 2^(a c))  -- mul, exp, fma, rcp, mul:
+// the power-of-two weight scale K and the bias cost no instruction of their own
+__device__ __forceinline__ float silu_sc(float a, float c, float K) {
+  return a * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_exp2f(a * c), K, K));
+}
+#ifndef ENFLOW_SILU4S_ASM
+#define ENFLOW_SILU4S_ASM 1
+#endif
+__device__ __forceinline__ f32x4 silu4s(f32x4 a, float c, float K) {
+#if ENFLOW_SILU4S_ASM
+  float t0, t1, t2, t3;
+  f32x4 y;
+  asm("v_mul_f32 %4, %12, %8\n\t"
+      "v_mul_f32 %5, %12, %9\n\t"
+      "v_mul_f32 %6, %12, %10\n\t"
+      "v_mul_f32 %7, %12, %11\n\t"
+      "v_exp_f32 %4, %4\n\t"
+      "v_exp_f32 %5, %5\n\t"
+      "v_exp_f32 %6, %6\n\t"
+      "v_exp_f32 %7, %7\n\t"
+      "v_fma_f32 %4, %4, %13, %13\n\t"
+      "v_fma_f32 %5, %5, %13, %13\n\t"
+      "v_fma_f32 %6, %6, %13, %13\n\t"
+      "v_fma_f32 %7, %7, %13, %13\n\t"
+      "v_rcp_f32 %4, %4\n\t"
+      "v_rcp_f32 %5, %5\n\t"
+      "v_rcp_f32 %6, %6\n\t"
+      "v_rcp_f32 %7, %7\n\t"
+      "v_mul_f32 %0, %8, %4\n\t"
+      "v_mul_f32 %1, %9, %5\n\t"
+      "v_mul_f32 %2, %10, %6\n\t"
+      "v_mul_f32 %3, %11, %7"
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "s"(c), "s"(K));
+  return y;
+#else
+  return (f32x4){silu_sc(a[0], c, K), silu_sc(a[1], c, K), silu_sc(a[2], c, K), silu_sc(a[3], c, K)};
+#endif
+}
+
 __device__ __forceinline__ float pbc1(float x, float b) { return x - rintf(x / b) * b; }
+
+// torch.clamp(x, -100, 100) (egcl.py:72): NaN passes through, as in torch
+// (fminf / fmaxf alone would map a NaN to a bound)
+__device__ __forceinline__ float clamp100(float x) {
+  return __builtin_isnan(x) ? x : fminf(fmaxf(x, -100.f), 100.f);
+}
 
 __device__ __forceinline__ float softplus_f(float x) { return x > 20.f ? x : log1pf(expf(x)); }
 __device__ __forceinline__ float logsigmoid_f(float x) { return fminf(x, 0.f) - log1pf(expf(-fabsf(x))); }
@@ -442,6 +481,50 @@ __device__ __forceinline__ void seg_scan4(float& a, float& b, float& c, float& d
       : "v"(M.m1), "v"(M.m2), "v"(M.m4), "v"(M.m8), "v"(M.m16));
 }
 
+// The same segmented scan, NaN-exact: each step's shifted copy is moved with
+// full EXEC (v_mov_b32_dpp), then added under an EXEC mask of the lanes whose
+// source lane is in their segment, so a NaN never leaks into a neighbouring
+// segment (the 0 * NaN of the multiplier form would).  2 VALU per value and
+// step instead of 1: used where it is cheap (the per-pair forces).
+struct SegExec { uint64_t e1, e2, e4, e8, e16; };
+
+__device__ __forceinline__ SegExec seg_exec(int row) {
+  SegExec E;
+  E.e1 = __ballot(dpp_i<0x111, 0xf>(-0x7fffffff, row) == row);
+  E.e2 = __ballot(dpp_i<0x112, 0xf>(-0x7fffffff, row) == row);
+  E.e4 = __ballot(dpp_i<0x114, 0xf>(-0x7fffffff, row) == row);
+  E.e8 = __ballot(dpp_i<0x118, 0xf>(-0x7fffffff, row) == row);
+  E.e16 = __ballot(dpp_i<0x142, 0xa>(-0x7fffffff, row) == row);
+  return E;
+}
+
+#define ENFLOW_SCANX_STEP(CTRL, MASK)                              \
+  "v_mov_b32_dpp %5, %0 " CTRL " bank_mask:0xf\n\t"              \
+  "v_mov_b32_dpp %6, %1 " CTRL " bank_mask:0xf\n\t"              \
+  "v_mov_b32_dpp %7, %2 " CTRL " bank_mask:0xf\n\t"              \
+  "v_mov_b32_dpp %8, %3 " CTRL " bank_mask:0xf\n\t"              \
+  "s_mov_b64 exec, " MASK "\n\t"                                 \
+  "v_add_f32 %0, %0, %5\n\t"                                     \
+  "v_add_f32 %1, %1, %6\n\t"                                     \
+  "v_add_f32 %2, %2, %7\n\t"                                     \
+  "v_add_f32 %3, %3, %8\n\t"                                     \
+  "s_mov_b64 exec, %4\n\t"
+
+__device__ __forceinline__ void seg_scan4x(float& a, float& b, float& c, float& d, const SegExec& E) {
+  uint64_t sv;
+  float t0, t1, t2, t3;
+  asm volatile("s_mov_b64 %4, exec\n\t"
+      "s_nop 1\n\t"
+      ENFLOW_SCANX_STEP("row_shr:1 row_mask:0xf", "%9")
+      ENFLOW_SCANX_STEP("row_shr:2 row_mask:0xf", "%10")
+      ENFLOW_SCANX_STEP("row_shr:4 row_mask:0xf", "%11")
+      ENFLOW_SCANX_STEP("row_shr:8 row_mask:0xf", "%12")
+      ENFLOW_SCANX_STEP("row_bcast:15 row_mask:0xa", "%13")
+      : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "=&s"(sv), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+      : "s"(E.e1), "s"(E.e2), "s"(E.e4), "s"(E.e8), "s"(E.e16));
+}
+#undef ENFLOW_SCANX_STEP
+
 __device__ __forceinline__ float seg_scan(float v, const SegMasks& M) {
   v = fmaf(M.m1, dpp_f<0x111, 0xf>(v), v);
   v = fmaf(M.m2, dpp_f<0x112, 0xf>(v), v);
@@ -497,9 +580,15 @@ __device__ __forceinline__ void chain_gemm_wide(rsrc_t W, int off_floats, const 
 // Same wide chain with a VALU/LDS "filler" interleaved into every step: fill(step)
 // must not touch acc; sched_group_barrier asks hipcc to alternate one MFMA with
 // up to FPM filler instructions, so the filler issues while the MFMAs execute.
-template <int NT, int FPM, class Fill>
+struct NoMid {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// mid(): called once (NT == 4 only), outside the MFMA/filler scheduling groups,
+// after fillers 0 .. 2 NT - 1 and before filler 2 NT
+template <int NT, int FPM, class Fill, class Mid = NoMid>
 __device__ __forceinline__ void chain_gemm_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                                int lane, Fill&& fill) {
+                                                int lane, Fill&& fill, Mid&& mid = NoMid{}) {
   f32x4 cur[NT], nxt[NT];
   const int vo = lane * 16;
 #pragma unroll
@@ -507,6 +596,11 @@ __device__ __forceinline__ void chain_gemm_fill(rsrc_t W, int off_floats, const 
 #pragma unroll
   for (int step = 0; step < NT * 4; ++step) {
     const int t = step >> 2, rg = step & 3;
+    if (NT == 4 && step == 8) {
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (step + 1 < NT * 4) {
       const int t2 = (step + 1) >> 2, rg2 = (step + 1) & 3;
 #pragma unroll
@@ -627,14 +721,14 @@ __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
 // filler calls (4 NT per GEMM, the fp32 chain's granularity) are interleaved
 // between the MFMAs.
 #ifndef ENFLOW_X3_TPG
-#define ENFLOW_X3_TPG 2      // output tiles per step
+#define ENFLOW_X3_TPG 1      // output tiles per step (2: 73 VGPR spills in the tile loop since the bias-in-accumulator SiLU)
 #endif
 #ifndef ENFLOW_X3_DEPTH
 #define ENFLOW_X3_DEPTH 2    // fragment ring depth (prefetch distance + 1 steps)
 #endif
-template <int NT, int FPM, class Fill>
+template <int NT, int FPM, class Fill, class Mid = NoMid>
 __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                              int lane, Fill&& fill) {
+                                              int lane, Fill&& fill, Mid&& mid = NoMid{}) {
   constexpr int TPG = NT >= ENFLOW_X3_TPG ? ENFLOW_X3_TPG : NT;
   constexpr int NGR = NT / TPG;
   constexpr int S = NT * 2 * NGR;
@@ -654,11 +748,7 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
 #pragma unroll
       for (int q = 0; q < TPG; ++q) {
         rh[d][q] = bload4(W, vo, foff(d, q));
-#ifdef ENFLOW_ABLATE_LOFRAG
-        rl[d][q] = rh[d][q];   // timing ablation: half the fragment traffic (wrong numerics)
-#else
         rl[d][q] = bload4(W, vo + 16, foff(d, q));
-#endif
       }
     }
   f16x8 bh, bl;
@@ -667,16 +757,17 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
   for (int step = 0; step < S; ++step) {
     const int gi = step % NGR;
     const int cur = step % D;
+    if (NT == 4 && step * FPS == 2 * NT) {   // fillers 0 .. 2 NT - 1 have run
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (step + D - 1 < S) {
       const int sl = (step + D - 1) % D;
 #pragma unroll
       for (int q = 0; q < TPG; ++q) {
         rh[sl][q] = bload4(W, vo, foff(step + D - 1, q));
-#ifdef ENFLOW_ABLATE_LOFRAG
-        rl[sl][q] = rh[sl][q];
-#else
         rl[sl][q] = bload4(W, vo + 16, foff(step + D - 1, q));
-#endif
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -706,9 +797,9 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
 }
 
 // acc[tp] += W[tp][t] X[t] in BF16: 2NT k-steps of NT MFMAs.
-template <int NT, int FPM, class Fill>
+template <int NT, int FPM, class Fill, class Mid = NoMid>
 __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                               int lane, Fill&& fill) {
+                                               int lane, Fill&& fill, Mid&& mid = NoMid{}) {
   constexpr int S = 2 * NT;
   f32x4 cb[NT], nb[NT];
   const int vo = lane * 16;
@@ -717,6 +808,11 @@ __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f
   bf16x8 b = to_bf16(X[0], 0);
 #pragma unroll
   for (int step = 0; step < S; ++step) {
+    if (NT == 4 && step == 4) {
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if (step + 1 < S) {
       const int t2 = (step + 1) >> 1, s2 = (step + 1) & 1;
 #pragma unroll
@@ -744,12 +840,28 @@ __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f
 }
 
 // GEMM with the precision's chain; off_* are the packed sections of the matrix
-template <int PREC, int NT, int FPM, class Fill>
+template <int PREC, int NT, int FPM, class Fill, class Mid = NoMid>
 __device__ __forceinline__ void chain_prec_fill(rsrc_t W, int off_f32, int off_x3, int off_b16, const f32x16 (&X)[NT],
-                                                f32x16 (&acc)[NT], int lane, Fill&& fill) {
-  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM>(W, off_x3, X, acc, lane, fill);
-  else if constexpr (PREC == PREC_BF16) chain_b16_fill<NT, FPM>(W, off_b16, X, acc, lane, fill);
-  else chain_gemm_fill<NT, FPM>(W, off_f32, X, acc, lane, fill);
+                                                f32x16 (&acc)[NT], int lane, Fill&& fill, Mid&& mid = NoMid{}) {
+  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM>(W, off_x3, X, acc, lane, fill, mid);
+  else if constexpr (PREC == PREC_BF16) chain_b16_fill<NT, FPM>(W, off_b16, X, acc, lane, fill, mid);
+  else chain_gemm_fill<NT, FPM>(W, off_f32, X, acc, lane, fill, mid);
+}
+
+// accumulators initialised from a bias image in LDS (acc[t][4 g4 + u] holds
+// feature 32 t + 8 g4 + 4 hh + u): the bias enters the MFMA chain, nothing is
+// added after it.  The image holds the bias times the weights' power-of-two
+// scale, so the chain's result is scale * (W x + b).
+template <int NT>
+__device__ __forceinline__ void acc_from_bias(f32x16 (&acc)[NT], const float* __restrict__ b, int hh) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 v = ld4(b + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[t][4 * g4 + u] = v[u];
+    }
 }
 
 // X[t][r] = silu(X[t][r] + bias[32 t + rho(r, hh)]); bias read from LDS as float4
@@ -860,8 +972,15 @@ struct Smem {
   int err;
   float red[WAVES];
   static constexpr int NDT = BWD ? 1 : NT, NDR = BWD ? 1 : RB;
+  // <= 32-atom images (and the large-system row blocks): the edge tiles' message
+  // segment sums go through a per-wave LDS scratch [32 pairs][MSP] in the union
+  // (free during the tiles); other images scan in registers (seg_scan4x)
+  static constexpr bool MSG_LDS = !BWD && NMAX == 32 && RB == 32 ;
+  static constexpr int MSW = H < 64 ? H : 64;                         // features per reduce chunk
+  static constexpr int MSP = MSW + 1;                                 // odd row stride: conflict-free
   union {
     int C[CW];                                                    // pair build (block rows x atoms)
+    float msg[MSG_LDS ? WAVES : 1][MSG_LDS ? 32 * MSP : 1];       // edge tiles: per-wave message scratch
     struct { float qp[NDT][NDR]; float gp[NDT][NFMAX][NDR]; } nd;   // node phase partials
     float net[NETA * 2 * NFMAX];                                  // ArgMax outputs
     float nb[NBW];                                                // BWD: node adjoint rows
@@ -1127,10 +1246,15 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   if (zero_agg)   // first compaction pass of the block (later passes accumulate)
     for (int e = tid; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
   for (int e = tid; e < WAVES * (H + 4); e += BLOCK) (&sm.head[0][0])[e] = 0.f;
+  // split-precision GEMMs run on weights scaled by 2^s (K below): the bias image
+  // carries the same factor, the accumulators start from it (acc_from_bias)
+  const float K0 = PREC != PREC_F32 ? Lp[L.scl + 4] : 1.f;   // edge_nn.0 runs F16X3 in bf16 mode too
+  const float K1 = PREC == PREC_F16X3 ? Lp[L.scl + 0] : 1.f;
+  const float K2 = PREC == PREC_F16X3 ? Lp[L.scl + 2] : 1.f;
   for (int k = tid; k < H; k += BLOCK) {
-    sm.bias[k] = Lp[L.be1 + k];
-    sm.bias[H + k] = Lp[L.be2 + k];
-    sm.bias[2 * H + k] = Lp[L.bc1 + k];
+    sm.bias[k] = Lp[L.be1 + k] * K0;
+    sm.bias[H + k] = Lp[L.be2 + k] * K1;
+    sm.bias[2 * H + k] = Lp[L.bc1 + k] * K2;
     sm.bias[3 * H + k] = Lp[L.wc2 + k];
   }
   if constexpr (PREC != PREC_F32 && Smem<H, NMAX, RB>::W1X_LDS) {   // GEMM0 is F16X3 in bf16 mode too
@@ -1162,16 +1286,26 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const int nh = (nf + 1) >> 1;
   const rsrc_t W = weights_rsrc(Lp, L.total);
   const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
-  // F16X3 accumulators carry the weight scale 2^s: unscale exactly in the bias fma
-  const float inv0 = PREC != PREC_F32 ? Lp[L.scl + 5] : 1.f;   // edge_nn.0 runs F16X3 in bf16 mode too
-  const float inv1 = PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f;
-  const float inv2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
+  // scaled SiLU constants (silu4s): c = -log2(e) / K
+  constexpr float NLOG2E = -1.4426950408889634f;
+  const float c0 = NLOG2E * (PREC != PREC_F32 ? Lp[L.scl + 5] : 1.f);
+  const float c1 = NLOG2E * (PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f);
+  const float c2 = NLOG2E * (PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f);
+  constexpr bool MSG_LDS = Smem<H, NMAX, RB>::MSG_LDS;
+  constexpr int MSP = Smem<H, NMAX, RB>::MSP;
+  float* const scr = MSG_LDS ? &sm.u.msg[w][0] : nullptr;
   // constructor variants of the layer (wave-uniform; compiled in only for VAR
   // kernels, the default-flag kernels keep their registers)
   const int vfl = VAR ? (int)Lp[L.vfl] : 0;
   const bool v_att = (vfl & EGCL_ATTENTION) != 0, v_nd = (vfl & EGCL_NORM_DIFF) != 0,
              v_tanh = (vfl & EGCL_TANH) != 0;
 
+  // split-precision range check: an fp16 / bf16 operand past its range makes the
+  // MFMA products inf / NaN; the per-pair scalars where the reference's own ops
+  // would squash that back to a finite value (tanh, the clamp, the attention
+  // sigmoid) are tested here, everything else propagates to the outputs, which
+  // the kernels test as well (ENFLOW_ERR_RANGE)
+  bool range_bad = false;
   STAMP(8);
   for (int tile = t0; tile < t1; ++tile) {
     const int p = tile * 32 + j;
@@ -1192,7 +1326,12 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     };
     // segments = runs of equal row; invalid lanes get unique rows of their own
     const int row = valid ? il : -1 - j;
-    const SegMasks SM = seg_masks(row);
+    // segment masks: exact (EXEC) form with the LDS message path, else the
+    // multiplier form (its 0 * NaN can spread a NaN input to a neighbouring row)
+    SegExec SE;
+    SegMasks SM;
+    if constexpr (MSG_LDS) SE = seg_exec(row);
+    else SM = seg_masks(row);
     const int row_next = __shfl_down(row, 1, 32);
     const bool seg_end = valid && (j == 31 || row_next != row);
     float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? il : 0) * AST];
@@ -1206,8 +1345,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     //      9 fixed k-steps (zero-padded past nf): 4 h_i pairs, 4 h_j pairs, radial;
     //      h rows are zero-padded in LDS, so padded steps multiply zeros
     f32x16 x0[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
+    acc_from_bias<NT>(x0, sm.bias, hh);
     if constexpr (PREC != PREC_F32) {   // F16X3 (bf16 mode too: a 16-wide k-step on the matrix cores
       // beats 9 f32 k-steps; only edge_nn.2 / coord_nn.0 run in bf16)
       // k order gemm0_col: lane half 0 = h_i's padded row, half 1 = h_j's (+ radial)
@@ -1280,46 +1418,37 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // (split-precision GEMM0 accumulators carry edge_nn.0's 2^s: unscaled in the bias fma)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 8 * g4 + 4 * hh);
-{
-        const f32x4 y = silu4_fma(x0[0][4 * g4], x0[0][4 * g4 + 1], x0[0][4 * g4 + 2], x0[0][4 * g4 + 3], inv0, b);
-        for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = y[u];
-      }
+      const f32x4 y = silu4s((f32x4){x0[0][4 * g4], x0[0][4 * g4 + 1], x0[0][4 * g4 + 2], x0[0][4 * g4 + 3]}, c0, K0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = y[u];
     }
     STAMP(10);
 
     // ---- GEMM1: E^T = edge_nn.2 (egcl.py:20-24)
     f32x16 e[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) e[t] = (f32x16)0.f;
+    acc_from_bias<NT>(e, sm.bias + H, hh);
     chain_prec_fill<PREC, NT, 2>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
-        const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 32 * t + 8 * g4 + 4 * hh);
-{
-          const f32x4 y = silu4_fma(x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3], inv0, b);
-          for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = y[u];
-        }
+        const f32x4 y = silu4s((f32x4){x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3]}, c0, K0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = y[u];
       }
     });
     STAMP(11);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 8 * g4 + 4 * hh);
-{
-        const f32x4 y = silu4_fma(e[0][4 * g4], e[0][4 * g4 + 1], e[0][4 * g4 + 2], e[0][4 * g4 + 3], inv1, b);
-        for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = y[u];
-      }
+      const f32x4 y = silu4s((f32x4){e[0][4 * g4], e[0][4 * g4 + 1], e[0][4 * g4 + 2], e[0][4 * g4 + 3]}, c1, K1);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = y[u];
     }
     if (v_att) {   // egcl.py:60-62: out *= sigmoid(att_nn(out)); every tile activated first
 #pragma unroll
       for (int t = 1; t < NT; ++t)
 #pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * t + 8 * g4 + 4 * hh);
+        for (int g4 = 0; g4 < 4; ++g4)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) e[t][4 * g4 + u] = silu_f(fmaf(e[t][4 * g4 + u], inv1, b[u]));
-        }
+          for (int u = 0; u < 4; ++u) e[t][4 * g4 + u] = silu_sc(e[t][4 * g4 + u], c1, K1);
       float d = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -1329,7 +1458,9 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
           for (int u = 0; u < 4; ++u) d = fmaf(wa[u], e[t][4 * g4 + u], d);
         }
-      const float att = sigm_f(d + __shfl_xor(d, 32, 64) + Lp[L.batt]);
+      const float dl = d + __shfl_xor(d, 32, 64) + Lp[L.batt];
+      if constexpr (PREC != PREC_F32) range_bad |= valid && !__builtin_isfinite(dl);
+      const float att = sigm_f(dl);
 #pragma unroll
       for (int t = 0; t < NT; ++t) e[t] *= att;
     }
@@ -1343,54 +1474,69 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     //      segment ends write), one adder per (row, feature) and tile)
     float* const rowp = dst_row + 4 * hh;
     float part = 0.f;
+    // message segment sums, LDS images: c e[t] of feature tile t goes to the wave's
+    // scratch (row = pair, 64-feature chunks); a chunk is reduced by feature lanes
+    // walking the tile's 32 pairs in order and adding each finished row segment
+    // into its aggregate row (uniform control: the segment ends are one mask)
+    const uint32_t endm = (uint32_t)__ballot(seg_end && hh == 0);
+    auto reduce_chunk = [&](int chn) {
+      if constexpr (MSG_LDS) {
+        const int f = lane;                        // feature (MSP - 1) chn + lane of the chunk
+        const bool fv = lane < MSP - 1;            // H = 32: 32 features, lanes 32.. idle
+        const float* col = scr + (fv ? f : 0);
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < 32; ++q) {
+          acc += col[q * MSP];
+          if (endm & (1u << q)) {
+            const int r = __builtin_amdgcn_readlane(row, q);
+            float* d = (ishead && r == headrow) ? &sm.head[w][0] : &sm.agg[r * AST];
+            if (fv) atomicAdd(d + (MSP - 1) * chn + f, acc);   // one wave adds to a row: fixed order
+            acc = 0.f;
+          }
+        }
+      }
+    };
     {
       f32x16 hc[NT];
-#pragma unroll
-      for (int t = 0; t < NT; ++t) hc[t] = (f32x16)0.f;
-#if ENFLOW_ABLATE & 16
-      for (int t = 0; t < NT; ++t) hc[t] = e[t];
-      if (0)
-#endif
+      acc_from_bias<NT>(hc, sm.bias + 2 * H, hh);
       chain_prec_fill<PREC, NT, 6>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
         const int t = step >> 2, g4 = step & 3;
-#if !(ENFLOW_ABLATE & 4)
-        f32x4* const slot = reinterpret_cast<f32x4*>(rowp + 32 * t + 8 * g4);
-        const f32x4 old = *slot;
         float v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = c * e[t][4 * g4 + u];
-#if ENFLOW_SEGSCAN_ASM
-        seg_scan4(v[0], v[1], v[2], v[3], SM);
-#else
+        if constexpr (MSG_LDS) {
+          float* const sp = scr + j * MSP + 32 * (t & 1) + 8 * g4 + 4 * hh;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = seg_scan(v[u], SM);
-#endif
-        if (seg_end) *slot = old + (f32x4){v[0], v[1], v[2], v[3]};
-#endif
-        if (t + 1 < NT && !v_att) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + H + 32 * (t + 1) + 8 * g4 + 4 * hh);
-{
-            const f32x4 y = silu4_fma(e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
-                                      e[t + 1][4 * g4 + 3], inv1, b);
-            for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
-          }
+          for (int u = 0; u < 4; ++u) sp[u] = v[u];
+        } else {
+          f32x4* const slot = reinterpret_cast<f32x4*>(rowp + 32 * t + 8 * g4);
+          const f32x4 old = *slot;
+          seg_scan4(v[0], v[1], v[2], v[3], SM);
+          if (seg_end) *slot = old + (f32x4){v[0], v[1], v[2], v[3]};
         }
-      });
+        if (t + 1 < NT && !v_att) {
+          const f32x4 y = silu4s((f32x4){e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
+                                         e[t + 1][4 * g4 + 3]}, c1, K1);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
+        }
+      }, [&] { reduce_chunk(0); });
+      reduce_chunk(NT == 4 ? 1 : 0);
       // coord_nn.2 as a per-pair dot
 #pragma unroll
       for (int tp = 0; tp < NT; ++tp)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 b = *reinterpret_cast<const f32x4*>(sm.bias + 2 * H + 32 * tp + 8 * g4 + 4 * hh);
           const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * tp + 8 * g4 + 4 * hh);
-{
-            const f32x4 y = silu4_fma(hc[tp][4 * g4], hc[tp][4 * g4 + 1], hc[tp][4 * g4 + 2], hc[tp][4 * g4 + 3],
-                                      inv2, b);
-            for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
-          }
+          const f32x4 y = silu4s((f32x4){hc[tp][4 * g4], hc[tp][4 * g4 + 1], hc[tp][4 * g4 + 2], hc[tp][4 * g4 + 3]},
+                                 c2, K2);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
         }
     }
     float phi = part + __shfl_xor(part, 32, 64);
+    if constexpr (PREC != PREC_F32) range_bad |= valid && !__builtin_isfinite(phi);
     if (v_tanh) phi = tanhf(phi);                        // egcl.py:40-42
     // norm_diff: coord_diff / (|coord_diff| + 1) (egcl.py:82-84; radial stays unnormalised)
     const float nd = v_nd ? __builtin_amdgcn_rcpf(sqrtf(radial) + 1.f) : 1.f;
@@ -1398,19 +1544,18 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // for the mean (egcl.py:73-74); lane half 0 stores
     f32x4* const fslot = reinterpret_cast<f32x4*>(dst_row + H);   // H + 3 is padding (tw = 0)
     const f32x4 fold = *fslot;
-    float tx = c * fminf(fmaxf(dx * nd * phi, -100.f), 100.f);
-    float ty = c * fminf(fmaxf(dy * nd * phi, -100.f), 100.f);
-    float tz = c * fminf(fmaxf(dz * nd * phi, -100.f), 100.f);
+    float tx = c * clamp100(dx * nd * phi);
+    float ty = c * clamp100(dy * nd * phi);
+    float tz = c * clamp100(dz * nd * phi);
     float tw = 0.f;
-#if ENFLOW_SEGSCAN_ASM
-    seg_scan4(tx, ty, tz, tw, SM);
-#else
-    tx = seg_scan(tx, SM);
-    ty = seg_scan(ty, SM);
-    tz = seg_scan(tz, SM);
-#endif
+    if constexpr (MSG_LDS) seg_scan4x(tx, ty, tz, tw, SE);
+    else seg_scan4(tx, ty, tz, tw, SM);
     if (seg_end && hh == 0) *fslot = fold + (f32x4){tx, ty, tz, tw};
     STAMP(14);
+  }
+  if constexpr (PREC != PREC_F32) {
+    if (__ballot(range_bad))
+      if (lane == 0) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
   }
   __syncthreads();
   STAMP(15);

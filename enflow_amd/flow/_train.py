@@ -58,15 +58,21 @@ class _FlowFunction(torch.autograd.Function):
         # queue the backward's weight packing (cached on the parameters' versions,
         # which cannot change before this graph's backward) and the dequantiser's
         # flat parameters behind the forward kernel, ahead of the error check's sync
-        flow.training_layers(dev)
+        # the buffers and the parameter versions they were packed from go with this
+        # graph: the backward uses exactly these and refuses in-place changes since
+        ctx.train_bufs = flow.training_layers(dev)
+        ctx.train_key = flow._params_key(dev)
         ctx.dq_raw = None
         if kind == _lib.DEQUANT_ARGMAX:
             ctx.dq_raw = flow.dequantize.kernel_raw(dev, hid)
         if meta["check_errors"]:
-            # no host sync here: the word is read at the next check -- the start of
-            # this graph's backward (before anything consumes the outputs' gradients),
-            # or the next forward -- so the host keeps queueing the loss and backward
-            _lib.defer_err(err)
+            if getattr(flow, "defer_error_check", False):
+                # no host sync: the word is read at the start of this graph's
+                # backward (before anything consumes the outputs' gradients) or
+                # at the next check
+                _lib.defer_err(err)
+            else:
+                _lib.raise_on_err(err)      # the reference raises inside forward
         ctx.flow, ctx.meta, ctx.kind = flow, meta, kind
         ctx.n_params = len(params)
         ctx.save_for_backward(h_in, tape, counts)
@@ -91,7 +97,10 @@ class _FlowFunction(torch.autograd.Function):
         ah, ag = adj(gh, (A, nf)), adj(gg, (A, nf))
         apos, avel = adj(gpos, (A, 3)), adj(gvel, (A, 3))
         aldj = adj(gldj, ()).reshape(1)
-        fwd, bwd, raw = flow.training_layers(dev)
+        if flow._params_key(dev) != ctx.train_key:
+            raise RuntimeError("enflow_amd: a parameter of the flow was modified in place between forward "
+                               "and backward (autograd would report a version mismatch here)")
+        fwd, bwd, raw = ctx.train_bufs
         grad_layers = torch.empty_like(raw)
         dq_raw, grad_dq = None, None
         if kind == _lib.DEQUANT_ARGMAX:

@@ -32,6 +32,11 @@ class LFIntegrator(BaseFlow):
     fp16 hi+lo, three products, fp32 accumulation; default) or "bf16"
     (reduced-precision generate path, BASELINE configs[2])."""
     gemm_precision = "f16x3"
+    # training forward: False (default) reads the kernel's error word before
+    # returning, so a bad batch raises inside forward like the reference
+    # (enflow/data/base.py:137); True queues it and raises at the start of
+    # loss.backward() instead (no host sync between forward and backward)
+    defer_error_check = False
 
     def _prec(self):
         try:
@@ -190,7 +195,7 @@ class LFIntegrator(BaseFlow):
             _lib.stream_ptr(dev)), "enflow_lf_forward_io_f32")
 
     def reverse_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, argmax_idx, max_idx, err,
-                        src=None):
+                        src=None, prec=None):
         """Fused reverse on preallocated fp32 device buffers (no host sync, no
         allocation); ``src`` = (h, g, pos, vel) inputs (None: in place); with
         ArgMax, argmax_idx / max_idx receive the dequantiser's indices
@@ -198,6 +203,7 @@ class LFIntegrator(BaseFlow):
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         L = _lib.lib()
+        prec = self._prec() if prec is None else prec
         if _lib.is_large(max_mol_atoms):
             if src is not None:
                 for o, i in zip((h, g, pos, vel), src):
@@ -208,7 +214,7 @@ class LFIntegrator(BaseFlow):
                 mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
                 _lib.ptr(box), _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
                 _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
-                _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), self._prec(), _lib.ptr(ws), ws.numel(),
+                _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), prec, _lib.ptr(ws), ws.numel(),
                 _lib.stream_ptr(h.device)), "enflow_lf_reverse_large_f32")
             return
         si = (None,) * 4 if src is None else tuple(_lib.ptr(t) for t in src)
@@ -216,7 +222,7 @@ class LFIntegrator(BaseFlow):
             mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
             _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
             _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
-            _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), self._prec(), _lib.stream_ptr(h.device)),
+            _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), prec, _lib.stream_ptr(h.device)),
             "enflow_lf_reverse_io_f32")
 
     def _state(self, data):
@@ -254,15 +260,30 @@ class LFIntegrator(BaseFlow):
             key = (int(torch.randint(0, 2 ** 62, (1,)).item()), 0)
         else:
             noise = noise.to(device=dev, dtype=torch.float32).contiguous()
+        if noise is None and _lib.is_large(s["max_n"]) and self._dequant_kind() != _lib.DEQUANT_NONE:
+            # the large-system path takes its draws from the caller: draw once here so
+            # that a range re-run (below) sees the same noise
+            noise = _host_noise(self._dequant_kind(), s["h"].shape, dev)
         M = s["mol_ptr"].numel() - 1
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
         st = _lib.status_word(dev) if check_errors else torch.zeros(2, dtype=torch.int32, device=dev)
-        self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
-                             s["max_n"], noise, ldj_mol, ldj, st[:1], src=s["src"], noise_key=key,
-                             ticket=st[1:])
-        if check_errors:
-            _lib.raise_on_err(st[:1], reset=True)
+        prec = self._prec()
+        while True:
+            self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
+                                 s["max_n"], noise, ldj_mol, ldj, st[:1], src=s["src"], noise_key=key,
+                                 ticket=st[1:], prec=prec)
+            if not check_errors:
+                break
+            try:
+                _lib.raise_on_err(st[:1], reset=True)
+                break
+            except _lib.RangeError:
+                # an fp16 / bf16 operand overflowed: the same launch with fp32 GEMMs
+                # (same noise key, same inputs) returns the reference's result
+                if (prec & 0xff) == _lib.PREC_F32:
+                    raise
+                prec = _fp32_prec(prec)
         dt = data.h.dtype
         data.h, data.g = s["h"].to(dt), s["g"].to(dt)
         data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
@@ -280,10 +301,20 @@ class LFIntegrator(BaseFlow):
         mx = torch.zeros(1, dtype=torch.int32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         L = _lib.lib()
-        self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"], s["max_n"],
-                             idx, mx, err, src=s["src"])
-        if check_errors:
-            _lib.raise_on_err(err)
+        prec = self._prec()
+        while True:
+            self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
+                                 s["max_n"], idx, mx, err, src=s["src"], prec=prec)
+            if not check_errors:
+                break
+            try:
+                _lib.raise_on_err(err, reset=True)
+                break
+            except _lib.RangeError:      # as in forward: re-run with fp32 GEMMs
+                if (prec & 0xff) == _lib.PREC_F32:
+                    raise
+                prec = _fp32_prec(prec)
+                mx.zero_()
         dt = data.h.dtype
         if kind == _lib.DEQUANT_ARGMAX:
             width = int(mx.item()) + 1
@@ -296,6 +327,11 @@ class LFIntegrator(BaseFlow):
         data.g = s["g"].to(dt)
         data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
         return data
+
+
+def _fp32_prec(prec):
+    """The same kernel selection with fp32 edge GEMMs (variant bits kept)."""
+    return (prec & ~0xff) | _lib.PREC_F32
 
 
 def _host_noise(kind, shape, dev):

@@ -55,8 +55,21 @@ extern "C" {
  * on large systems -- tape / pair_rows of enflow_lf_forward_large_f32, enflow_lf_backward_large_f32,
  * enflow_alchemical_nll_backward_f32 for any molecule size; 8: out-of-place, self-contained
  * forward / reverse -- enflow_lf_forward_io_f32 (in-kernel dequantiser draws, in-launch
- * log|detJ| reduction), enflow_lf_reverse_io_f32). */
+ * log|detJ| reduction), enflow_lf_reverse_io_f32; 9: ENFLOW_ERR_RANGE also flagged for a
+ * non-finite phi / attention logit before tanh / clamp / sigmoid, the clamp passes NaN like
+ * torch.clamp, latency instances of the fused flow kernel, enflow_set_latency_threshold). */
 int enflow_abi_version(void);
+
+/* Batches of <= 32-atom molecules with at most this many molecules run the
+ * fused flow kernel's latency instance (8 waves per molecule, one workgroup
+ * per CU) instead of the 4-wave one (two per CU).  -1 (default): the current
+ * device's CU count.  Replaces no reference interface: the reference has no
+ * kernels; this is the strong-scaling knob of enflow/main.py:141-145's
+ * DistributedSampler split (a fixed batch over more GPUs = fewer molecules per
+ * GPU).  Returns the previous setting; enflow_latency_threshold() returns the
+ * one in effect on the current device. */
+int enflow_set_latency_threshold(int max_mols);
+int enflow_latency_threshold(void);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept. */
 int enflow_max_atoms(void);

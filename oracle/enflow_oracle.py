@@ -110,8 +110,16 @@ def molecule_edges(pos, box, r_cut):
     self pairs by label (base.py:139).
     """
     imgs, id_mapping = periodic_images_within(pos, box, r_cut)
-    d2 = np.sum((imgs[:, None, :] - pos[None, :, :]) ** 2, axis=2)
-    ids = np.argwhere(d2 < r_cut * r_cut)          # row-major == torch.nonzero
+    # row-major hits (== torch.nonzero), in chunks of images so that large
+    # boxes (example/generate.yaml: 2944 atoms, ~80 k images) fit in memory
+    chunk = max(1, (1 << 24) // max(pos.shape[0], 1))
+    parts = []
+    for c0 in range(0, imgs.shape[0], chunk):
+        d2 = np.sum((imgs[c0:c0 + chunk, None, :] - pos[None, :, :]) ** 2, axis=2)
+        hit = np.argwhere(d2 < r_cut * r_cut)
+        hit[:, 0] += c0
+        parts.append(hit)
+    ids = np.concatenate(parts) if parts else np.zeros((0, 2), dtype=np.int64)
     if ids.size and ids[:, 1].max() >= id_mapping.shape[0]:
         raise IndexError("reference would index id_mapping out of range "
                          "(fewer periodic images than atoms)")

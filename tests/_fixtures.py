@@ -64,10 +64,58 @@ def n_layers(inp):
     return int(inp["n_layers"])
 
 
-def rel_err(a, b):
+class NonFiniteError(AssertionError):
+    """A parity operand holds NaN / inf: the comparison is meaningless."""
+
+
+def _finite_pair(a, b, allow_nonfinite):
     a = np.asarray(a, dtype=np.float64)
     b = np.asarray(b, dtype=np.float64)
+    if not allow_nonfinite:
+        for name, x in (("result", a), ("reference", b)):
+            if not np.all(np.isfinite(x)):
+                bad = int(np.size(x) - np.count_nonzero(np.isfinite(x)))
+                raise NonFiniteError(f"{name} holds {bad} non-finite of {np.size(x)} values")
+    return a, b
+
+
+def rel_err(a, b, allow_nonfinite=False):
+    """max|a - b| / max|b| (per tensor).  Raises NonFiniteError when either
+    side holds NaN / inf (NaN would otherwise compare False against any bar
+    and vanish inside max()), unless the caller opts in."""
+    a, b = _finite_pair(a, b, allow_nonfinite)
+    if a.size == 0 and b.size == 0:
+        return 0.0
     return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))
+
+
+def normwise(a, b, allow_nonfinite=False):
+    """||a - b||_2 / ||b||_2, same non-finite rule as rel_err."""
+    a, b = _finite_pair(a, b, allow_nonfinite)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def scalar_rel(a, b):
+    """|a - b| / |b| for two scalars; raises on non-finite."""
+    a, b = float(a), float(b)
+    if not (np.isfinite(a) and np.isfinite(b)):
+        raise NonFiniteError(f"non-finite scalar: {a} vs {b}")
+    return abs(a - b) / max(abs(b), 1e-300)
+
+
+def worst_of(errs):
+    """max over a dict / list of errors that is NaN-propagating."""
+    vals = list(errs.values()) if isinstance(errs, dict) else list(errs)
+    if any(not np.isfinite(v) for v in vals):
+        return float("nan")
+    return max(vals) if vals else 0.0
+
+
+def assert_all_within(errs, tol, what=""):
+    """Every error finite and <= tol.  NaN fails (it would slip through max())."""
+    items = errs.items() if isinstance(errs, dict) else enumerate(errs)
+    bad = {k: v for k, v in items if not (np.isfinite(v) and v <= tol)}
+    assert not bad, f"{what} over {tol:g} or non-finite: {bad}"
 
 
 def flow_from_fixture(inp, device="cuda"):

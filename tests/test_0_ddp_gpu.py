@@ -18,6 +18,8 @@ import sys
 import numpy as np
 import pytest
 
+from _fixtures import rel_err
+
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 TOL = 1e-6
@@ -58,7 +60,7 @@ def test_ddp_two_ranks_average_the_hip_gradients(tmp_path):
         want = (z[0][f"local0_{i}"] + z[0][f"local1_{i}"]) / 2
         for r in range(2):
             got = z[r][f"ddp_{i}"]
-            err = float(np.max(np.abs(got - want)) / max(np.max(np.abs(want)), 1e-30))
+            err = rel_err(got, want)      # raises on NaN / inf
             worst = max(worst, err)
             assert err <= TOL, (i, r, err)
         np.testing.assert_array_equal(z[0][f"ddp_{i}"], z[1][f"ddp_{i}"])

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 import torch
 
-from _fixtures import load, flow_from_fixture, rel_err
+from _fixtures import load, flow_from_fixture, rel_err, assert_all_within
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -165,7 +165,7 @@ def test_in_kernel_normals_match_explicit_philox_noise():
     errs = {k: rel_err(a[k], b[k]) for k in a}
     errs["ldj"] = abs(la - lb) / abs(lb)
     print("in-kernel vs explicit Philox normals:", errs)
-    assert all(v < 1e-6 for v in errs.values()), errs
+    assert_all_within(errs, 1e-6)
     z = philox_normal(1, 0, 1 << 16)
     assert abs(z.mean()) < 0.02 and abs(z.var() - 1) < 0.02
 

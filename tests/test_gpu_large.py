@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from oracle import enflow_oracle as O
-from _fixtures import rel_err
+from _fixtures import rel_err, normwise, worst_of, assert_all_within
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-5
@@ -87,7 +87,7 @@ def test_large_flow_forward_and_roundtrip(prec):
     errs = {k: rel_err(getattr(back, k).cpu().numpy(), rback[k]) for k in ("g", "pos", "vel")}
     print(f"256-atom chains {prec} reverse vs oracle (same fp32 inputs):",
           {k: f"{v:.2e}" for k, v in errs.items()})
-    assert all(v < TOL for v in errs.values()), errs
+    assert_all_within(errs, TOL)
     assert rel_err(back.vel.cpu().numpy(), b["vel"]) < 1e-4      # round trip
 
 
@@ -109,9 +109,86 @@ def test_training_past_64_atoms_vs_oracle():
     dq = {k: v.detach().double().cpu().numpy() for k, v in model.dequantize.named_parameters()}
     rloss, _, gl, gd, _ = OG.train_loss_and_grads(layers, dq, b, eps.astype(np.float64), model.dt, 1.0, 0.1)
     assert abs(float(loss) - rloss) <= 1e-5 * abs(rloss)
-    nw = lambda a, r: float(np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-300))  # noqa: E731
+    nw = normwise
     errs = {f"p{i}.{k}": nw(p.grad.cpu().double().numpy(), gl[i][k])
             for i, n in enumerate(model.networks) for k, p in n.named_parameters()}
     errs.update({f"dq.{k}": nw(p.grad.cpu().double().numpy(), gd[k]) for k, p in model.dequantize.named_parameters()})
-    print("100+22-atom training: max normwise grad err", f"{max(errs.values()):.2e}")
-    assert max(errs.values()) <= 1e-4, {k: v for k, v in errs.items() if v > 1e-4}
+    print("100+22-atom training: max normwise grad err", f"{worst_of(errs):.2e}")
+    assert_all_within(errs, 1e-4)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configs[4] at its stated size: 512 x 256-atom chains, 16 layers, H=128
+# ---------------------------------------------------------------------------
+CHAIN_SAMPLE = [0, 255, 511]
+
+
+@pytest.fixture(scope="module")
+def chain_run():
+    from enflow_amd.data import Data
+    b = _batch([256] * 512, 4000)
+    model = _model(128, 5, 16, 4001)
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(4002))
+    with torch.no_grad():
+        o1, l1 = model(d.clone(), noise=noise)
+        o2, l2 = model(d.clone(), noise=noise)
+    return b, model, noise, (o1, l1), (o2, l2)
+
+
+def _chain_sub(b, m):
+    a0, a1 = int(b["mol_ptr"][m]), int(b["mol_ptr"][m + 1])
+    sub = {k: b[k][a0:a1] for k in ("h", "g", "pos", "vel", "box")}
+    sub["r_cut"] = b["r_cut"][m:m + 1]
+    sub["mol_ptr"] = np.array([0, a1 - a0])
+    return sub, a0, a1
+
+
+def test_configs4_chains_full_batch_deterministic(chain_run):
+    _, _, _, (o1, l1), (o2, l2) = chain_run
+    for k in ("h", "g", "pos", "vel"):
+        assert torch.equal(getattr(o1, k), getattr(o2, k)), k
+    assert torch.equal(l1, l2) and np.isfinite(float(l1))
+
+
+def test_configs4_chains_sampled_vs_oracle(chain_run):
+    """16 accumulated layers: sampled chains of the full-batch run against the
+    float64 oracle forward on the same inputs, then the oracle reverse of the
+    HIP forward's float32 output against the HIP reverse of the whole batch."""
+    b, model, noise, (o1, _), _ = chain_run
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    dq = {k: v.detach().cpu().double().numpy() for k, v in model.dequantize.state_dict().items()}
+    with torch.no_grad():
+        back = model.reverse(o1.clone())
+    fwd, rev = {}, {}
+    for m in CHAIN_SAMPLE:
+        sub, a0, a1 = _chain_sub(b, m)
+        ref, ref_ldj = O.lf_forward(layers, dq, sub, noise[a0:a1].cpu().double().numpy(), model.dt)
+        for k in ("h", "g", "pos", "vel"):
+            fwd[f"{m}.{k}"] = rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k])
+        st = {k: getattr(o1, k)[a0:a1].cpu().double().numpy() for k in ("h", "g", "pos", "vel")}
+        st.update(box=sub["box"], r_cut=sub["r_cut"], mol_ptr=sub["mol_ptr"])
+        rb = O.lf_reverse(layers, st, model.dt)
+        np.testing.assert_array_equal(back.h[a0:a1].cpu().numpy(), rb["h"])
+        for k in ("g", "pos", "vel"):
+            rev[f"{m}.{k}"] = rel_err(getattr(back, k)[a0:a1].cpu().numpy(), rb[k])
+    print(f"configs[4] 512 x 256 chains, 16 layers: forward vs oracle worst {worst_of(fwd):.2e}, "
+          f"reverse vs oracle worst {worst_of(rev):.2e} ({len(CHAIN_SAMPLE)} chains)")
+    assert_all_within(fwd, TOL, "forward")
+    assert_all_within(rev, TOL, "reverse")
+
+
+def test_configs4_chains_roundtrip(chain_run):
+    b, model, _, (o1, _), _ = chain_run
+    with torch.no_grad():
+        back = model.reverse(o1.clone())
+    np.testing.assert_array_equal(np.argmax(back.h.cpu().numpy(), 1), np.argmax(b["h"], 1))
+    errs = {k: rel_err(getattr(back, k).cpu().numpy(), b[k]) for k in ("g", "vel")}
+    dpos = O.apply_pbc(back.pos.cpu().numpy() - b["pos"], b["box"])
+    errs["pos"] = float(np.max(np.abs(dpos)) / np.max(np.abs(b["pos"])))
+    print("configs[4] round trip:", {k: f"{v:.2e}" for k, v in errs.items()})
+    # a round trip through 16 layers in fp32 amplifies the forward's roundoff
+    # (g the most: h is rebuilt from g at every layer); forward and reverse are
+    # each held to 1e-5 against the oracle above -- this is the property check
+    assert_all_within({k: errs[k] for k in ("pos", "vel")}, 1e-3)
+    assert_all_within({"g": errs["g"]}, 1e-2)

@@ -10,18 +10,12 @@ import numpy as np
 import pytest
 import torch
 
-from _fixtures import load, egcl_from_fixture, data_from_fixture, ARGMAX_KEYS
+from _fixtures import load, egcl_from_fixture, data_from_fixture, ARGMAX_KEYS, normwise, worst_of, assert_all_within
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 GRAD_TOL = 1e-4
 LOSS_TOL = 1e-5
-
-
-def normwise(a, b):
-    a = np.asarray(a, dtype=np.float64)
-    b = np.asarray(b, dtype=np.float64)
-    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -47,9 +41,9 @@ def test_egcl_backward_matches_reference(name):
             "pos": normwise(d.pos.grad.cpu().numpy(), ref["grad_pos"])}
     for k, p in net.named_parameters():
         errs[k] = normwise(p.grad.cpu().numpy(), ref[f"grad_p0.{k}"])
-    print(name, "max normwise grad err", f"{max(errs.values()):.2e}",
+    print(name, "max normwise grad err", f"{worst_of(errs):.2e}",
           {k: f"{v:.1e}" for k, v in errs.items() if v > 1e-6})
-    assert max(errs.values()) <= GRAD_TOL, errs
+    assert_all_within(errs, GRAD_TOL)
 
 
 def test_egcl_outputs_unchanged_by_autograd_path():
@@ -76,8 +70,8 @@ def test_argmax_backward_matches_reference():
     loss.backward()
     assert abs(float(loss) - float(ref["loss"])) <= LOSS_TOL * abs(float(ref["loss"]))
     errs = {k: normwise(p.grad.cpu().numpy(), ref[f"grad_dq.{k}"]) for k, p in am.named_parameters()}
-    print("argmax max normwise grad err", f"{max(errs.values()):.2e}")
-    assert max(errs.values()) <= GRAD_TOL, errs
+    print("argmax max normwise grad err", f"{worst_of(errs):.2e}")
+    assert_all_within(errs, GRAD_TOL)
 
 
 def test_egcl_training_loop_reduces_loss():
@@ -136,5 +130,5 @@ def test_egcl_backward_large_box_vs_oracle(hid, variants):
             "pos": normwise(d.pos.grad.cpu().numpy(), pos64.grad.numpy())}
     for k, p in net.named_parameters():
         errs[k] = normwise(p.grad.cpu().numpy(), P[k].grad.numpy())
-    print(f"EGCL 300-atom box H={hid} {sorted(variants)}: max normwise grad err {max(errs.values()):.2e}")
-    assert max(errs.values()) <= GRAD_TOL, errs
+    print(f"EGCL 300-atom box H={hid} {sorted(variants)}: max normwise grad err {worst_of(errs):.2e}")
+    assert_all_within(errs, GRAD_TOL)

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 from oracle import enflow_oracle as O
-from _fixtures import (load, layer_params, dequant_params, state, n_layers, rel_err,
+from _fixtures import (load, layer_params, dequant_params, state, n_layers, rel_err, scalar_rel, worst_of, assert_all_within,
                        flow_from_fixture, data_from_fixture, egcl_from_fixture, EGCL_KEYS, ARGMAX_KEYS)
 
 pytestmark = pytest.mark.gpu
@@ -114,7 +114,7 @@ def test_lf_forward_matches_reference(name, prec):
     nll = Alchemical_NLL(kBT=float(inp["kBT"]), softening=float(inp["softening"]))(o, ldj)
     errs["nll"] = abs(float(nll) - float(out["nll"])) / abs(float(out["nll"]))
     print(f"{name} {prec} forward vs reference golden:", fmt(errs))
-    assert all(v < TOL for v in errs.values()), errs
+    assert_all_within(errs, TOL)
 
 
 def _fixture_layers(inp):
@@ -148,8 +148,8 @@ def test_lf_reverse_matches_reference(name, prec):
     errs = {k: rel_err(getattr(back, k).cpu().numpy(), ref[k]) for k in ("g", "pos", "vel")}
     gold = {k: rel_err(getattr(back, k).cpu().numpy(), out["rev_" + k]) for k in ("g", "pos", "vel")}
     print(f"{name} {prec} reverse vs oracle(same fp32 inputs):", fmt(errs), "| vs golden:", fmt(gold))
-    assert all(v < TOL for v in errs.values()), errs
-    assert all(v < TOL for v in gold.values()), gold
+    assert_all_within(errs, TOL)
+    assert_all_within(gold, TOL)
 
 
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2"])
@@ -173,7 +173,7 @@ def test_lf_bf16_generate_and_forward(name):
     errs.update({"fwd_" + k: rel_err(getattr(o, k).cpu().numpy(), out[k]) for k in ("h", "g", "pos", "vel")})
     errs["fwd_ldj"] = abs(float(ldj) - float(out["ldj"])) / abs(float(out["ldj"]))
     print(f"{name} bf16 vs reference golden:", fmt(errs))
-    assert all(v < BF16_TOL for v in errs.values()), errs
+    assert_all_within(errs, BF16_TOL)
 
 
 def _oracle_flow(model, batch, noise):
@@ -248,7 +248,7 @@ def test_floor_dequant_vs_oracle():
     ref, ref_ldj = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
     errs = {k: rel_err(getattr(o, k).cpu().numpy(), ref[k]) for k in ("h", "g", "pos", "vel")}
     print("floor forward vs oracle:", fmt(errs))
-    assert all(v < TOL for v in errs.values()), errs
+    assert_all_within(errs, TOL)
     assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
     with torch.no_grad():
         back = model.reverse(o.clone())
@@ -325,9 +325,9 @@ def test_bench_config_sampled_molecules_vs_oracle(bench_run):
         sub, a0, a1 = _sub(b, m)
         ref, _ = _oracle_flow(model, sub, noise[a0:a1])
         for k in worst:
-            worst[k] = max(worst[k], rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k]))
+            worst[k] = worst_of([worst[k], rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k])])
     print(f"bench config forward, {len(SAMPLE)} molecules vs oracle:", fmt(worst))
-    assert all(v < TOL for v in worst.values()), worst
+    assert_all_within(worst, TOL)
 
 
 def test_bench_config_reverse_vs_oracle(bench_run):
@@ -346,9 +346,9 @@ def test_bench_config_reverse_vs_oracle(bench_run):
         ref = O.lf_reverse(layers, st, model.dt)
         np.testing.assert_array_equal(np.argmax(back.h[a0:a1].cpu().numpy(), 1), np.argmax(ref["h"], 1))
         for k in worst:
-            worst[k] = max(worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k]))
+            worst[k] = worst_of([worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k])])
     print(f"bench config reverse, {len(SAMPLE)} molecules vs oracle:", fmt(worst))
-    assert all(v < TOL for v in worst.values()), worst
+    assert_all_within(worst, TOL)
 
 
 BF16_L8_TOL = 1e-4     # bf16 generate at 8 layers (configs[2]), normwise per tensor; measured 2.6e-5 (r02a)
@@ -378,9 +378,9 @@ def test_bf16_generate_8_layers_vs_oracle():
         ref = O.lf_reverse(layers, st, model.dt)
         np.testing.assert_array_equal(np.argmax(back.h[a0:a1].cpu().numpy(), 1), np.argmax(ref["h"], 1))
         for k in worst:
-            worst[k] = max(worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k]))
+            worst[k] = worst_of([worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k])])
     print(f"bf16 generate 8 layers, {len(SAMPLE[::2])} molecules vs oracle:", fmt(worst), f"(bar {BF16_L8_TOL:g})")
-    assert all(v < BF16_L8_TOL for v in worst.values()), worst
+    assert_all_within(worst, BF16_L8_TOL)
 
 
 def test_bench_config_roundtrip(bench_run):
@@ -420,14 +420,28 @@ def test_few_images_error_semantics(tag):
         assert np.isfinite(float(ldj))
 
 
+def test_grad_enabled_forward_raises_index_error_at_forward():
+    """The reference's generate() calls the model with autograd on and no
+    backward (enflow/main.py:275): the IndexError must surface at the call."""
+    from enflow_amd import _lib
+    _lib.check_pending()
+    inp, _ = load("edges_fewimg_raise")
+    model = _make_model(32, 5, 2, 3, 0.01)
+    assert torch.is_grad_enabled() and model.training
+    with pytest.raises(IndexError):
+        model(data_from_fixture(inp, DEV))
+    assert not _lib._pending
+
+
 def test_training_forward_defers_the_index_error_to_backward():
-    """Training: the forward queues its error word (no host sync); the
-    reference's IndexError surfaces when loss.backward() starts."""
+    """defer_error_check=True: the forward queues its error word (no host
+    sync); the reference's IndexError surfaces when loss.backward() starts."""
     from enflow_amd.flow import Alchemical_NLL
     from enflow_amd import _lib
     _lib.check_pending()
     inp, _ = load("edges_fewimg_raise")
     model = _make_model(32, 5, 2, 3, 0.01)
+    model.defer_error_check = True
     o, ldj = model(data_from_fixture(inp, DEV))            # grad enabled: training path, no raise
     loss = Alchemical_NLL(kBT=1.0, softening=0.1)(o, ldj)
     with pytest.raises(IndexError):
@@ -436,32 +450,109 @@ def test_training_forward_defers_the_index_error_to_backward():
     assert not _lib._pending
 
 
-@pytest.mark.parametrize("scale", [3e4, 1e6])
-def test_f16x3_range_guard(scale):
-    """Features scaled so the hidden activations pass the fp16 range (65504):
-    the f16x3 path must either raise FloatingPointError (ENFLOW_ERR_RANGE) or
-    return the oracle's result; the f32 path returns the oracle's result."""
+def _range_model_and_batch(scale):
+    """4 x 22-atom molecules whose Floor-dequantised features reach `scale`;
+    layer 0 default flags with coord_nn.2 x300 (|coord_diff * phi| passes the
+    +-100 clamp of egcl.py:72 on 20 % (3e4) / 96 % (1e6) of the pairs), layer 1
+    tanh=True (egcl.py:40-41).  vel_scaling_nn.2 is zeroed (bias 0.01) so that
+    Q, exp(Q) and log|detJ| stay finite: the float64 reference output is finite
+    everywhere (checked below) while the edge MLP's hidden activations reach
+    3.9e4 / 1.3e6, i.e. past the fp16 range (65504) at 1e6."""
     from enflow_amd.nn import EGCL, Floor
     from enflow_amd.flow import LFIntegrator
-    from enflow_amd.data import Data
     from enflow_amd.data.synthetic import make_molecules, default_dt
     b = _f32(make_molecules(4, 22, nf=4, seed=13))
     b["h"] = np.floor(np.random.default_rng(14).uniform(0, scale, size=b["h"].shape)).astype(np.float32).astype(np.float64)
     torch.manual_seed(15)
-    model = LFIntegrator([EGCL(4, 4, 64) for _ in range(2)], Floor(), dt=default_dt()).to(DEV)
+    nets = [EGCL(4, 4, 64), EGCL(4, 4, 64, tanh=True)]
+    with torch.no_grad():
+        for n in nets:
+            n.vel_scaling_nn[2].weight.zero_()
+            n.vel_scaling_nn[2].bias.fill_(0.01)
+            n.coord_nn[2].weight.mul_(300.0)
+    model = LFIntegrator(nets, Floor(), dt=default_dt()).to(DEV)
     u = torch.rand(b["h"].shape, device=DEV, generator=torch.Generator(DEV).manual_seed(16))
-    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
-    ref, _ = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
+    layers = []
+    for n in model.networks:
+        p = {k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()}
+        p["flags"] = (False, False, bool(n.tanh))
+        layers.append(p)
+    ref, ref_ldj = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
+    for k in ("h", "g", "pos", "vel"):
+        assert np.isfinite(ref[k]).all(), k        # the reference itself is finite here
+    return model, b, u, ref, ref_ldj
+
+
+@pytest.mark.parametrize("scale", [3e4, 1e6])
+def test_f16x3_range_guard(scale):
+    """Features past the fp16 range, finite reference (see _range_model_and_batch).
+    * gemm_precision f32: the oracle's result at 1e-5 on h, g, pos, vel and ldj.
+    * the raw f16x3 launch (forward_buffers) either flags ENFLOW_ERR_RANGE or
+      returns the oracle's result -- never a finite wrong one (the clamp and
+      the tanh layer would squash an overflowed phi to a finite value: the
+      kernel tests phi before them).  Both scales overflow somewhere (at 3e4
+      the edge activations fit fp16, 3.9e4, but the node MLP's message sums
+      do not), so the flag must be raised at both.
+    * the default (f16x3) module call returns the oracle's result: on the flag
+      it re-runs the launch with fp32 GEMMs."""
+    from enflow_amd import _lib
+    from enflow_amd.data import Data
+    model, b, u, ref, ref_ldj = _range_model_and_batch(scale)
     outcome = {}
-    for prec in ("f16x3", "f32"):
+    for prec in ("f32", "f16x3"):
         model.gemm_precision = prec
-        try:
-            with torch.no_grad():
-                o, _ = model(Data.from_arrays(b, device=DEV), noise=u)
-            errs = {k: rel_err(getattr(o, k).cpu().numpy(), ref[k]) for k in ("h", "g", "pos", "vel")}
-            outcome[prec] = ("result", max(errs.values()))
-        except FloatingPointError as e:
-            outcome[prec] = ("raised", str(e)[:60])
-    print(f"range guard, features up to {scale:g}:", outcome)
-    assert outcome["f32"][0] == "result" and outcome["f32"][1] < TOL, outcome
-    assert outcome["f16x3"][0] == "raised" or outcome["f16x3"][1] < TOL, outcome
+        with torch.no_grad():
+            o, ldj = model(Data.from_arrays(b, device=DEV), noise=u)
+        errs = {k: rel_err(getattr(o, k).cpu().numpy(), ref[k]) for k in ("h", "g", "pos", "vel")}
+        errs["ldj"] = scalar_rel(ldj, ref_ldj)
+        outcome[prec] = errs
+        print(f"range guard {scale:g}, module call {prec}:", fmt(errs))
+        assert_all_within(errs, TOL, f"{prec} vs oracle")
+    # the raw split-precision launch, no retry
+    model.gemm_precision = "f16x3"
+    s = model._state(Data.from_arrays(b, device=DEV))
+    M = s["mol_ptr"].numel() - 1
+    ldj_mol = torch.empty(M, device=DEV)
+    ldj = torch.empty(1, device=DEV)
+    st = torch.zeros(2, dtype=torch.int32, device=DEV)
+    with torch.no_grad():
+        model.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"], s["max_n"],
+                              u, ldj_mol, ldj, st[:1], src=s["src"], ticket=st[1:])
+    flagged = bool(int(st[0].item()) & _lib.ERR_RANGE)
+    raw = {k: rel_err(s[k].cpu().numpy(), ref[k], allow_nonfinite=True) for k in ("h", "g", "pos", "vel")}
+    print(f"range guard {scale:g}, raw f16x3 launch: flagged={flagged}", fmt(raw))
+    assert flagged, "fp16 overflow not flagged"
+
+
+def test_clamp_propagates_nan_like_torch():
+    """torch.clamp(NaN) is NaN (egcl.py:72): one NaN feature must reach the
+    same outputs as in the reference -- through the messages of its pairs into
+    G (h, g) and through phi and the clamp into F (vel, pos) of every row
+    atom paired with it -- not be clamped to +-100.  One layer: past it the
+    NaN positions would also enter the neighbour search."""
+    from enflow_amd.nn import Floor
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    model2, b, u, _, _ = _range_model_and_batch(3e4)
+    model = LFIntegrator([model2.networks[0]], Floor(), dt=model2.dt).to(DEV)
+    b = dict(b)
+    b["h"] = b["h"].copy()
+    row, _, _ = O.batch_edges(b["pos"], b["box"], b["r_cut"], b["mol_ptr"])
+    a_nan = int(np.bincount(row).argmax())          # the atom with the most edges
+    b["h"][a_nan, 1] = np.nan
+    model.gemm_precision = "f32"
+    with torch.no_grad():
+        o, _ = model(Data.from_arrays(b, device=DEV), noise=u)
+    layers = []
+    for n in model.networks:
+        p = {k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()}
+        p["flags"] = (False, False, bool(n.tanh))
+        layers.append(p)
+    with np.errstate(all="ignore"):
+        ref, _ = O.lf_forward(layers, 1.0, b, u.cpu().double().numpy(), model.dt, dequant_kind="floor")
+    for k in ("h", "g", "pos", "vel"):
+        got = getattr(o, k).cpu().numpy()
+        np.testing.assert_array_equal(np.isnan(got), np.isnan(ref[k]), err_msg=k)
+        fin = ~np.isnan(ref[k])
+        assert rel_err(got[fin], ref[k][fin]) < TOL, k
+    assert np.isnan(o.vel.cpu().numpy()).any(axis=1).sum() > 1      # F of the NaN atom's partners too

@@ -16,18 +16,13 @@ import numpy as np
 import pytest
 import torch
 
-from _fixtures import load, flow_from_fixture, layer_params, dequant_params, state, n_layers
+from _fixtures import (load, flow_from_fixture, layer_params, dequant_params, state, n_layers, normwise, worst_of,
+                       assert_all_within)
 
 pytestmark = pytest.mark.gpu
 
 GRAD_TOL = 1e-4
 LOSS_TOL = 1e-5
-
-
-def normwise(a, b):
-    a = np.asarray(a, dtype=np.float64)
-    b = np.asarray(b, dtype=np.float64)
-    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
 def _train_step(model, data, eps, kBT, softening):
@@ -58,7 +53,7 @@ def test_training_gradients_match_reference(name):
     for k, p in model.dequantize.named_parameters():
         worst[f"dq.{k}"] = normwise(p.grad.cpu().numpy(), ref[f"grad_dq.{k}"])
     bad = {k: v for k, v in worst.items() if not v <= GRAD_TOL}
-    print(name, "max normwise grad err", max(worst.values()))
+    print(name, "max normwise grad err", worst_of(worst))
     assert not bad, bad
 
 
@@ -95,7 +90,7 @@ def test_training_gradients_bench_shape_vs_oracle(sizes):
             errs[f"p{i}.{k}"] = normwise(p.grad.cpu().numpy(), gl[i][k])
     for k, p in model.dequantize.named_parameters():
         errs[f"dq.{k}"] = normwise(p.grad.cpu().numpy(), gd[k])
-    print("bench-shape max normwise grad err", max(errs.values()))
+    print("bench-shape max normwise grad err", worst_of(errs))
     bad = {k: v for k, v in errs.items() if not v <= GRAD_TOL}
     assert not bad, bad
 
@@ -184,8 +179,8 @@ def test_training_through_all_egcl_variants_vs_oracle():
     for i, net in enumerate(model.networks):
         for k, p in net.named_parameters():
             worst[f"p{i}.{k}"] = normwise(p.grad.cpu().numpy(), gl[i][k])
-    print("variants max normwise grad err", max(worst.values()))
-    assert max(worst.values()) <= GRAD_TOL, {k: v for k, v in worst.items() if v > GRAD_TOL}
+    print("variants max normwise grad err", worst_of(worst))
+    assert_all_within(worst, GRAD_TOL)
 
 
 def test_backward_error_word_is_deferred_then_checked():
@@ -230,3 +225,84 @@ def test_training_gradients_bitwise_reproducible_bench_scale():
     for g in grads[1:]:
         for a, b_ in zip(grads[0], g):
             assert torch.equal(a, b_)
+
+
+def test_inplace_parameter_change_between_forward_and_backward_raises():
+    """The backward runs on the weights packed at forward time; a parameter
+    changed in place in between makes it refuse (torch autograd reports a
+    version mismatch in that case) instead of mixing old tape / new weights."""
+    from enflow_amd.flow import Alchemical_NLL
+    inp, _ = load("train_h32_L3")
+    model, data = flow_from_fixture(inp, "cuda")
+    out, ldj = model(data, noise=torch.tensor(inp["eps"], device="cuda"))
+    loss = Alchemical_NLL(kBT=float(inp["kBT"]), softening=float(inp["softening"]))(out, ldj)
+    with torch.no_grad():
+        model.networks[1].edge_nn[0].weight.mul_(1.01)
+    with pytest.raises(RuntimeError, match="modified in place"):
+        loss.backward()
+
+
+def test_configs3_training_step_1024x64_8_layers():
+    """BASELINE configs[3] per GPU at its stated size: 1024 x 64-atom molecules,
+    8 layers, H=128, one loss.backward().  The NLL is a sum over molecules
+    divided by their number (enflow/flow/loss.py:21-25), so the full batch's
+    gradient equals the molecule-weighted sum of the gradients of any partition
+    into sub-batches (same noise).  Checked on the partition [4, 124, 7 x 128]:
+    full vs weighted sum normwise <= SPLIT_TOL, and the 4-molecule sub-batch vs
+    the float64 gradient oracle at GRAD_TOL (the oracle is pinned to the
+    reference's loss.backward() by the train_* goldens)."""
+    from oracle import enflow_oracle_grad as OG
+    from enflow_amd.data.synthetic import make_molecules, default_dt, default_kBT
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    SPLIT_TOL = 1e-5
+    nf, hid, nl, M = 5, 128, 8, 1024
+    b = make_molecules(M, 64, nf=nf, seed=3000, radius=4.0 * (64 / 22.0) ** (1.0 / 3.0))
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        b[k] = b[k].astype(np.float32).astype(np.float64)
+    torch.manual_seed(3001)
+    model = LFIntegrator([EGCL(nf, nf, hid) for _ in range(nl)], ArgMax(nf, hid), dt=default_dt()).cuda()
+    eps = np.random.default_rng(3002).normal(size=b["h"].shape).astype(np.float32)
+    kBT = default_kBT()
+    params = list(model.parameters())
+    names = [f"p{i}.{k}" for i, n in enumerate(model.networks) for k, _ in n.named_parameters()] + \
+            [f"dq.{k}" for k, _ in model.dequantize.named_parameters()]
+
+    def step(lo, hi):
+        a0, a1 = int(b["mol_ptr"][lo]), int(b["mol_ptr"][hi])
+        sub = {k: b[k][a0:a1] for k in ("h", "g", "pos", "vel", "box")}
+        sub["r_cut"] = b["r_cut"][lo:hi]
+        sub["mol_ptr"] = b["mol_ptr"][lo:hi + 1] - b["mol_ptr"][lo]
+        loss, _ = _train_step(model, Data.from_arrays(sub, device="cuda"),
+                              torch.tensor(eps[a0:a1], device="cuda"), kBT, 0.1)
+        return sub, float(loss), [p.grad.double().cpu().numpy() for p in params]
+
+    _, loss_full, g_full = step(0, M)
+    cuts = [0, 4, 128] + list(range(256, M + 1, 128))
+    acc = [np.zeros_like(g) for g in g_full]
+    loss_sum = 0.0
+    sub4 = None
+    for lo, hi in zip(cuts[:-1], cuts[1:]):
+        sub, loss, g = step(lo, hi)
+        w = (hi - lo) / M
+        loss_sum += w * loss
+        for a, gk in zip(acc, g):
+            a += w * gk
+        if lo == 0:
+            sub4, g4, loss4 = sub, g, loss
+    split = {n: normwise(gf, a) for n, gf, a in zip(names, g_full, acc)}
+    print(f"configs[3] 1024 x 64, 8 layers: full vs weighted sub-batch gradients worst {worst_of(split):.2e}; "
+          f"loss {loss_full:.6e} vs {loss_sum:.6e}")
+    assert abs(loss_full - loss_sum) <= 1e-5 * abs(loss_full)
+    assert_all_within(split, SPLIT_TOL, "full vs sub-batch sum")
+    layers = [{k: v.detach().double().cpu().numpy() for k, v in n.named_parameters()} for n in model.networks]
+    dq = {k: v.detach().double().cpu().numpy() for k, v in model.dequantize.named_parameters()}
+    rloss, _, gl, gd, _ = OG.train_loss_and_grads(layers, dq, sub4, eps[:int(b["mol_ptr"][4])].astype(np.float64),
+                                                  default_dt(), kBT, 0.1)
+    assert abs(loss4 - rloss) <= LOSS_TOL * abs(rloss), (loss4, rloss)
+    ref = [gl[i][k] for i, n in enumerate(model.networks) for k, _ in n.named_parameters()] + \
+          [gd[k] for k, _ in model.dequantize.named_parameters()]
+    oerr = {n: normwise(g, r) for n, g, r in zip(names, g4, ref)}
+    print(f"configs[3] 4-molecule sub-batch vs gradient oracle worst {worst_of(oerr):.2e}")
+    assert_all_within(oerr, GRAD_TOL, "sub-batch vs oracle")

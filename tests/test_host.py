@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 8
+    assert L.enflow_abi_version() == 9
     assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):

@@ -3,7 +3,8 @@ extra -D defines / hipcc flags, linked with the product build's other objects.
 
     python tools/build_variant.py NAME [--tu backward] [-DFOO=1 | -fflag ...]   ->  enflow_amd/var/libenflow_NAME.so
 
---tu backward recompiles enflow_backward.hip instead (the training kernels).
+--tu NAME recompiles enflow_NAME.hip instead (backward: the training kernels, latency: the
+8-wave flow instances).
 """
 import os
 import subprocess
@@ -16,15 +17,15 @@ LIB = os.path.join(ROOT, "enflow_amd", "libenflow_hip.so")
 def main():
     name, flags = sys.argv[1], sys.argv[2:]
     tu = "enflow_flow.hip"
-    if flags[:2] == ["--tu", "backward"]:
-        tu, flags = "enflow_backward.hip", flags[2:]
+    if flags[:1] == ["--tu"]:
+        tu, flags = f"enflow_{flags[1]}.hip", flags[2:]
     out_dir = os.path.join(ROOT, "enflow_amd", "var")
     os.makedirs(out_dir, exist_ok=True)
     obj = os.path.join(out_dir, f"{tu.split('.')[0]}_{name}.o")
     base = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include")]
     subprocess.run(base + flags + ["-c", os.path.join(ROOT, "enflow_amd", "csrc", tu), "-o", obj], check=True)
     others = [LIB + "." + s + ".o" for s in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip",
-                                            "enflow_timing.hip") if s != tu]
+                                            "enflow_timing.hip", "enflow_latency.hip") if s != tu]
     so = os.path.join(out_dir, f"libenflow_{name}.so")
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, obj] + others, check=True)
     print(so)

@@ -22,19 +22,27 @@ def main():
     model.gemm_precision = "f16x3"
     g = make_molecules(1024, bench.ATOMS, nf=bench.NF, seed=1000)
     out = {"workload": bench.workload_name("forward"), "rows": []}
+    from enflow_amd import _lib
+    L = _lib.lib()
+    out["latency_threshold_auto"] = L.enflow_latency_threshold()
     t1 = None
     for n in (1, 2, 4, 8):
         m1 = 1024 // n
-        run = bench.FlowRunner(model, bench.batch_tensors(bench.sub_batch(g, 0, m1), dev), bench.ATOMS, False, dev,
-                               torch.Generator(dev).manual_seed(0))
-        el = bench.timed(run.step, 40, 30, None, dev)
-        run.check()
-        ms = el / 40 * 1e3
-        t1 = ms if n == 1 else t1
-        out["rows"].append({"ranks": n, "molecules_per_rank": m1, "workgroups": m1, "ms_per_step": ms,
-                            "global_molecule_transforms_per_s": 1024 / (ms * 1e-3),
-                            "strong_scaling_efficiency": t1 / (n * ms)})
-        print(json.dumps(out["rows"][-1]), file=sys.stderr, flush=True)
+        for mode, thr in (("auto", -1), ("4-wave only", 0)):
+            L.enflow_set_latency_threshold(thr)
+            run = bench.FlowRunner(model, bench.batch_tensors(bench.sub_batch(g, 0, m1), dev), bench.ATOMS, False,
+                                   dev, torch.Generator(dev).manual_seed(0))
+            el = bench.timed(run.step, 40, 30, None, dev)
+            run.check()
+            ms = el / 40 * 1e3
+            if n == 1 and mode == "auto":
+                t1 = ms
+            out["rows"].append({"ranks": n, "kernel": mode, "molecules_per_rank": m1,
+                                "latency_instance": m1 <= L.enflow_latency_threshold(), "ms_per_step": ms,
+                                "global_molecule_transforms_per_s": 1024 / (ms * 1e-3),
+                                "strong_scaling_efficiency": t1 / (n * ms)})
+            print(json.dumps(out["rows"][-1]), file=sys.stderr, flush=True)
+    L.enflow_set_latency_threshold(-1)
     print(json.dumps(out, indent=1))
 
 
