@@ -510,6 +510,7 @@ def run_train(args, world, rank, local, device, dist):
     if dist:
         from torch.nn.parallel import DistributedDataParallel as DDP
         net = DDP(model, device_ids=[local])      # main.py:159; backend nccl = RCCL
+    model.defer_error_check = not args.sync_errors
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     nll = Alchemical_NLL(kBT=default_kBT(), softening=0.1)
     base = Data.from_arrays(b, device=device)
@@ -661,6 +662,7 @@ def run_lj_train(args, world, rank, local, device, dist):
     if dist:
         from torch.nn.parallel import DistributedDataParallel as DDP
         net = DDP(model, device_ids=[local])
+    model.defer_error_check = not args.sync_errors
     opt = torch.optim.Adam(model.parameters(), lr=1e-5)
     nll = Alchemical_NLL(kBT=default_kBT(), softening=0.1)
     base = Data.from_arrays(b, device=device)
@@ -717,6 +719,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=30,
                     help="untimed steps first: the first ~20 launches run while the clock ramps up")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--sync-errors", action="store_true",
+                    help="train / lj_train: read the forward's error word before the forward returns (the module "
+                         "default, LFIntegrator.defer_error_check = False) instead of at the start of "
+                         "loss.backward(), which the reference's loop body calls right after (main.py:219-221)")
     ap.add_argument("--cpu-per-core", type=int, default=192,
                     help="cpu_baseline sample: molecules per host core (16 cores: ~15 s)")
     ap.add_argument("--cpu-baseline-only", action="store_true", help=argparse.SUPPRESS)

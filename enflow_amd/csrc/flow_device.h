@@ -17,6 +17,10 @@
 #endif
 #define BLOCK (64 * WAVES)
 #define NFMAX 8
+#ifndef ENFLOW_MSG_LDS
+#define ENFLOW_MSG_LDS 0   // 1: message segment sums through a per-wave LDS scratch instead of DPP
+                           // scans (measured 10 % slower: the serial reduce exposes LDS latency)
+#endif
 #define NFP 9  // LDS row stride of h / g / G (odd -> conflict-free across atoms)
 #ifndef ENFLOW_WAVES_PER_SIMD
 #define ENFLOW_WAVES_PER_SIMD 2   // workgroups of 4 waves per CU (VGPR budget 256 / 168 for 2 / 3)
@@ -975,7 +979,7 @@ struct Smem {
   // <= 32-atom images (and the large-system row blocks): the edge tiles' message
   // segment sums go through a per-wave LDS scratch [32 pairs][MSP] in the union
   // (free during the tiles); other images scan in registers (seg_scan4x)
-  static constexpr bool MSG_LDS = !BWD && NMAX == 32 && RB == 32 ;
+  static constexpr bool MSG_LDS = ENFLOW_MSG_LDS && !BWD && NMAX == 32 && RB == 32;
   static constexpr int MSW = H < 64 ? H : 64;                         // features per reduce chunk
   static constexpr int MSP = MSW + 1;                                 // odd row stride: conflict-free
   union {
@@ -1326,12 +1330,13 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     };
     // segments = runs of equal row; invalid lanes get unique rows of their own
     const int row = valid ? il : -1 - j;
-    // segment masks: exact (EXEC) form with the LDS message path, else the
-    // multiplier form (its 0 * NaN can spread a NaN input to a neighbouring row)
-    SegExec SE;
+    // segment masks: the exact (EXEC) form for the forces -- phi feeds the
+    // clamp, whose NaN must stay NaN -- and the multiplier form for the message
+    // scans (1 VALU per value and step; its 0 * NaN can spread a NaN input to a
+    // neighbouring row of the same molecule, never turn it finite)
+    const SegExec SE = seg_exec(row);
     SegMasks SM;
-    if constexpr (MSG_LDS) SE = seg_exec(row);
-    else SM = seg_masks(row);
+    if constexpr (!MSG_LDS) SM = seg_masks(row);
     const int row_next = __shfl_down(row, 1, 32);
     const bool seg_end = valid && (j == 31 || row_next != row);
     float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? il : 0) * AST];
@@ -1548,8 +1553,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     float ty = c * clamp100(dy * nd * phi);
     float tz = c * clamp100(dz * nd * phi);
     float tw = 0.f;
-    if constexpr (MSG_LDS) seg_scan4x(tx, ty, tz, tw, SE);
-    else seg_scan4(tx, ty, tz, tw, SM);
+    seg_scan4x(tx, ty, tz, tw, SE);
     if (seg_end && hh == 0) *fslot = fold + (f32x4){tx, ty, tz, tw};
     STAMP(14);
   }

@@ -2,7 +2,9 @@
 
 Builds libenflow_hip_stamps.so (-DENFLOW_STAMPS, never shipped as the product
 library), runs the bench workload through it and prints the share of wave-0
-cycles spent in each phase.  Usage (GPU box): python tools/stamps.py
+cycles spent in each phase.  Usage (GPU box): python tools/stamps.py [MOLS]
+(MOLS molecules of the bench's 22-atom workload, default 1024; the 4-wave
+instance is forced, so e.g. 128 shows one molecule's latency chain per CU)
 """
 import ctypes
 import os
@@ -25,6 +27,7 @@ def main():
         build(force=True, out=SO, defines=["ENFLOW_STAMPS"])
     if len(sys.argv) > 1 and sys.argv[1] == "build":
         return
+    mols = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1024
     os.environ["ENFLOW_LIB"] = SO
     sys.path.insert(0, ROOT)
     import torch
@@ -33,13 +36,14 @@ def main():
     L = _lib.lib()
     L.enflow_read_stamps.restype = ctypes.c_int
     L.enflow_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.enflow_set_latency_threshold(0)      # the stamped instance is the 4-wave one
     dev = torch.device("cuda", 0)
     from enflow_amd.data.synthetic import make_molecules
     model = bench.build_model(dev, bench.LAYERS)
-    inp = bench.batch_tensors(make_molecules(bench.MOLS_PER_GPU, bench.ATOMS, nf=bench.NF, seed=1000), dev)
+    inp = bench.batch_tensors(make_molecules(mols, bench.ATOMS, nf=bench.NF, seed=1000), dev)
     work = {k: inp[k].clone() for k in ("h", "g", "pos", "vel")}
     noise = torch.randn_like(inp["h"])
-    ldj_mol = torch.empty(bench.MOLS_PER_GPU, device=dev)
+    ldj_mol = torch.empty(mols, device=dev)
     ldj = torch.empty(1, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     buf = (ctypes.c_ulonglong * 16)()
@@ -54,7 +58,8 @@ def main():
         L.enflow_read_stamps(buf, 1)
     tot = sum(buf)       # every stamp closes the interval since the previous one: disjoint
     for name, v in zip(PHASES, buf):
-        print(f"{name:12s} {100.0 * v / tot:6.2f} %   {v / bench.MOLS_PER_GPU:12.0f} cycles/WG")
+        print(f"{name:24s} {100.0 * v / tot:6.2f} %   {v / mols:12.0f} cycles/WG  "
+              f"{v / mols / bench.LAYERS:10.0f} cycles/WG/layer")
 
 
 if __name__ == "__main__":
