@@ -9,7 +9,14 @@ import os
 
 import torch
 
-LIB_PATH = os.environ.get("ENFLOW_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libenflow_hip.so")
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ENFLOW_LIB") or os.path.join(_HERE, "libenflow_hip.so")
+# the same sources built with -DENFLOW_NFMAX=16: node_nf 9..16 (training 9..15)
+LIB_NF16_PATH = os.environ.get("ENFLOW_LIB_NF16") or os.path.join(_HERE, "libenflow_hip_nf16.so")
+BASE_NFMAX = 8
+MAX_NODE_NF = 16
+# the backward's transposed edge_nn.0 GEMM has one 32-row output tile: 2 nf + 1 <= 32
+TRAIN_MAX_NODE_NF = 15
 
 ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2
@@ -88,7 +95,7 @@ SIGNATURES = {
     "enflow_timing_reset": (_i, []),
 }
 
-_lib = None
+_libs = {}
 
 
 class HipPathError(RuntimeError):
@@ -101,23 +108,35 @@ class RangeError(FloatingPointError):
     with fp32 GEMMs; the training path raises it."""
 
 
-def lib():
-    """Load (once) and return the ctypes handle; raise if it is unavailable."""
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib_path(nf=None):
+    """The library whose kernels hold `nf` node features: libenflow_hip.so up
+    to 8, libenflow_hip_nf16.so for 9..16."""
+    if nf is None or int(nf) <= BASE_NFMAX:
+        return LIB_PATH
+    if int(nf) <= MAX_NODE_NF:
+        return LIB_NF16_PATH
+    raise NotImplementedError(f"enflow_amd kernels are built for node_nf <= {MAX_NODE_NF} (got {nf})")
+
+
+def lib(nf=None):
+    """Load (once) and return the ctypes handle of the library for `nf` node
+    features (default: the 8-feature build); raise if it is unavailable."""
+    path = lib_path(nf)
+    handle = _libs.get(path)
+    if handle is None:
+        if not os.path.exists(path):
             raise HipPathError(
-                f"{LIB_PATH} is missing: build it with "
+                f"{path} is missing: build it with "
                 "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
-        handle = ctypes.CDLL(LIB_PATH)
+        handle = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
             if not hasattr(handle, name):    # an older build (A/B tools): calling it raises
                 continue
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
-        _lib = handle
-    return _lib
+        _libs[path] = handle
+    return handle
 
 
 def ptr(t):
@@ -159,7 +178,7 @@ def is_large(max_mol_atoms):
 def large_workspace(num_mols, num_atoms, max_mol_atoms, nf, device):
     """Device workspace of the large-system kernels (uint8, cached per device;
     grown on demand, never shrunk)."""
-    need = lib().enflow_lf_large_workspace_size(num_mols, num_atoms, int(max_mol_atoms), nf)
+    need = lib(nf).enflow_lf_large_workspace_size(num_mols, num_atoms, int(max_mol_atoms), nf)
     if need < 0:
         raise HipPathError("enflow_lf_large_workspace_size: bad arguments")
     key = str(device)
@@ -264,7 +283,7 @@ def _raise_code(e):
     if e & ERR_TOO_MANY_ATOMS:
         raise HipPathError(f"molecule larger than {lib().enflow_max_atoms()} atoms")
     if e & ERR_TOO_MANY_FEATURES:
-        raise HipPathError(f"node_nf larger than {lib().enflow_max_node_nf()}")
+        raise HipPathError(f"node_nf larger than the kernels' feature width (at most {MAX_NODE_NF})")
     if e & ERR_RANGE:
         raise RangeError("the split-precision (f16x3 / bf16) GEMMs produced a non-finite result: an "
                                  "operand is past the fp16 / bf16 range; run with gemm_precision='f32'")

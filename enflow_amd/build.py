@@ -14,11 +14,18 @@ OUT = os.path.join(HERE, "libenflow_hip.so")
 ARCH = os.environ.get("ENFLOW_OFFLOAD_ARCH", "gfx950")
 
 
-def build(force=False, verbose=False, out=OUT, defines=()):
-    """defines: extra -D flags (A/B and ablation variants built to another `out`)."""
+OUT_NF16 = os.path.join(HERE, "libenflow_hip_nf16.so")
+# the product libraries: (output, extra -D flags).  The 16-feature build is the
+# same sources with ENFLOW_NFMAX=16 (node_nf 9..16); the 8-feature build keeps
+# the smaller LDS images (two training workgroups per CU).
+VARIANTS = [(OUT, ()), (OUT_NF16, ("ENFLOW_NFMAX=16",))]
+
+
+def _start(force, verbose, out, defines):
+    """Start the out-of-date compiles of one library; returns (procs, finish)."""
     deps = SRCS + HDRS
     if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps):
-        return out
+        return [], lambda: None
     # one hipcc per source, in parallel, then one link
     base = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
             "-I", os.path.join(ROOT, "include"), *[f"-D{d}" for d in defines]]
@@ -28,26 +35,46 @@ def build(force=False, verbose=False, out=OUT, defines=()):
     stamp = out + ".flags"
     flags = " ".join(base)
     same_flags = os.path.exists(stamp) and open(stamp).read() == flags
-    hdrs = HDRS
     procs = []
     for src, obj in zip(SRCS, objs):
         if (not force and same_flags and os.path.exists(obj) and
-                all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in [src] + hdrs)):
+                all(os.path.getmtime(obj) >= os.path.getmtime(d) for d in [src] + HDRS)):
             continue
         cmd = base + ["-c", src, "-o", obj]
         if verbose:
             print(" ".join(cmd))
         procs.append(subprocess.Popen(cmd))
+
+    def finish():
+        with open(stamp, "w") as fh:
+            fh.write(flags)
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        os.replace(out + ".tmp", out)
+    return procs, finish
+
+
+def build(force=False, verbose=False, out=OUT, defines=()):
+    """One library (defines: extra -D flags; A/B and diagnostic variants are
+    built to another `out`)."""
+    procs, finish = _start(force, verbose, out, defines)
     if any(p.wait() != 0 for p in procs):
         raise subprocess.CalledProcessError(1, "hipcc")
-    with open(stamp, "w") as fh:
-        fh.write(flags)
-    cmd = ["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp"] + objs
-    if verbose:
-        print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    finish()
     return out
+
+
+def build_all(force=False, verbose=False):
+    """Every product library, all translation units compiled in parallel."""
+    jobs = [_start(force, verbose, out, defs) for out, defs in VARIANTS]
+    ok = all(p.wait() == 0 for procs, _ in jobs for p in procs)
+    if not ok:
+        raise subprocess.CalledProcessError(1, "hipcc")
+    for _, finish in jobs:
+        finish()
+    return [out for out, _ in VARIANTS]
 
 
 if __name__ == "__main__":
@@ -56,4 +83,4 @@ if __name__ == "__main__":
     if len(sys.argv) > 1:
         print(build(force=True, verbose=True, out=os.path.abspath(sys.argv[1]), defines=sys.argv[2:]))
     else:
-        print(build(force=True, verbose=True))
+        print(build_all(force=True, verbose=True))

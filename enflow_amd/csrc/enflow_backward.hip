@@ -186,8 +186,12 @@ struct BwdArgs {
   float* colc;                // [pair rows][CSTR] out
   long long prb;              // pair rows allocated
 };
-__host__ __device__ inline int xin_width(int nf) { return 2 * nf + 1 > 16 ? 32 : 16; }
-constexpr int CSTR = 12;      // colc row: d h_j [NFMAX], d pos_j [3], pad
+// edge_nn.0 input rows [h_i, h_j, radial]: 2 nf + 1 columns rounded up to 16
+__host__ __device__ inline int xin_width(int nf) { return (2 * nf + 1 + 15) & ~15; }
+constexpr int CSTR = NFMAX + 4;   // colc row: d h_j [NFMAX], d pos_j [3], pad
+// the transposed edge_nn.0 GEMM (d [h_i, h_j, radial]) has one 32-row output
+// tile: training needs 2 nf + 1 <= 32
+constexpr int BWD_NFMAX = NFMAX < 15 ? NFMAX : 15;
 
 // <= 80 KB at (H, NMAX) = (128, 64): two workgroups per CU.  The node-MLP
 // adjoint rows go through LDS a chunk of Smem::NBCH atoms at a time, in the
@@ -283,10 +287,10 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
     const int ac = va ? a : 0;
     f32x16 hin = (f32x16)0.f, gin = (f32x16)0.f;
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const bool on = va && hh == 0 && jj < nf;
-      hin[jj] = on ? sm.h[ac * NFP + jj] : 0.f;
-      gin[jj] = on ? sb.aG[ac * NFP + jj] : 0.f;
+    for (int jj = 0; jj < 8; ++jj) {   // k = feature 8 hh + jj (half 1: features 8..15)
+      const bool on = va && 8 * hh + jj < nf;
+      hin[jj] = on ? sm.h[ac * NFP + 8 * hh + jj] : 0.f;
+      gin[jj] = on ? sb.aG[ac * NFP + 8 * hh + jj] : 0.f;
     }
     f16x8 bh, bl;
     split_f16(hin, 0, bh, bl);
@@ -334,7 +338,7 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
         st4(B.an + row, an4);
       }
     }
-    // d h partial over this item's hidden units (rows f = rho(r, hh) < nf: r < 4)
+    // d h partial over this item's hidden units (rows f = rho(r, hh) < nf: r < NFMAX / 2)
     f32x16 tu[1] = {au}, tn[1] = {an};
     const float iu = tile_pow2_scale(tu), in = tile_pow2_scale(tn);
     f32x16 dv = (f32x16)0.f, dn = (f32x16)0.f;
@@ -347,8 +351,8 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
     }
     if (va) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = r + 4 * hh;
+      for (int r = 0; r < NFMAX / 2; ++r) {
+        const int q = rho(r, hh);
         if (q < nf) gp[(tp * NFMAX + q) * NMAX + a] = dv[r] * (inv_v1 * iu) + dn[r] * (inv_n1 * in);
       }
     }
@@ -467,7 +471,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     ma0 = a0;
     mn = n;
   }
-  if (n > NMAX || B.nf > NFMAX) {
+  if (n > NMAX || B.nf > BWD_NFMAX) {
     if (tid == 0) atomicOr(B.err, n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
     return;
   }
@@ -746,17 +750,24 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       const float radial = dx * dx + dy * dy + dz * dz;
 
       // X row of edge_nn.0: [h_i, h_j, radial]
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = 8 * hh + u;
+      auto xin_col = [&](int q) -> float {
         float v = 0.f;
         if (q < nf) v = sm.h[i * NFP + q];
         else if (q < 2 * nf) v = colh(q - nf);
         else if (q == 2 * nf) v = radial;
-        ST_OUT(rxin, (hh * 256 + j) * 4, gt * XW * 128 + u * 128, valid ? v : 0.f);
+        return valid ? v : 0.f;
+      };
+      if constexpr (NFMAX == 8) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) ST_OUT(rxin, (hh * 256 + j) * 4, gt * XW * 128 + u * 128, xin_col(8 * hh + u));
+        if (XW > 16 && hh == 0)   // q = 16 = 2 nf: the radial of an nf = 8 layer
+          ST_OUT(rxin, j * 4, gt * XW * 128 + 16 * 128, valid ? radial : 0.f);
+      } else {   // 16-column chunks, every column of the row written
+        for (int c16 = 0; c16 < XW / 16; ++c16)
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            ST_OUT(rxin, (hh * 256 + j) * 4, gt * XW * 128 + (16 * c16 + u) * 128, xin_col(16 * c16 + 8 * hh + u));
       }
-      if (XW > 16 && hh == 0)   // q = 16 = 2 nf: the radial of an nf = 8 layer
-        ST_OUT(rxin, j * 4, gt * XW * 128 + 16 * 128, valid ? radial : 0.f);
 
       // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1.  Run twice per
       // tile (here, and again for silu'(pre0) after GEMM4) instead of parking pre0
@@ -766,28 +777,29 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
       if constexpr (PREC == PREC_F16X3) {
-        const int ks_n = gemm0_ksteps(nf);
+        const int ks_n = gemm0_ksteps(nf), nch = gemm0_nch(nf);
         // the first k-step's fragments requested before the operand build, so
         // their L2 round trip overlaps it (they are the only loads the chain waits on)
         f32x4 fh0[NT], fl0[NT];
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const int so = (L.we1x + (t * 2) * 512) * 4;
+          const int so = (L.we1x + (t * KS0MAX) * 512) * 4;
           fh0[t] = bload4(W, lane * 32, so);
           fl0[t] = bload4(W, lane * 32 + 16, so);
         }
         for (int ks = 0; ks < ks_n; ++ks) {   // k order gemm0_col (as the forward)
           f32x16 in;
-          if (ks == 0) {
+          if (ks < nch) {
+            const int f0 = 8 * ks;
             if (BIG && hh) {
 #pragma unroll
-              for (int jj = 0; jj < 8; ++jj) in[jj] = jj < nf ? colh(jj) : 0.f;
+              for (int jj = 0; jj < 8; ++jj) in[jj] = f0 + jj < nf ? colh(f0 + jj) : 0.f;
             } else {
-              const float* hrow = &sm.h[(hh ? jl : i) * NFP];   // rows zero-padded past nf
+              const float* hrow = &sm.h[(hh ? jl : i) * NFP + f0];   // rows zero-padded past nf
 #pragma unroll
               for (int jj = 0; jj < 8; ++jj) in[jj] = hrow[jj];
             }
-            if (hh && nf <= 7) in[7] = radial;
+            if (hh && ks == nch - 1 && gemm0_radial_slot7(nf)) in[7] = radial;
           } else {
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) in[jj] = 0.f;
@@ -799,7 +811,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           for (int t = 0; t < NT; ++t) {
             f32x4 ah = fh0[t], al = fl0[t];
             if (ks) {
-              const int so = (L.we1x + (t * 2 + 1) * 512) * 4;
+              const int so = (L.we1x + (t * KS0MAX + ks) * 512) * 4;
               ah = bload4(W, lane * 32, so);
               al = bload4(W, lane * 32 + 16, so);
             }
@@ -1404,8 +1416,8 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   f32x4 wfh = (f32x4)0.f, wfl = (f32x4)0.f;
   if constexpr (rcm == RECOMP_X0) {
     if (w < NT) {
-      wfh = bload4(W, lane * 32, (L.we1x + (w * 2) * 512) * 4);
-      wfl = bload4(W, lane * 32 + 16, (L.we1x + (w * 2) * 512) * 4);
+      wfh = bload4(W, lane * 32, (L.we1x + (w * KS0MAX) * 512) * 4);
+      wfl = bload4(W, lane * 32 + 16, (L.we1x + (w * KS0MAX) * 512) * 4);
     }
   }
   f32x16 acc[2][2];
@@ -1477,16 +1489,32 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
       }
     }
     if constexpr (rcm == RECOMP_X0) {
-      // GEMM0's B operand of lane (row j, half hh), as the layer backward builds it:
-      // half 0 = h_i's row, half 1 = h_j's (+ radial in slot 7 for nf <= 7); rx[8] =
-      // radial (the second k-step of nf = 8)
+      // GEMM0's B operand of lane (row j, half hh), as the layer backward builds it
+      // (k order gemm0_col): rx[8 ks + u] = k-slice ks, half 0 = h_i's features
+      // 8 ks + u, half 1 = h_j's (+ radial in slot 7 of the last slice when that is
+      // padding); nf = 8: rx[8] = radial (the second k-slice)
+      if constexpr (NFMAX == 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = hh ? nf + u : u;
-        G.rx[u] = (pv && u < nf) ? xblk[q * 32 + j] : 0.f;
+        for (int u = 0; u < 8; ++u) {
+          const int q = hh ? nf + u : u;
+          G.rx[u] = (pv && u < nf) ? xblk[q * 32 + j] : 0.f;
+        }
+        if (hh && nf <= 7) G.rx[7] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
+        G.rx[8] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
+      } else {   // nf <= 15 (BWD_NFMAX): at most two k-slices
+        const int nch = gemm0_nch(nf);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int f = u, q = hh ? nf + f : f;
+          G.rx[u] = (pv && f < nf && u < 8 * nch) ? xblk[q * 32 + j] : 0.f;
+        }
+        const float rad = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
+        if (gemm0_radial_slot7(nf)) {
+          if (hh) G.rx[8 * nch - 1] = rad;
+        } else if (hh == 0) {
+          G.rx[8] = rad;   // nf == 8: the radial's own slice
+        }
       }
-      if (hh && nf <= 7) G.rx[7] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
-      G.rx[8] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
     } else {
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
@@ -1553,15 +1581,20 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         f32x16 x = (f32x16)0.f;
         for (int ks = 0; ks < ks_n; ++ks) {
           f32x16 in;
+          if constexpr (NFMAX == 8) {
 #pragma unroll
-          for (int u = 0; u < 8; ++u) in[u] = ks == 0 ? G.rx[u] : 0.f;
-          if (ks == 1 && hh == 0) in[0] = G.rx[8];
+            for (int u = 0; u < 8; ++u) in[u] = ks == 0 ? G.rx[u] : 0.f;
+            if (ks == 1 && hh == 0) in[0] = G.rx[8];
+          } else {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) in[u] = ks == 0 ? G.rx[u] : G.rx[8 + u];
+          }
           f16x8 bh, bl;
           split_f16(in, 0, bh, bl);
           f32x4 ah = wfh, al = wfl;
           if (ks == 1) {
-            ah = bload4(W, lane * 32, (L.we1x + (w * 2 + 1) * 512) * 4);
-            al = bload4(W, lane * 32 + 16, (L.we1x + (w * 2 + 1) * 512) * 4);
+            ah = bload4(W, lane * 32, (L.we1x + (w * KS0MAX + 1) * 512) * 4);
+            al = bload4(W, lane * 32 + 16, (L.we1x + (w * KS0MAX + 1) * 512) * 4);
           }
           x = mfma_f16(ah, bh, x);
           x = mfma_f16(ah, bl, x);
@@ -2372,17 +2405,17 @@ int enflow_read_stamps(unsigned long long* host_out, int reset) {
 #endif
 
 int64_t enflow_lf_tape_size(int num_atoms, int nf, int H, int n_layers) {
-  if (num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || n_layers < 0) return -1;
+  if (num_atoms < 0 || nf < 1 || nf > BWD_NFMAX || !hid_ok_b(H) || n_layers < 0) return -1;
   return (int64_t)tape_layout(num_atoms, nf, H, n_layers).total;
 }
 
 int64_t enflow_egcl_bwd_packed_size(int H, int nf) {
-  if (!hid_ok_b(H) || nf < 1 || nf > NFMAX) return -1;
+  if (!hid_ok_b(H) || nf < 1 || nf > BWD_NFMAX) return -1;
   return egcl_bwd_layout(H).total;
 }
 
 int enflow_pack_egcl_bwd_f32(const float* raw, int H, int nf, float* packed, void* stream) {
-  if (!hid_ok_b(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
+  if (!hid_ok_b(H) || nf < 1 || nf > BWD_NFMAX || !raw || !packed) return -1;
   const int total = egcl_bwd_layout(H).total;
   hipLaunchKernelGGL(egcl_bwd_scale_kernel, dim3(6), dim3(256), 0, SB(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, SB(stream), raw, H, nf, packed);
@@ -2391,7 +2424,7 @@ int enflow_pack_egcl_bwd_f32(const float* raw, int H, int nf, float* packed, voi
 
 int64_t enflow_lf_backward_workspace_size(int num_mols, int num_atoms, int nf, int H, int n_layers,
                                           int64_t pair_row_bound) {
-  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0)
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > BWD_NFMAX || !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0)
     return -1;
   return (int64_t)(bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound).total * sizeof(float));
 }
@@ -2431,7 +2464,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
   // dequant_kind may carry ENFLOW_EGCL_VARIANTS: layers with norm_diff / tanh flags
   const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
   dequant_kind &= 0xff;
-  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > NFMAX ||
+  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > BWD_NFMAX ||
       !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0 || pair_row_bound > 0x7fffffffLL)
     return -1;
   if (!tape || !pair_counts || !layers || !layers_bwd || !layers_raw || !adj_h || !adj_g || !adj_pos ||
@@ -2564,7 +2597,7 @@ static LgBwdWs lg_bwd_ws(int num_mols, int num_atoms, int max_n, int nf, int H, 
 
 int64_t enflow_lf_backward_large_workspace_size(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
                                                 int64_t pair_row_bound) {
-  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms >= (1 << 22) || nf < 1 || nf > NFMAX ||
+  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms >= (1 << 22) || nf < 1 || nf > BWD_NFMAX ||
       !hid_ok_b(H) || pair_row_bound < 0 || pair_row_bound > 0x7fffffffLL)
     return -1;
   return (int64_t)lg_bwd_ws(num_mols, num_atoms, max_mol_atoms, nf, H, pair_row_bound).total;
@@ -2708,7 +2741,7 @@ static size_t egcl_bwd_extra(int num_atoms, int nf) {
   return al64((size_t)num_atoms * 3) + al64((size_t)num_atoms * nf) + 64;
 }
 int64_t enflow_egcl_backward_workspace_size(int num_mols, int num_atoms, int nf, int H, int64_t pair_row_bound) {
-  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || pair_row_bound < 0) return -1;
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > BWD_NFMAX || !hid_ok_b(H) || pair_row_bound < 0) return -1;
   return (int64_t)((bwd_ws(num_mols, num_atoms, nf, H, 1, pair_row_bound).total + egcl_bwd_extra(num_atoms, nf)) *
                    sizeof(float));
 }
@@ -2721,7 +2754,7 @@ int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int
                              float* adj_h, float* adj_pos, float* grad_layer,
                              void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
                              int32_t* err_flag, void* stream) {
-  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > NFMAX || !hid_ok_b(H) || pair_row_bound < 0) return -1;
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > BWD_NFMAX || !hid_ok_b(H) || pair_row_bound < 0) return -1;
   if (!adj_Q || !adj_F || !adj_G || !workspace) return -1;
   const BwdWs Wl = bwd_ws(num_mols, num_atoms, nf, H, 1, pair_row_bound);
   if ((uint64_t)workspace_bytes < (Wl.total + egcl_bwd_extra(num_atoms, nf)) * sizeof(float)) return -6;
@@ -2791,7 +2824,7 @@ int enflow_argmax_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, i
                                const int32_t* mol_ptr, const float* h, const float* dequant_raw, const float* noise,
                                const float* adj_z, const float* adj_log_q, float* grad_dequant,
                                void* workspace, int64_t workspace_bytes, void* stream) {
-  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > NFMAX ||
+  if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > BWD_NFMAX ||
       !hid_ok_b(H))
     return -1;
   if (!mol_ptr || !h || !dequant_raw || !noise || !adj_z || !adj_log_q || !grad_dequant || !workspace) return -1;

@@ -95,7 +95,7 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
     else if (idx < L.scl + 16) continue;     // written by egcl_scale_kernel
     else if (idx >= L.we1x && idx < L.wv1x) {  // F16X3 edge_nn.0: [t][ks][lane][hi 8 | lo 8], A[m][k]
       const int e = idx - L.we1x;
-      const int d = e & 7, lane = (e >> 3) & 63, ks = (e >> 9) & 1, t = e >> 10;
+      const int d = e & 7, lane = (e >> 3) & 63, ks = (e >> 9) % KS0MAX, t = (e >> 9) / KS0MAX;
       const float sc = out[L.scl + 4];
       const int row = 32 * t + (lane & 31);
       uint32_t bits = 0;

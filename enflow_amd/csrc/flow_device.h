@@ -16,12 +16,20 @@
 #define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
 #endif
 #define BLOCK (64 * WAVES)
-#define NFMAX 8
+// node feature capacity: 8 in libenflow_hip.so; libenflow_hip_nf16.so is the
+// same sources built with -DENFLOW_NFMAX=16 (node_nf 9..16).  Only 8 and 16:
+// the F16X3 GEMM0 / node-phase k-slices hold 8 features per lane half.
+#ifndef ENFLOW_NFMAX
+#define ENFLOW_NFMAX 8
+#endif
+#define NFMAX ENFLOW_NFMAX
+static_assert(NFMAX == 8 || NFMAX == 16, "ENFLOW_NFMAX must be 8 or 16");
+#define KS0MAX (NFMAX / 8 + 1)   // F16X3 GEMM0 k-slices (feature chunks of 8, + radial)
 #ifndef ENFLOW_MSG_LDS
 #define ENFLOW_MSG_LDS 0   // 1: message segment sums through a per-wave LDS scratch instead of DPP
                            // scans (measured 10 % slower: the serial reduce exposes LDS latency)
 #endif
-#define NFP 9  // LDS row stride of h / g / G (odd -> conflict-free across atoms)
+#define NFP (NFMAX + 1)  // LDS row stride of h / g / G (odd -> conflict-free across atoms)
 #ifndef ENFLOW_WAVES_PER_SIMD
 #define ENFLOW_WAVES_PER_SIMD 2   // workgroups of 4 waves per CU (VGPR budget 256 / 168 for 2 / 3)
 #endif
@@ -86,7 +94,7 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   L.scl = o; o += 16;                      // (2^s, 2^-s) of edge_nn.2, coord_nn.0, edge_nn.0,
                                            // vel_scaling_nn.0, node_nn.0, node_nn.2 (F16X3)
   o = (o + 63) & ~63;
-  L.we1x = o; o += NT * 2 * 512;           // [t][ks][lane][hi 8 | lo 8] f16, k = raw column of edge_nn.0
+  L.we1x = o; o += NT * KS0MAX * 512;      // [t][ks][lane][hi 8 | lo 8] f16, k = raw column of edge_nn.0
   L.wv1x = o; o += NT * 512;               // [tp][lane][hi|lo]: vel_scaling_nn.0, k = h feature
   L.wn1hx = o; o += NT * 512;              // [tp][lane][hi|lo]: node_nn.0 h part
   L.wn1ax = o; o += NT * (H / 16) * 512;   // [tp][ks][lane][hi|lo]: node_nn.0 agg part, k = 16 ks + 8 kh + j
@@ -101,19 +109,26 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
 }
 
 // F16X3 edge_nn.0 (GEMM0) k order, chosen so each lane half reads ONE atom's
-// zero-padded feature row: k-slice 0 = [h_i[0..7] | h_j[0..6], radial] for
-// nf <= 7 ([.., h_j[7]] for nf == 8), k-slice 1 (nf == 8 only) = [radial, 0..].
+// zero-padded feature row: k-slice ks < nch = ceil(nf / 8) holds features
+// 8 ks .. 8 ks + 7 of h_i (lane half 0) and of h_j (lane half 1); the radial
+// takes half 1's slot 7 of the last slice when that slot is padding (nf % 8 !=
+// 0), else an extra slice of its own (half 0, slot 0).  nf <= 7: one slice
+// [h_i[0..7] | h_j[0..6], radial]; nf == 8: [h_i | h_j], [radial, 0..].
 // Returns the raw edge_nn.0 input column of (k-slice ks, k = 8 half + slot), or -1.
+__host__ __device__ inline int gemm0_nch(int nf) { return (nf + 7) >> 3; }
+__host__ __device__ inline bool gemm0_radial_slot7(int nf) { return (nf & 7) != 0; }
 __host__ __device__ inline int gemm0_col(int ks, int kk, int nf) {
   const int half = kk >> 3, s = kk & 7;
-  if (ks == 0) {
-    if (half == 0) return s < nf ? s : -1;
-    if (s < 7) return s < nf ? nf + s : -1;
-    return nf <= 7 ? 2 * nf : nf + 7;
+  const int nch = gemm0_nch(nf);
+  if (ks < nch) {
+    if (half == 1 && s == 7 && ks == nch - 1 && gemm0_radial_slot7(nf)) return 2 * nf;
+    const int f = 8 * ks + s;
+    if (f >= nf) return -1;
+    return half == 0 ? f : nf + f;
   }
-  return (nf == 8 && kk == 0) ? 2 * nf : -1;
+  return (ks == nch && kk == 0 && !gemm0_radial_slot7(nf)) ? 2 * nf : -1;
 }
-__host__ __device__ inline int gemm0_ksteps(int nf) { return nf == 8 ? 2 : 1; }
+__host__ __device__ inline int gemm0_ksteps(int nf) { return gemm0_nch(nf) + (gemm0_radial_slot7(nf) ? 0 : 1); }
 
 struct RawEgcl {  // offsets into the raw (torch) concatenation
   int We1, be1, We2, be2, Wn1, bn1, Wn2, bn2, Wc1, bc1, wc2, Wv1, bv1, Wv2, bv2, total;
@@ -302,13 +317,11 @@ __device__ __forceinline__ float silu_f(float x) {
 #endif
 __device__ __forceinline__ f32x4 silu4(f32x4 z) {
 #if ENFLOW_SILU4_ASM
-  float t0, t1, t2, t3;
+  // first reads of z in compiler code (see silu4s: MFMA-result hazards)
+  float t0 = z[0] * -1.4426950408889634f, t1 = z[1] * -1.4426950408889634f, t2 = z[2] * -1.4426950408889634f,
+        t3 = z[3] * -1.4426950408889634f;
   f32x4 y;
-  asm("v_mul_f32 %4, 0xbfb8aa3b, %8\n\t"
-      "v_mul_f32 %5, 0xbfb8aa3b, %9\n\t"
-      "v_mul_f32 %6, 0xbfb8aa3b, %10\n\t"
-      "v_mul_f32 %7, 0xbfb8aa3b, %11\n\t"
-      "v_exp_f32 %4, %4\n\t"
+  asm("v_exp_f32 %4, %4\n\t"
       "v_exp_f32 %5, %5\n\t"
       "v_exp_f32 %6, %6\n\t"
       "v_exp_f32 %7, %7\n\t"
@@ -323,8 +336,9 @@ __device__ __forceinline__ f32x4 silu4(f32x4 z) {
       "v_mul_f32 %0, %8, %4\n\t"
       "v_mul_f32 %1, %9, %5\n\t"
       "v_mul_f32 %2, %10, %6\n\t"
-      "v_mul_f32 %3, %11, %7"
-      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
+      "v_mul_f32 %3, %11, %7\n\t"
+      "s_nop 1"
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3)
       : "v"(z[0]), "v"(z[1]), "v"(z[2]), "v"(z[3]));
   return y;
 #else
@@ -347,20 +361,21 @@ __device__ __forceinline__ float silu_sc(float a, float c, float K) {
 #endif
 __device__ __forceinline__ f32x4 silu4s(f32x4 a, float c, float K) {
 #if ENFLOW_SILU4S_ASM
-  float t0, t1, t2, t3;
+  // a is usually an MFMA accumulator: its first readers (the scaled arguments)
+  // are compiler code, so hipcc pads the MFMA-result -> VALU read hazard; an asm
+  // statement gets no such pad (cdna_hip_programming.md §5.7 item 2) and read
+  // the accumulators before the chain's last MFMA had landed.  The asm reads a
+  // again only in its last multiply, after those reads.
+  float t0 = a[0] * c, t1 = a[1] * c, t2 = a[2] * c, t3 = a[3] * c;
   f32x4 y;
-  asm("v_mul_f32 %4, %12, %8\n\t"
-      "v_mul_f32 %5, %12, %9\n\t"
-      "v_mul_f32 %6, %12, %10\n\t"
-      "v_mul_f32 %7, %12, %11\n\t"
-      "v_exp_f32 %4, %4\n\t"
+  asm("v_exp_f32 %4, %4\n\t"
       "v_exp_f32 %5, %5\n\t"
       "v_exp_f32 %6, %6\n\t"
       "v_exp_f32 %7, %7\n\t"
-      "v_fma_f32 %4, %4, %13, %13\n\t"
-      "v_fma_f32 %5, %5, %13, %13\n\t"
-      "v_fma_f32 %6, %6, %13, %13\n\t"
-      "v_fma_f32 %7, %7, %13, %13\n\t"
+      "v_fma_f32 %4, %4, %12, %12\n\t"
+      "v_fma_f32 %5, %5, %12, %12\n\t"
+      "v_fma_f32 %6, %6, %12, %12\n\t"
+      "v_fma_f32 %7, %7, %12, %12\n\t"
       "v_rcp_f32 %4, %4\n\t"
       "v_rcp_f32 %5, %5\n\t"
       "v_rcp_f32 %6, %6\n\t"
@@ -368,9 +383,10 @@ __device__ __forceinline__ f32x4 silu4s(f32x4 a, float c, float K) {
       "v_mul_f32 %0, %8, %4\n\t"
       "v_mul_f32 %1, %9, %5\n\t"
       "v_mul_f32 %2, %10, %6\n\t"
-      "v_mul_f32 %3, %11, %7"
-      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3)
-      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "s"(c), "s"(K));
+      "v_mul_f32 %3, %11, %7\n\t"
+      "s_nop 1"   // an fp32 chain's MFMA may read y as its B operand next
+      : "=&v"(y[0]), "=&v"(y[1]), "=&v"(y[2]), "=&v"(y[3]), "+v"(t0), "+v"(t1), "+v"(t2), "+v"(t3)
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "s"(K));
   return y;
 #else
   return (f32x4){silu_sc(a[0], c, K), silu_sc(a[1], c, K), silu_sc(a[2], c, K), silu_sc(a[3], c, K)};
@@ -955,7 +971,7 @@ struct Smem {
   // F16X3 edge_nn.0 fragments of the current layer ([t][ks][hi lanes | lo lanes]
   // x 4 floats) for the <= 32-atom image (larger images read them from L2)
   static constexpr bool W1X_LDS = !BLOCKED && !BWD && NMAX <= 32;
-  alignas(16) float w1x[W1X_LDS ? NT * 2 * 512 : 4];
+  alignas(16) float w1x[W1X_LDS ? NT * KS0MAX * 512 : 4];
   alignas(16) float agg[RB * AST];
   alignas(16) float head[BWD ? 1 : WAVES][BWD ? 1 : H + 4];
   uint32_t pairs[PC];
@@ -963,7 +979,7 @@ struct Smem {
   // <= 32-atom images: the surviving periodic images that can reach the
   // molecule's bounding box within r_cut (bit s of near27[a]), their positions
   // imgp[a][s] kept in the edge_nn.0 fragment buffer (free during the pair build)
-  static constexpr bool IMG_LDS = W1X_LDS && NT * 2 * 512 >= NMAX * 27 * 4;
+  static constexpr bool IMG_LDS = W1X_LDS && NT * KS0MAX * 512 >= NMAX * 27 * 4;
   uint32_t near27[IMG_LDS ? NMAX : 1];
   float bbox[8];
   int idmap[NMAX];
@@ -1267,8 +1283,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     for (int e = tid; e < NT * ks_n * 128; e += BLOCK) {   // 128 x 16 B per (t, ks)
       const int blk = e >> 7, r = e & 127, ln = r >> 1, part = r & 1;
       const int t = blk / ks_n, ks = blk - t * ks_n;
-      const f32x4 v = ld4(Lp + L.we1x + (t * 2 + ks) * 512 + ln * 8 + part * 4);
-      st4(&sm.w1x[(t * 2 + ks) * 512 + part * 256 + ln * 4], v);
+      const f32x4 v = ld4(Lp + L.we1x + (t * KS0MAX + ks) * 512 + ln * 8 + part * 4);
+      st4(&sm.w1x[(t * KS0MAX + ks) * 512 + part * 256 + ln * 4], v);
     }
   }
   if (tid < WAVES) {
@@ -1354,19 +1370,21 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     if constexpr (PREC != PREC_F32) {   // F16X3 (bf16 mode too: a 16-wide k-step on the matrix cores
       // beats 9 f32 k-steps; only edge_nn.2 / coord_nn.0 run in bf16)
       // k order gemm0_col: lane half 0 = h_i's padded row, half 1 = h_j's (+ radial)
-      const int ks_n = gemm0_ksteps(nf);
+      const int ks_n = gemm0_ksteps(nf), nch = gemm0_nch(nf);
       for (int ks = 0; ks < ks_n; ++ks) {
         f32x16 in;
-        if (ks == 0) {
+        if (ks < nch) {
+          const int f0 = 8 * ks;
           if constexpr (BIG) {
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) in[jj] = hh ? (jj < nf ? chf(jj) : 0.f) : sm.h[i * NFP + jj];
+            for (int jj = 0; jj < 8; ++jj)
+              in[jj] = hh ? (f0 + jj < nf ? chf(f0 + jj) : 0.f) : sm.h[i * NFP + f0 + jj];
           } else {
-            const float* hrow = &sm.h[(hh ? jl : i) * NFP];   // rows zero-padded past nf
+            const float* hrow = &sm.h[(hh ? jl : i) * NFP + f0];   // rows zero-padded past nf
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) in[jj] = hrow[jj];
           }
-          if (hh && nf <= 7) in[7] = radial;
+          if (hh && ks == nch - 1 && gemm0_radial_slot7(nf)) in[7] = radial;
         } else {
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) in[jj] = 0.f;
@@ -1378,10 +1396,10 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         for (int t = 0; t < NT; ++t) {
           f32x4 ah, al;
           if constexpr (Smem<H, NMAX, RB>::W1X_LDS) {
-            ah = ld4(&sm.w1x[(t * 2 + ks) * 512 + lane * 4]);
-            al = ld4(&sm.w1x[(t * 2 + ks) * 512 + 256 + lane * 4]);
+            ah = ld4(&sm.w1x[(t * KS0MAX + ks) * 512 + lane * 4]);
+            al = ld4(&sm.w1x[(t * KS0MAX + ks) * 512 + 256 + lane * 4]);
           } else {
-            const int so = (L.we1x + (t * 2 + ks) * 512) * 4;
+            const int so = (L.we1x + (t * KS0MAX + ks) * 512) * 4;
             ah = bload4(W, lane * 32, so);
             al = bload4(W, lane * 32 + 16, so);
           }
@@ -1654,7 +1672,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(acc[4 * g4 + u] + b1[u]);
     }
-    // node_nn.2 partial: rows q = rho(r, hh), only r < 4 (q < 8) can be < nf
+    // node_nn.2 partial: rows q = rho(r, hh), only r < NFMAX / 2 (q < NFMAX) can be < nf
     f32x16 gacc = (f32x16)0.f;
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
@@ -1664,8 +1682,8 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
     }
     if (va) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = r + 4 * hh;
+      for (int r = 0; r < NFMAX / 2; ++r) {
+        const int q = rho(r, hh);
         if (q < nf) sm.u.nd.gp[tp][q][a] = gacc[r];
       }
     }
@@ -1725,10 +1743,10 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     const bool va = a < rb;
     const int ac = va ? a : 0;
     const int ag = r0 + ac;                 // atom
-    // h operand (k = feature, lane half 0 only; nf <= 8)
+    // h operand (k = feature 8 hh + jj: lane half 1 holds features 8..15, zero for nf <= 8)
     f32x16 hin;
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && hh == 0 && jj < nf) ? sm.h[ag * NFP + jj] : 0.f;
+    for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && 8 * hh + jj < nf) ? sm.h[ag * NFP + 8 * hh + jj] : 0.f;
     f16x8 hh16, hl16;
     split_f16(hin, 0, hh16, hl16);
     // vel_scaling_nn: Q partial over this wave's 32 hidden features
@@ -1777,7 +1795,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
     }
-    // node_nn.2 partial: rows q = rho(r, hh), only r < 4 (q < 8) can be < nf
+    // node_nn.2 partial: rows q = rho(r, hh), only r < NFMAX / 2 (q < NFMAX) can be < nf
     f32x16 gacc = (f32x16)0.f;
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
@@ -1790,8 +1808,8 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     if (item + WAVES < NT * NA) issue(item + WAVES);
     if (va) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int q = r + 4 * hh;
+      for (int r = 0; r < NFMAX / 2; ++r) {
+        const int q = rho(r, hh);
         if (q < nf) sm.u.nd.gp[tp][q][a] = gacc[r] * inv_n2;
       }
     }

@@ -27,7 +27,7 @@ class _FlowFunction(torch.autograd.Function):
         hid, nf, cw = flow._geometry()
         kind = flow._dequant_kind()
         dev = h.device
-        L = _lib.lib()
+        L = _lib.lib(nf)
         n_layers = len(flow.networks)
         A = h.shape[0]
         M = meta["mol_ptr"].numel() - 1
@@ -84,7 +84,7 @@ class _FlowFunction(torch.autograd.Function):
         h_in, tape, counts = ctx.saved_tensors
         hid, nf, cw = flow._geometry()
         dev = h_in.device
-        L = _lib.lib()
+        L = _lib.lib(nf)
         A = h_in.shape[0]
         M = meta["mol_ptr"].numel() - 1
         n_layers = len(flow.networks)
@@ -196,7 +196,7 @@ def flow_forward_train(flow, data, noise, check_errors):
 class _NLLFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, nll, meta, h, g, pos, vel, ldj):
-        L = _lib.lib()
+        L = _lib.lib(h.shape[1])
         dev = h.device
         M = meta["mol_ptr"].numel() - 1
         nll_mol = torch.empty((max(M, 1), 4), dtype=torch.float32, device=dev)
@@ -216,7 +216,7 @@ class _NLLFunction(torch.autograd.Function):
     def backward(ctx, gloss):
         h, g, pos, vel = ctx.saved_tensors
         nll, meta = ctx.nll, ctx.meta
-        L = _lib.lib()
+        L = _lib.lib(h.shape[1])
         dev = h.device
         M = meta["mol_ptr"].numel() - 1
         ah, ag = torch.empty_like(h), torch.empty_like(g)
@@ -266,7 +266,7 @@ class _EGCLFunction(torch.autograd.Function):
         net, meta = ctx.net, ctx.meta
         h, pos = ctx.saved_tensors
         large = meta["max_n"] > _lib.TRAIN_MAX_ATOMS
-        L = _lib.lib()
+        L = _lib.lib(net.kernel_nf)
         dev = h.device
         A, nf, hid = h.shape[0], net.kernel_nf, net.kernel_hidden
         M = meta["mol_ptr"].numel() - 1
@@ -353,7 +353,7 @@ class _ArgMaxFunction(torch.autograd.Function):
     def backward(ctx, gz, glq):
         am, meta = ctx.am, ctx.meta
         h, noise = ctx.saved_tensors
-        L = _lib.lib()
+        L = _lib.lib(am.node_nf)
         dev = h.device
         A, nf, hid = h.shape[0], am.node_nf, am.kernel_hidden
         raw = am.kernel_raw(dev)

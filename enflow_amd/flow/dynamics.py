@@ -87,7 +87,7 @@ class LFIntegrator(BaseFlow):
         if getattr(self, "_layers_key", None) == key:
             return self._layers_buf
         hid, nf, _ = self._geometry()
-        L = _lib.lib()
+        L = _lib.lib(nf)
         stride = L.enflow_egcl_packed_size(hid, nf)
         buf = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)
         for i, n in enumerate(self.networks):
@@ -101,7 +101,7 @@ class LFIntegrator(BaseFlow):
         if getattr(self, "_train_key", None) == key:
             return self._train_bufs
         hid, nf, _ = self._geometry()
-        L = _lib.lib()
+        L = _lib.lib(nf)
         self._check_trainable()
         # per layer: the default-flag raw parameters, then att_nn.0 (weight, bias) or
         # H + 1 zeros (enflow_lf_backward_f32's layers_raw stride)
@@ -132,8 +132,12 @@ class LFIntegrator(BaseFlow):
 
     def _check_trainable(self):
         """The HIP backward covers every EGCL constructor variant (attention,
-        norm_diff, tanh); only non-EGCL networks are refused (by _geometry)."""
-        self._geometry()
+        norm_diff, tanh); non-EGCL networks are refused (by _geometry), and
+        node_nf 16 (the backward holds 2 node_nf + 1 <= 32 edge inputs)."""
+        _, nf, _ = self._geometry()
+        if nf is not None and nf > _lib.TRAIN_MAX_NODE_NF:
+            raise NotImplementedError(f"enflow_amd trains node_nf <= {_lib.TRAIN_MAX_NODE_NF} (got {nf}); "
+                                      "inference runs up to 16")
 
     def _needs_grad(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
@@ -164,7 +168,7 @@ class LFIntegrator(BaseFlow):
         prec = self._prec() if prec is None else prec
         dq = self.dequantize.packed(dev, hid) if kind == _lib.DEQUANT_ARGMAX else None
         scale = float(getattr(self.dequantize, "dequant_scale", 1.0)) if kind == _lib.DEQUANT_FLOOR else 0.0
-        L = _lib.lib()
+        L = _lib.lib(nf)
         # training past the fused backward's molecule size records its tape on the
         # large-system path (pair_counts then holds the per-layer pair rows)
         if _lib.is_large(max_mol_atoms) or (tape is not None and max_mol_atoms > _lib.TRAIN_MAX_ATOMS):
@@ -202,7 +206,7 @@ class LFIntegrator(BaseFlow):
         (enflow_one_hot_f32 materialises the one-hot)."""
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
-        L = _lib.lib()
+        L = _lib.lib(nf)
         prec = self._prec() if prec is None else prec
         if _lib.is_large(max_mol_atoms):
             if src is not None:
@@ -300,7 +304,7 @@ class LFIntegrator(BaseFlow):
         idx = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         mx = torch.zeros(1, dtype=torch.int32, device=dev)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
-        L = _lib.lib()
+        L = _lib.lib(nf)
         prec = self._prec()
         while True:
             self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],

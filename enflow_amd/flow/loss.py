@@ -23,7 +23,7 @@ class Alchemical_NLL:
         if torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad
                                            for t in (out.h, out.g, out.pos, out.vel, ldj)):
             return self._differentiable(out, ldj)
-        L = _lib.lib()
+        L = _lib.lib(out.h.shape[1])
         dev = out.pos.device
         f = lambda t: t.detach().to(device=dev, dtype=torch.float32).contiguous()  # noqa: E731
         h, g, pos, vel = f(out.h), f(out.g), f(out.pos), f(out.vel)

@@ -45,7 +45,7 @@ class ArgMax(nn.Module):
         key = (str(device), width) + tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is not None and self._packed_key == key:
             return self._packed
-        L = _lib.lib()
+        L = _lib.lib(self.node_nf)
         raw = self.kernel_raw(device, width)
         out = torch.empty(L.enflow_argmax_packed_size(width, self.node_nf),
                           dtype=torch.float32, device=device)
@@ -68,7 +68,7 @@ class ArgMax(nn.Module):
                     num_mols=N.numel())
 
     def _infer(self, h, eps, meta):
-        L = _lib.lib()
+        L = _lib.lib(self.node_nf)
         dev = h.device
         n = h.shape[0]
         hf = h.to(torch.float32).contiguous()

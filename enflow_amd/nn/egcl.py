@@ -66,19 +66,20 @@ class EGCL(nn.Module):
     def hip_supported(self):
         """The HIP kernels implement every constructor flag of the reference
         (attention, norm_diff, tanh; ``clamp`` is stored and unused there too)
-        with the SiLU activation, input_nf and output_nf <= 8 and any hidden_nf
+        with the SiLU activation, input_nf and output_nf <= 16 and any hidden_nf
         <= 128 (hidden 32 / 64 / 128 and one feature width compiled, other
         shapes zero-padded)."""
-        L = _lib.lib()
         kh = self.kernel_hidden
-        return (isinstance(self.act_fn, nn.SiLU) and min(self.input_nf, self.output_nf) >= 1
-                and self.kernel_nf <= L.enflow_max_node_nf()
-                and kh is not None and bool(L.enflow_supports_hidden(kh)))
+        if not (isinstance(self.act_fn, nn.SiLU) and 1 <= min(self.input_nf, self.output_nf)
+                and self.kernel_nf <= _lib.MAX_NODE_NF and kh is not None):
+            return False
+        L = _lib.lib(self.kernel_nf)
+        return self.kernel_nf <= L.enflow_max_node_nf() and bool(L.enflow_supports_hidden(kh))
 
     def _check_supported(self):
         if not self.hip_supported():
             raise NotImplementedError(
-                "enflow_amd EGCL kernels implement the SiLU activation, input_nf / output_nf <= 8 "
+                "enflow_amd EGCL kernels implement the SiLU activation, input_nf / output_nf <= 16 "
                 "and hidden_nf <= 128")
 
     def variant_flags(self):
@@ -106,7 +107,7 @@ class EGCL(nn.Module):
                            EGCL_HDIMS, self.pad_geom(), device)
 
     def _pack(self, raw, dst, device):
-        L = _lib.lib()
+        L = _lib.lib(self.kernel_nf)
         att = self._att_raw(device)
         _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.kernel_hidden, self.kernel_nf, self.variant_flags(),
                                              _lib.ptr(att), _lib.ptr(dst), _lib.stream_ptr(device)),
@@ -119,7 +120,7 @@ class EGCL(nn.Module):
         key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is not None and self._packed_key == key:
             return self._packed
-        L = _lib.lib()
+        L = _lib.lib(self.kernel_nf)
         raw = self.kernel_raw(device)
         size = L.enflow_egcl_packed_size(self.kernel_hidden, self.kernel_nf)
         out = torch.empty(size, dtype=torch.float32, device=device)
@@ -140,7 +141,7 @@ class EGCL(nn.Module):
 
     def _infer(self, h, pos, meta):
         """EGCL.forward on the HIP kernels: (Q [n, 1], F [n, 3], G [n, nf]) fp32."""
-        L = _lib.lib()
+        L = _lib.lib(self.kernel_nf)
         dev = h.device
         n = h.shape[0]
         nf = self.kernel_nf
@@ -188,6 +189,9 @@ class EGCL(nn.Module):
         params = list(self.parameters())
         if torch.is_grad_enabled() and (h.requires_grad or edges.pos.requires_grad or
                                         any(p.requires_grad for p in params)):
+            if self.kernel_nf > _lib.TRAIN_MAX_NODE_NF:
+                raise NotImplementedError(f"enflow_amd differentiates EGCL up to node_nf {_lib.TRAIN_MAX_NODE_NF} "
+                                          "(inference runs up to 16); call it under torch.no_grad()")
             from ..flow._train import _EGCLFunction
             q, f, g = _EGCLFunction.apply(self, meta, h, edges.pos, *params)
         else:

@@ -71,7 +71,13 @@ int enflow_abi_version(void);
 int enflow_set_latency_threshold(int max_mols);
 int enflow_latency_threshold(void);
 
-/* Largest molecule (atoms) / node_nf the compiled kernels accept. */
+/* Largest molecule (atoms) / node_nf the compiled kernels accept.  The ABI
+ * ships as two builds of the same sources: libenflow_hip.so (node_nf <= 8) and
+ * libenflow_hip_nf16.so (-DENFLOW_NFMAX=16: node_nf <= 16 for inference, <= 15
+ * for the training / EGCL backward entry points, whose transposed edge_nn.0
+ * GEMM holds 2 node_nf + 1 <= 32 inputs); the host picks by node_nf.  The
+ * reference sizes EGCL / ArgMax by the dataset's node_nf
+ * (enflow/main.py:148-151). */
 int enflow_max_atoms(void);
 int enflow_max_node_nf(void);
 /* 1 if hidden_nf is one of the compiled widths (32, 64, 128). */

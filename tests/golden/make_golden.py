@@ -149,17 +149,16 @@ def case_edges():
                                  "coord_diff": e.coord_diff.numpy()})
 
 
-def case_egcl(hid, seed):
+def case_egcl(hid, seed, nf=5, name=None):
     torch.manual_seed(seed)
-    nf = 5
     net = EGCL(nf, nf, hid).double()
     b = batch_inputs(4, [22, 9, 15, 3], nf, seed=seed, one_hot=False)
     d = ref_data(b)
     q, f, g = net(d.h, d.edges)
     inp = dict(b)
     inp.update(params_of(net, "p0."))
-    save(f"egcl_h{hid}", inp, {"Q": q.detach().numpy(), "F": f.detach().numpy(),
-                               "G": g.detach().numpy()})
+    save(name or f"egcl_h{hid}", inp, {"Q": q.detach().numpy(), "F": f.detach().numpy(),
+                                       "G": g.detach().numpy()})
 
 
 def case_egcl_variant(hid, seed, flags, name):
@@ -194,10 +193,9 @@ def case_argmax(hid, seed):
                                  "reverse": rev.numpy()})
 
 
-def case_flow(hid, n_layers, sizes, seed, name, flags=None):
+def case_flow(hid, n_layers, sizes, seed, name, flags=None, nf=5):
     """``flags``: per layer (attention, norm_diff, tanh), default flags when None."""
     torch.manual_seed(seed)
-    nf = 5
     dt = default_dt()
     if flags is None:
         nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
@@ -376,6 +374,15 @@ if __name__ == "__main__":
         case_flow(64, 3, [22, 9, 15, 3], 34, "lf_var_h64_L3",
                   flags=[(True, False, False), (False, True, True), (True, True, True)])
         case_flow(128, 2, [22, 22, 30], 35, "lf_var_h128_L2", flags=[(False, True, False), (True, False, True)])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "wide_nf":
+        # node_nf past 8 (the dataset decides it: enflow/main.py:148-151): the
+        # 16-feature build (libenflow_hip_nf16.so)
+        case_flow(64, 2, [22, 9, 15], 61, "lf_nf12_h64_L2", nf=12)
+        case_flow(32, 2, [22, 13], 62, "lf_nf16_h32_L2", nf=16)
+        case_egcl(128, 63, nf=16, name="egcl_nf16_h128")
+        case_train(32, 2, [22, 9, 15], 64, "train_nf12_h32_L2", nf=12)
+        case_train(128, 2, [22, 17], 65, "train_nf15_h128_L2", nf=15)
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "train":
         case_train(32, 3, [22, 9, 15, 3], 21, "train_h32_L3")

@@ -22,13 +22,29 @@ def header_symbols():
     return sorted(set(re.findall(r"\b(enflow_\w+)\s*\(", txt)))
 
 
-def test_library_exports_every_header_symbol():
-    L = _lib.lib()
+@pytest.mark.parametrize("nf", [None, 16], ids=["libenflow_hip", "libenflow_hip_nf16"])
+def test_library_exports_every_header_symbol(nf):
+    L = _lib.lib(nf)
     syms = header_symbols()
     assert len(syms) >= 14
     for s in syms:
         assert hasattr(L, s), s
         assert s in _lib.SIGNATURES, f"{s} has no ctypes signature"
+
+
+def test_node_feature_library_selection():
+    """node_nf <= 8: libenflow_hip.so; 9..16: libenflow_hip_nf16.so (the same
+    sources with ENFLOW_NFMAX=16); wider is refused."""
+    assert _lib.lib_path(5) == _lib.lib_path(None) == _lib.LIB_PATH
+    assert _lib.lib_path(8) == _lib.LIB_PATH and _lib.lib_path(9) == _lib.LIB_NF16_PATH
+    L16 = _lib.lib(16)
+    assert L16.enflow_abi_version() == 9 and L16.enflow_max_node_nf() == 16
+    assert L16.enflow_egcl_packed_size(128, 16) > 0 and L16.enflow_egcl_packed_size(128, 17) == -1
+    # training: 2 nf + 1 <= 32 edge inputs (one output tile of the transposed edge_nn.0 GEMM)
+    assert L16.enflow_lf_backward_workspace_size(4, 88, 15, 128, 2, 4 * 480) > 0
+    assert L16.enflow_lf_backward_workspace_size(4, 88, 16, 128, 2, 4 * 480) == -1
+    with pytest.raises(NotImplementedError):
+        _lib.lib_path(17)
 
 
 def test_abi_queries():

@@ -32,7 +32,7 @@ def main():
     outs = {}
 
     def run(path, reps):
-        _lib._lib = None
+        _lib._libs.clear()
         _lib.LIB_PATH = path
         model._layers_key = None
         model.dequantize._packed_key = None

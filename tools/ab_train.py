@@ -46,8 +46,8 @@ def main():
                 os.environ.pop(kv.partition("=")[0], None)
 
     def _run(spec, path, reps):
-        if _lib.LIB_PATH != path or _lib._lib is None:
-            _lib._lib = None
+        if _lib.LIB_PATH != path or not _lib._libs:
+            _lib._libs.clear()
             _lib.LIB_PATH = path
         for mod in model.modules():
             for attr in ("_packed_key", "_layers_key", "_train_key"):

@@ -28,7 +28,7 @@ def main():
     names = [n for n, _ in model.named_parameters()] + ["input.pos", "input.vel"]
 
     def run(path):
-        _lib._lib = None
+        _lib._libs.clear()
         _lib.LIB_PATH = path
         for mod in model.modules():
             for attr in ("_packed_key", "_layers_key", "_train_key"):
