@@ -25,7 +25,7 @@ ERR_RANGE = 8
 DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
 PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
-EGCL_ATTENTION, EGCL_NORM_DIFF, EGCL_TANH = 1, 2, 4   # ENFLOW_EGCL_* (include/enflow_hip.h)
+EGCL_ATTENTION, EGCL_NORM_DIFF, EGCL_TANH, EGCL_ACT = 1, 2, 4, 8   # ENFLOW_EGCL_* (include/enflow_hip.h)
 EGCL_VARIANTS = 0x100                                  # OR into gemm_precision
 
 _i, _i64, _f, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
@@ -43,6 +43,7 @@ SIGNATURES = {
     "enflow_argmax_packed_size": (_i64, [_i, _i]),
     "enflow_pack_egcl_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_pack_egcl_ex_f32": (_i, [_p, _i, _i, _i, _p, _p, _p]),
+    "enflow_pack_egcl_act_f32": (_i, [_p, _i, _i, _i, _i, _f, _f, _p, _p, _p]),
     "enflow_pack_argmax_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_lf_forward_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                    _i, _p, _p, _f, _f, _f, _p, _p, _p, _p, _p, _p, _i, _p]),

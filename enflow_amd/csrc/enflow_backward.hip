@@ -125,6 +125,12 @@ __device__ __forceinline__ float dsilu_f(float z) {   // d silu / dz
   const float s = sigmoid_f(z);
   return s * (1.f + z * (1.f - s));
 }
+// act'(z): the SiLU form above unless a generic (GEN) instance runs another act_fn
+template <bool GEN>
+__device__ __forceinline__ float dact_v(const Act& A, float z) {
+  if (!GEN || A.k == ACT_SILU) return dsilu_f(z);
+  return act_d(A, z);
+}
 
 // ---------------------------------------------------------------------------
 // per-layer backward
@@ -250,7 +256,7 @@ __device__ __forceinline__ int pow2_exp(float m) {
 //            (per-item partials, fixed-order sum over tp),
 //   d agg  = node_nn.0.weight[:, nf:]^T d pre   (into sm.agg, over the message sums).
 // Adjoint operands carry power-of-two scales like the edge chain's.
-template <int H, int NMAX>
+template <int H, int NMAX, bool VAR = false>
 __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs& B, const EgclLayout& L,
                                             const EgclBwdLayout& LB, int a0, int n, int nf, int tid) {
   auto& sm = sb.f;
@@ -262,6 +268,7 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
   const rsrc_t W = weights_rsrc(B.Lp, L.total), WB = weights_rsrc(B.Bp, LB.total);
   const int vo = lane * 32;
   const float inv_v1 = B.Lp[L.scl + 7], inv_n1 = B.Lp[L.scl + 9], inv_n2 = B.Lp[L.scl + 11];
+  const Act act = VAR ? act_of(B.Lp + L.vfl + 1) : act_silu();
   float* const gp = sm.u.nb;   // d h partials [tp][q][atom]
   for (int k = tid; k < H; k += BLOCK) {
     sm.bias[k] = B.Lp[L.bv1 + k];
@@ -322,11 +329,13 @@ __device__ __forceinline__ void node_bwd_x3(BwdSmem<H, NMAX>& sb, const BwdArgs&
       for (int u = 0; u < 4; ++u) {
         const int r = 4 * g4 + u;
         const float z1 = fmaf(zu[r], inv_v1, b1[u]), z2 = fmaf(zn[r], inv_n1, bn[u]);
-        const float s1 = sigmoid_f(z1), s2 = sigmoid_f(z2);
-        su4[u] = z1 * s1;
-        sn4[u] = z2 * s2;
-        au4[u] = aq * w2[u] * (s1 * (1.f + z1 * (1.f - s1)));
-        an4[u] = asn[r] * ug * (s2 * (1.f + z2 * (1.f - s2)));
+        float f1, f2, d1, d2;
+        act_fd<VAR>(act, z1, f1, d1);
+        act_fd<VAR>(act, z2, f2, d2);
+        su4[u] = f1;
+        sn4[u] = f2;
+        au4[u] = aq * w2[u] * d1;
+        an4[u] = asn[r] * ug * d2;
         au[r] = au4[u];
         an[r] = an4[u];
       }
@@ -582,7 +591,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     B.agr[(size_t)a0 * nf + e] = sb.aG[a * NFP + q];
   }
   if constexpr (PREC == PREC_F16X3) {
-    node_bwd_x3<H, NMAX>(sb, B, L, LB, a0, n, nf, tid);
+    node_bwd_x3<H, NMAX, VAR>(sb, B, L, LB, a0, n, nf, tid);
   } else {
   // VALU form (fp32 mode), NBCH atoms at a time:
   //      threads = (hidden unit k, atom group); adjoint rows staged in sm.u.nb
@@ -604,16 +613,18 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
         const float* wcol = Bp + LB.wn1T + NFMAX * H + k;
 #pragma unroll 8
         for (int f = 0; f < H; ++f) nn = fmaf(wcol[f * H], arow[f], nn);
-        const float s_u = sigmoid_f(u), s_n = sigmoid_f(nn);
-        const float du = s_u * (1.f + u * (1.f - s_u)), dn = s_n * (1.f + nn * (1.f - s_n));
+        const Act act = VAR ? act_of(B.Lp + L.vfl + 1) : act_silu();
+        float su_v, sn_v, du, dn;
+        act_fd<VAR>(act, u, su_v, du);
+        act_fd<VAR>(act, nn, sn_v, dn);
         const float au = sb.aQ[a] * wv2 * du;
         float asn = 0.f;
         for (int q = 0; q < nf; ++q) asn = fmaf(Rp[R.Wn2 + q * H + k], sb.aG[a * NFP + q], asn);
         const float an = asn * dn;
         const size_t row = (size_t)(a0 + a) * H + k;
-        B.su[row] = u * s_u;
+        B.su[row] = su_v;
         B.au[row] = au;
-        B.sn[row] = nn * s_n;
+        B.sn[row] = sn_v;
         B.an[row] = an;
         sm.u.nb[(a - c0) * 2 * H + k] = au;
         sm.u.nb[(a - c0) * 2 * H + H + k] = an;
@@ -675,6 +686,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const int vfl = VAR ? (int)B.Lp[L.vfl] : 0;   // wave-uniform constructor variants
     const bool v_nd = VAR && (vfl & EGCL_NORM_DIFF) != 0, v_tanh = VAR && (vfl & EGCL_TANH) != 0;
     const bool v_att = VAR && (vfl & EGCL_ATTENTION) != 0;
+    const Act act = VAR ? act_of(B.Lp + L.vfl + 1) : act_silu();   // act_fn (egcl.py:11)
     // the molecule's tile-blocked rows (trow): buffer resources on its first
     // row, per element a wave-uniform byte offset (tile, feature) + the lane's
     const size_t nrow = (size_t)TT_all * 32;
@@ -847,7 +859,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
           const f32x4 b = ld4(sm.bias + f0);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = silu_f(x0[t][4 * g4 + u] + b[u]);
+          for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = act_v<VAR>(act, x0[t][4 * g4 + u] + b[u]);
         }
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(5);
@@ -866,7 +878,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(ev[t][4 * g4 + u], inv1, b[u]);
             ST_PARK(rpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
-            ev[t][4 * g4 + u] = silu_f(z);
+            ev[t][4 * g4 + u] = act_v<VAR>(act, z);
           }
         }
       float att = 1.f;
@@ -903,9 +915,14 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(cv[t][4 * g4 + u], inv2, b[u]);
-            const float s = sigmoid_f(z);
-            part = fmaf(w2[u], z * s, part);   // pc is not stored: outer_x3_kernel recomputes it
-            cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
+            if (!VAR || act.k == ACT_SILU) {
+              const float s = sigmoid_f(z);
+              part = fmaf(w2[u], z * s, part);   // pc is not stored: outer_x3_kernel recomputes it
+              cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
+            } else {
+              part = fmaf(w2[u], act_f(act, z), part);
+              cv[t][4 * g4 + u] = w2[u] * act_d(act, z);
+            }
           }
         }
       float phi = part + __shfl_xor(part, 32, 64);
@@ -953,7 +970,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
           for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) s = fmaf(ae[t][r], silu_f(rl[t][r]), s);   // d message . e
+            for (int r = 0; r < 16; ++r) s = fmaf(ae[t][r], act_v<VAR>(act, rl[t][r]), s);   // d message . e
           dl = (s + __shfl_xor(s, 32, 64)) * att * (1.f - att);                      // d logit
 #pragma unroll
           for (int t = 0; t < NT; ++t)
@@ -975,7 +992,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           const int f0 = 32 * t + 8 * g4 + 4 * hh;
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            ae[t][4 * g4 + u] *= dsilu_f(rl[t][4 * g4 + u]);
+            ae[t][4 * g4 + u] *= dact_v<VAR>(act, rl[t][4 * g4 + u]);
             ST_OUT(rdpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7), ae[t][4 * g4 + u]);
           }
         }
@@ -999,7 +1016,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           const f32x4 b = ld4(sm.bias + f0);
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
-            ax[t][4 * g4 + u] = ax[t][4 * g4 + u] * u4 * dsilu_f(rl[t][4 * g4 + u] + b[u]);
+            ax[t][4 * g4 + u] = ax[t][4 * g4 + u] * u4 * dact_v<VAR>(act, rl[t][4 * g4 + u] + b[u]);
             ST_OUT(rdp0, lob, tsb + ((32 * t + 8 * g4 + u) << 7), ax[t][4 * g4 + u]);
           }
         }
@@ -1178,6 +1195,7 @@ struct OuterDesc {
   int recomp;                // outer_x3_kernel operands recomputed instead of read (RECOMP_*)
   const float* Lp;           // RECOMP_*: the layer's packed forward weights
   int nf;                    // RECOMP_X0: node features (xin row layout)
+  const float* actp;         // the layer's act_fn (kind, p0, p1; packed layer + vfl + 1), NULL: SiLU
 };
 // RECOMP_X0: X = silu(pre0), pre0 = edge_nn.0 . xin + be1 (the X source is xin, width ldx);
 // RECOMP_PC: DY = rowv * silu'(pc), pc = coord_nn.0 . X + bc1 (X read; no DY source), and
@@ -1219,7 +1237,7 @@ __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
 #endif
 #define PAIR_OUTER (ENFLOW_OUTER_X3 ? 2 : 1)
 #define OB_LD 129   // LDS row stride: tile-blocked stages write down the columns
-template <bool TILED>
+template <bool TILED, bool GEN = false>
 __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
@@ -1233,6 +1251,7 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   const int NB = D.N + (D.outB ? 1 : 0);
   const int n0 = nbi * 128;
   const int M = D.M, N = D.N;
+  const Act act = GEN && D.actp ? act_of(D.actp) : act_silu();
   __shared__ float sd[2][OB_ROWS][OB_LD];
   __shared__ float sx[2][OB_ROWS][OB_LD];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, j = lane & 31, hh = lane >> 5;
@@ -1284,11 +1303,11 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   auto lstore = [&](int buf) {
     if (tiled && D.xf_dy) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) rd[q] = ra * dsilu_f(rd[q]);
+      for (int q = 0; q < 16; ++q) rd[q] = ra * dact_v<GEN>(act, rd[q]);
     }
     if (tiled && D.xf_x) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) rx[q] = silu_f(rx[q]);
+      for (int q = 0; q < 16; ++q) rx[q] = act_v<GEN>(act, rx[q]);
     }
     if (tiled && D.xrow) {
 #pragma unroll
@@ -1388,7 +1407,7 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 #endif
 static_assert(ENFLOW_OUTER_X3 == 1, "pair-row weight gradients run on outer_x3_kernel (recomputed operands)");
 
-template <int H, int RCM>
+template <int H, int RCM, bool GEN = false>
 __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int nbi, int r0, int r1,
                                               float (*sd)[128][OX_LD], float (*sx)[128][OX_LD]) {
   constexpr int NT = H / 32;
@@ -1402,6 +1421,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   const bool do_bias = D.outB != nullptr && nbi == 0 && tid < M;
   const bool xf_dy = D.xf_dy != 0, xf_x = D.xf_x != 0;
   const bool fold = xf_dy && D.part2 != nullptr && nbi == 0;   // coord_nn.2's gradient rides along
+  const Act act = GEN && D.actp ? act_of(D.actp) : act_silu();
   // recompute: the layer's packed forward weights
   const int nf = rcm ? D.nf : 1;
   const EgclLayout L = egcl_layout(H, nf);
@@ -1533,9 +1553,11 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
           for (int q = 0; q < 4; ++q)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-              const float z = G.rd[4 * q + u], sg = sigmoid_f(z);
-              if (fold) wacc[q] = fmaf(G.ra4[u], z * sg, wacc[q]);
-              G.rd[4 * q + u] = G.ra4[u] * (sg * (1.f + z * (1.f - sg)));
+              const float z = G.rd[4 * q + u];
+              float fz, dz;
+              act_fd<GEN>(act, z, fz, dz);
+              if (fold) wacc[q] = fmaf(G.ra4[u], fz, wacc[q]);
+              G.rd[4 * q + u] = G.ra4[u] * dz;
             }
         }
 #pragma unroll
@@ -1545,7 +1567,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
       }
       if (xf_x) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) G.rx[q] = silu_f(G.rx[q]);
+        for (int q = 0; q < 16; ++q) G.rx[q] = act_v<GEN>(act, G.rx[q]);
       }
       if (D.xrow) {
 #pragma unroll
@@ -1567,9 +1589,11 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
       if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-          const float z = G.rd[q], sg = sigmoid_f(z);
-          if (fold) wacc[q] = fmaf(G.ra, z * sg, wacc[q]);
-          G.rd[q] = G.ra * (sg * (1.f + z * (1.f - sg)));
+          const float z = G.rd[q];
+          float fz, dz;
+          act_fd<GEN>(act, z, fz, dz);
+          if (fold) wacc[q] = fmaf(G.ra, fz, wacc[q]);
+          G.rd[q] = G.ra * dz;
         }
       }
 #pragma unroll
@@ -1606,13 +1630,13 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
           const int f0 = 32 * w + 8 * g4 + 4 * hh;
           const f32x4 b = ld4(D.Lp + L.be1 + f0);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) sx[buf][f0 + u][j] = G.pv ? silu_f(x[4 * g4 + u] + b[u]) : 0.f;
+          for (int u = 0; u < 4; ++u) sx[buf][f0 + u][j] = G.pv ? act_v<GEN>(act, x[4 * g4 + u] + b[u]) : 0.f;
         }
       }
     } else {
       if (xf_x) {
 #pragma unroll
-        for (int q = 0; q < 16; ++q) G.rx[q] = silu_f(G.rx[q]);
+        for (int q = 0; q < 16; ++q) G.rx[q] = act_v<GEN>(act, G.rx[q]);
       }
       if (D.xrow) {
 #pragma unroll
@@ -1668,9 +1692,10 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float z = fmaf(cacc[4 * g4 + u], inv2, b[u]);
-          const float sg = sigmoid_f(z);
-          wacc2[4 * g4 + u] = fmaf(ra, z * sg, wacc2[4 * g4 + u]);
-          sd[buf][f0 + u][j] = ra * (sg * (1.f + z * (1.f - sg)));
+          float fz, dz;
+          act_fd<GEN>(act, z, fz, dz);
+          wacc2[4 * g4 + u] = fmaf(ra, fz, wacc2[4 * g4 + u]);
+          sd[buf][f0 + u][j] = ra * dz;
         }
       }
     }
@@ -1799,6 +1824,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   }
 }
 
+template <bool GEN = false>
 __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
@@ -1814,15 +1840,15 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
   // recomputed operands need the layer's hidden width at compile time
   // (one register allocation per branch: the modes' staged operands differ)
   if (D.recomp == RECOMP_X0) {
-    if (D.N == 128) outer_x3_body<128, RECOMP_X0>(D, chunk, nbi, r0, r1, sd, sx);
-    else if (D.N == 64) outer_x3_body<64, RECOMP_X0>(D, chunk, nbi, r0, r1, sd, sx);
-    else outer_x3_body<32, RECOMP_X0>(D, chunk, nbi, r0, r1, sd, sx);
+    if (D.N == 128) outer_x3_body<128, RECOMP_X0, GEN>(D, chunk, nbi, r0, r1, sd, sx);
+    else if (D.N == 64) outer_x3_body<64, RECOMP_X0, GEN>(D, chunk, nbi, r0, r1, sd, sx);
+    else outer_x3_body<32, RECOMP_X0, GEN>(D, chunk, nbi, r0, r1, sd, sx);
   } else if (D.recomp == RECOMP_PC) {
-    if (D.N == 128) outer_x3_body<128, RECOMP_PC>(D, chunk, nbi, r0, r1, sd, sx);
-    else if (D.N == 64) outer_x3_body<64, RECOMP_PC>(D, chunk, nbi, r0, r1, sd, sx);
-    else outer_x3_body<32, RECOMP_PC>(D, chunk, nbi, r0, r1, sd, sx);
+    if (D.N == 128) outer_x3_body<128, RECOMP_PC, GEN>(D, chunk, nbi, r0, r1, sd, sx);
+    else if (D.N == 64) outer_x3_body<64, RECOMP_PC, GEN>(D, chunk, nbi, r0, r1, sd, sx);
+    else outer_x3_body<32, RECOMP_PC, GEN>(D, chunk, nbi, r0, r1, sd, sx);
   } else {
-    outer_x3_body<128, RECOMP_NONE>(D, chunk, nbi, r0, r1, sd, sx);
+    outer_x3_body<128, RECOMP_NONE, GEN>(D, chunk, nbi, r0, r1, sd, sx);
   }
 }
 
@@ -1875,6 +1901,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_pt
   const int a0 = mol_ptr[m], n = mol_ptr[m + 1] - a0;
   if (n > NMAX) return;
   const int rW1 = 0, rb1 = H * nf, rW2 = rb1 + H, rb2 = rW2 + 2 * nf * H;
+  const Act am = act_of(Draw + rb2 + 2 * nf);   // network.1 (the raw vector's act trailer, ABI 10)
   for (int e = tid; e < n * nf; e += BLOCK) hs[e / nf][e % nf] = hdata[(size_t)a0 * nf + e];
   __syncthreads();
   constexpr int NG = BLOCK / H;
@@ -1883,7 +1910,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_pt
     float v = Draw[rb1 + k];
     for (int f = 0; f < nf; ++f) v = fmaf(Draw[rW1 + k * nf + f], hs[a][f], v);
     pre[a][k] = v;
-    spre_rows[(size_t)(a0 + a) * H + k] = v * sigmoid_f(v);
+    spre_rows[(size_t)(a0 + a) * H + k] = am.k == ACT_SILU ? v * sigmoid_f(v) : act_f(am, v);
   }
   __syncthreads();
   for (int e = tid; e < n * 2 * nf; e += BLOCK) {
@@ -1891,7 +1918,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_pt
     float s = Draw[rb2 + o];
     for (int kk = 0; kk < H; ++kk) {
       const float p = pre[a][kk];
-      s = fmaf(Draw[rW2 + o * H + kk], p * sigmoid_f(p), s);
+      s = fmaf(Draw[rW2 + o * H + kk], am.k == ACT_SILU ? p * sigmoid_f(p) : act_f(am, p), s);
     }
     net[a][o] = s;
   }
@@ -1938,8 +1965,13 @@ __global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_pt
   for (int a = grp; a < n; a += NG) {
     float s = 0.f;
     for (int o = 0; o < 2 * nf; ++o) s = fmaf(Draw[rW2 + o * H + k], anet[a][o], s);
-    const float p = pre[a][k], sp = sigmoid_f(p);
-    apre_rows[(size_t)(a0 + a) * H + k] = s * sp * (1.f + p * (1.f - sp));
+    const float p = pre[a][k];
+    if (am.k == ACT_SILU) {
+      const float sp = sigmoid_f(p);
+      apre_rows[(size_t)(a0 + a) * H + k] = s * sp * (1.f + p * (1.f - sp));
+    } else {
+      apre_rows[(size_t)(a0 + a) * H + k] = s * act_d(am, p);
+    }
   }
 }
 
@@ -2244,6 +2276,7 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.recomp = RECOMP_NONE;
   D.Lp = nullptr;
   D.nf = 0;
+  D.actp = nullptr;
   D.chunk = tiled ? OA_CHUNK : OA_CHUNK_ATOM;
   D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
   D.rows_dev = rows_dev; D.rows_static = rows_static;
@@ -2275,8 +2308,11 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
       sub.start[++sub.nd] = swg;
     }
     if (swg > 0) {
-      if (tl) ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL(outer_acc_kernel<true>, dim3(swg), dim3(256), 0, st, sub));
-      else ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL(outer_acc_kernel<false>, dim3(swg), dim3(256), 0, st, sub));
+      bool gen = false;   // a non-SiLU act_fn in the batch: the generic-activation instance
+      for (int k = 0; k < sub.nd; ++k) gen |= sub.d[k].actp != nullptr;
+      if (tl && gen) ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL((outer_acc_kernel<true, true>), dim3(swg), dim3(256), 0, st, sub));
+      else if (tl) ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL((outer_acc_kernel<true, false>), dim3(swg), dim3(256), 0, st, sub));
+      else ENFLOW_TIMED("outer_acc_kernel", st, hipLaunchKernelGGL((outer_acc_kernel<false, false>), dim3(swg), dim3(256), 0, st, sub));
     }
   }
   // F16X3 MFMA: tile-blocked descriptors with M > 1
@@ -2291,7 +2327,10 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
       swg += ob.start[k + 1] - ob.start[k];
       sub.start[++sub.nd] = swg;
     }
-    if (swg > 0) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel, dim3(swg), dim3(256), 0, st, sub));
+    bool gen = false;
+    for (int k = 0; k < sub.nd; ++k) gen |= sub.d[k].actp != nullptr;
+    if (swg > 0 && gen) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel<true>, dim3(swg), dim3(256), 0, st, sub));
+    else if (swg > 0) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel<false>, dim3(swg), dim3(256), 0, st, sub));
   }
   (void)wg;
   // reducer: one workgroup per 256 outputs of each descriptor
@@ -2333,10 +2372,14 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, XW, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1,
              PAIR_OUTER);
     // edge_nn.2: X = silu(pre0), pre0 recomputed from the xin rows
+    // the layer's act_fn (variant layers; packed layer + vfl + 1): the recomputed
+    // activations and their derivatives follow it (NULL: SiLU instances)
+    const float* actp = variants ? Lp + egcl_layout(H, nf).vfl + 1 : nullptr;
     add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.xin, XW, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
     ob.d[ob.nd - 1].recomp = RECOMP_X0;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
+    ob.d[ob.nd - 1].actp = actp;
     // coord_nn.0: X = silu(pre_e) = the message; DY = aphi * wc2 * silu'(pc), pc recomputed from X
     add_desc(ob, wg, nullptr, H, H, wb + Wl.pe, H, H, prow, 0, prb, part,
              G + R.Wc1, G + R.bc1, PAIR_OUTER);
@@ -2348,6 +2391,7 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     ob.d[ob.nd - 1].recomp = RECOMP_PC;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
+    ob.d[ob.nd - 1].actp = actp;
     // coord_nn.2: d wc2 = sum_rows aphi silu(pc), folded into coord_nn.0's pass (its partials
     // written there; this descriptor only sizes them and feeds the reduction)
     add_desc(ob, wg, wb + Wl.aphi, 1, 1, nullptr, H, H, prow, 0, prb, part, G + R.wc2, nullptr, 3);
@@ -2355,6 +2399,7 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     if (variants) {   // att_nn.0: d w = sum_rows dlogit e, d b = sum_rows dlogit (0 rows without attention)
       add_desc(ob, wg, wb + Wl.dlogit, 1, 1, wb + Wl.pe, H, H, prow, 0, prb, part, G + R.watt, G + R.batt, 1);
       ob.d[ob.nd - 1].xf_x = 1;                                 // X = silu(pre_e) = e
+      ob.d[ob.nd - 1].actp = actp;
     }
     add_desc(ob, wg, wb + Wl.au, H, H, hx, nf + H, nf, nullptr, num_atoms, num_atoms, part, G + R.Wv1, G + R.bv1);
     add_desc(ob, wg, wb + Wl.aq, 1, 1, wb + Wl.su, H, H, nullptr, num_atoms, num_atoms, part, G + R.Wv2, G + R.bv2);

@@ -32,7 +32,7 @@
 // packing kernels
 // ---------------------------------------------------------------------------
 __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out, int flags,
-                                 const float* __restrict__ att) {
+                                 const float* __restrict__ att, int act_kind, float act_p0, float act_p1) {
   const EgclLayout L = egcl_layout(H, nf);
   const RawEgcl R = raw_egcl(H, nf);
   const int NT = H / 32;
@@ -91,7 +91,10 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
     else if (idx < L.watt) { if (idx == L.bv2) v = raw[R.bv2]; }
     else if (idx < L.batt) { if (att) v = att[idx - L.watt]; }
     else if (idx < L.vfl) { if (idx == L.batt && att) v = att[H]; }
-    else if (idx < L.scl) { if (idx == L.vfl) v = (float)flags; }
+    else if (idx < L.scl) {                  // flags, act_fn kind / p0 / p1
+      const int e = idx - L.vfl;
+      v = e == 0 ? (float)flags : (e == 1 ? (float)act_kind : (e == 2 ? act_p0 : act_p1));
+    }
     else if (idx < L.scl + 16) continue;     // written by egcl_scale_kernel
     else if (idx >= L.we1x && idx < L.wv1x) {  // F16X3 edge_nn.0: [t][ks][lane][hi 8 | lo 8], A[m][k]
       const int e = idx - L.we1x;
@@ -190,7 +193,8 @@ __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf,
     if (idx < L.ba1) { int e = idx - L.wa1t; int q = e / H, k = e % H; v = raw[rW1 + k * nf + q]; }
     else if (idx < L.wa2) v = raw[rb1 + idx - L.ba1];
     else if (idx < L.ba2) v = raw[rW2 + idx - L.wa2];
-    else { int e = idx - L.ba2; if (e < 2 * nf) v = raw[rb2 + e]; }
+    else if (idx < L.act) { int e = idx - L.ba2; if (e < 2 * nf) v = raw[rb2 + e]; }
+    else if (idx < L.act + 3) v = raw[rb2 + 2 * nf + (idx - L.act)];   // act trailer: kind, p0, p1
     out[idx] = v;
   }
 }
@@ -221,7 +225,7 @@ __global__ void __launch_bounds__(BLOCK, 2) egcl_forward_kernel(FlowArgs A, floa
       block_compact(sm, n, tid, rb, p0);
       edge_tiles<H, NMAX, RB, PREC_F32, true>(sm, A.layers, L, M, nf, tid, r0, rb, false STAMP_PASS);
     }
-    node_phase(sm, A.layers, L, n, nf, tid, r0, rb);
+    node_phase<H, NMAX, RB, true>(sm, A.layers, L, n, nf, tid, r0, rb);
     for (int a = tid; a < rb; a += BLOCK) {
       const int ag = r0 + a;
       Qo[M.a0 + ag] = sm.Q[ag];
@@ -242,7 +246,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float
   if (!load_molecule(sm, A, M, LOAD_H)) return;
   const int tid = threadIdx.x;
   const int n = M.n, nf = A.nf;
-  const float lq = argmax_dequant(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+  const float lq = argmax_dequant<H, NMAX, RB, true>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
   for (int e = tid; e < n * nf; e += BLOCK) {
     const int a = e / nf, q = e - a * nf;
     z[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
@@ -514,16 +518,23 @@ int64_t enflow_argmax_packed_size(int hidden_nf, int node_nf) {
   return argmax_layout(hidden_nf, node_nf).total;
 }
 
-int enflow_pack_egcl_ex_f32(const float* raw, int H, int nf, int flags, const float* att, float* packed,
-                            void* stream) {
+int enflow_pack_egcl_act_f32(const float* raw, int H, int nf, int flags, int act_kind, float act_p0, float act_p1,
+                             const float* att, float* packed, void* stream) {
   if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed) return -1;
-  if (flags & ~(EGCL_ATTENTION | EGCL_NORM_DIFF | EGCL_TANH)) return -1;
+  if (flags & ~(ENFLOW_EGCL_ATTENTION | ENFLOW_EGCL_NORM_DIFF | ENFLOW_EGCL_TANH | ENFLOW_EGCL_ACT)) return -1;
   if ((flags & EGCL_ATTENTION) && !att) return -1;
+  if (act_kind < 0 || act_kind >= ACT_COUNT || ((act_kind != ACT_SILU) != ((flags & ENFLOW_EGCL_ACT) != 0))) return -1;
   const int total = egcl_layout(H, nf).total;
   hipLaunchKernelGGL(egcl_scale_kernel, dim3(6), dim3(256), 0, S(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_kernel, dim3((total + 255) / 256), dim3(256), 0, S(stream), raw, H, nf, packed,
-                     flags, (flags & EGCL_ATTENTION) ? att : nullptr);
+                     flags, (flags & EGCL_ATTENTION) ? att : nullptr, act_kind, act_p0, act_p1);
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_pack_egcl_ex_f32(const float* raw, int H, int nf, int flags, const float* att, float* packed,
+                            void* stream) {
+  if (flags & ENFLOW_EGCL_ACT) return -1;   // an act_fn needs its kind: enflow_pack_egcl_act_f32
+  return enflow_pack_egcl_act_f32(raw, H, nf, flags, ACT_SILU, 0.f, 0.f, att, packed, stream);
 }
 
 int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {

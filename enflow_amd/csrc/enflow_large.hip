@@ -360,8 +360,8 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
     p0 += PC;
     if (p0 >= tot) break;
   }
-  if constexpr (PREC != PREC_F32) node_phase_x3(sm, B.layer, L, rb, nf, tid, 0, rb);
-  else node_phase(sm, B.layer, L, rb, nf, tid, 0, rb);
+  if constexpr (PREC != PREC_F32) node_phase_x3<H, 32, 32, VAR>(sm, B.layer, L, rb, nf, tid, 0, rb);
+  else node_phase<H, 32, 32, VAR>(sm, B.layer, L, rb, nf, tid, 0, rb);
   if (tid == 0 && sm.err) atomicOr(B.err, sm.err);   // edge tiles' range check (split precision)
 
   const bool tape = mode == 0 && B.tape != nullptr;
@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(BLOCK) lg_dequant_kernel(LgArgs B, int kind, c
       sm.h[e] = (a < rb && q < nf) ? B.h[(size_t)(g0 + a) * nf + q] : 0.f;
     }
     __syncthreads();
-    lq = argmax_dequant(sm, dq, NoiseSrc{noise, 0, 0}, g0, rb, nf);
+    lq = argmax_dequant<H, 32, 32, true>(sm, dq, NoiseSrc{noise, 0, 0}, g0, rb, nf);   // act read per launch
     for (int e = tid; e < rb * nf; e += BLOCK) {
       const int a = e / nf, q = e - a * nf;
       B.h[(size_t)g0 * nf + e] = sm.h[a * NFP + q];

@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 9
+#define ENFLOW_ABI 10
 #ifndef WAVES
 #define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
 #endif
@@ -90,7 +90,7 @@ __host__ __device__ inline EgclLayout egcl_layout(int H, int nf) {
   L.bv2 = o; o += 4;
   L.watt = o; o += H;                      // att_nn.0.weight (attention layers; else zeros)
   L.batt = o; o += 4;                      // att_nn.0.bias
-  L.vfl = o; o += 4;                       // EGCL_* flags of the layer (as a float)
+  L.vfl = o; o += 4;                       // EGCL_* flags of the layer, act_fn kind, p0, p1 (as floats)
   L.scl = o; o += 16;                      // (2^s, 2^-s) of edge_nn.2, coord_nn.0, edge_nn.0,
                                            // vel_scaling_nn.0, node_nn.0, node_nn.2 (F16X3)
   o = (o + 63) & ~63;
@@ -257,7 +257,7 @@ __device__ __forceinline__ uint32_t f16_split_bits(float w0, float w1, bool lo) 
   return (uint32_t)__builtin_bit_cast(uint16_t, p0) | ((uint32_t)__builtin_bit_cast(uint16_t, p1) << 16);
 }
 
-struct AmLayout { int wa1t, ba1, wa2, ba2, total; };
+struct AmLayout { int wa1t, ba1, wa2, ba2, act, total; };
 __host__ __device__ inline AmLayout argmax_layout(int H, int nf) {
   AmLayout L;
   int o = 0;
@@ -265,6 +265,7 @@ __host__ __device__ inline AmLayout argmax_layout(int H, int nf) {
   L.ba1 = o; o += H;
   L.wa2 = o; o += 2 * nf * H; // [o][k] (torch layout)
   L.ba2 = o; o += 2 * NFMAX;
+  L.act = o; o += 4;          // activation of network.1: kind, p0, p1 (argmax_raw_act)
   o = (o + 63) & ~63;
   L.total = o;
   return L;
@@ -391,6 +392,119 @@ __device__ __forceinline__ f32x4 silu4s(f32x4 a, float c, float K) {
 #else
   return (f32x4){silu_sc(a[0], c, K), silu_sc(a[1], c, K), silu_sc(a[2], c, K), silu_sc(a[3], c, K)};
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// act_fn of EGCL / ArgMax (enflow/nn/egcl.py:11, enflow/nn/argmax.py:7): the
+// reference takes any torch activation module.  Kind + two parameters, packed
+// with the layer (EgclLayout::vfl + 1, AmLayout::act).  Only the variant-capable
+// (VAR) kernel instances read them; the default instances are SiLU by
+// construction, so their code is unchanged.  Definitions and derivatives (at
+// the kinks as torch's backward formulas take them):
+//   relu        max(z, 0)                        d = z > 0
+//   leaky_relu  z > 0 ? z : p0 z                 d = z > 0 ? 1 : p0
+//   elu         z > 0 ? z : p0 (e^z - 1)         d = z > 0 ? 1 : p0 e^z
+//   celu        z > 0 ? z : p0 (e^(z/p0) - 1)    d = z > 0 ? 1 : e^(z/p0)
+//   selu        s (z > 0 ? z : a (e^z - 1))      d = s (z > 0 ? 1 : a e^z)
+//   gelu        z Phi(z) (erf)                   d = Phi(z) + z phi(z)
+//   gelu_tanh   z (1 + tanh(u)) / 2, u = c (z + 0.044715 z^3)
+//   tanh, sigmoid, identity
+//   softplus    beta = p0, threshold = p1: z beta > p1 ? z : log1p(e^(beta z)) / beta
+//   mish        z tanh(softplus(z))
+//   hardtanh    clamp(z, p0, p1)                 d = p0 < z < p1
+// ---------------------------------------------------------------------------
+enum { ACT_SILU = 0, ACT_RELU = 1, ACT_LEAKY_RELU = 2, ACT_ELU = 3, ACT_CELU = 4, ACT_SELU = 5, ACT_GELU = 6,
+       ACT_GELU_TANH = 7, ACT_TANH = 8, ACT_SIGMOID = 9, ACT_SOFTPLUS = 10, ACT_MISH = 11, ACT_HARDTANH = 12,
+       ACT_IDENTITY = 13, ACT_COUNT = 14 };
+struct Act {
+  int k;
+  float p0, p1;
+};
+__host__ __device__ constexpr Act act_silu() { return Act{ACT_SILU, 0.f, 0.f}; }
+__device__ __forceinline__ Act act_of(const float* __restrict__ p) {
+  return Act{(int)p[0], p[1], p[2]};
+}
+__device__ __forceinline__ float sigm_exact(float x) { return 1.f / (1.f + expf(-x)); }
+// Out of line: inlined at every site of the unrolled tile code the switch
+// exceeds hipcc's unroll budget (register arrays then fall back to scratch);
+// as calls, the generic path costs a call per element and the SiLU path nothing.
+__device__ __attribute__((noinline)) float act_f(const Act& A, float z) {
+  switch (A.k) {
+    case ACT_RELU: return z > 0.f ? z : 0.f;
+    case ACT_LEAKY_RELU: return z > 0.f ? z : A.p0 * z;
+    case ACT_ELU: return z > 0.f ? z : A.p0 * expm1f(z);
+    case ACT_CELU: return z > 0.f ? z : A.p0 * expm1f(z / A.p0);
+    case ACT_SELU: return 1.0507009873554805f * (z > 0.f ? z : 1.6732632423543772f * expm1f(z));
+    case ACT_GELU: return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    case ACT_GELU_TANH: {
+      const float u = 0.79788456080286536f * (z + 0.044715f * z * z * z);
+      return 0.5f * z * (1.f + tanhf(u));
+    }
+    case ACT_TANH: return tanhf(z);
+    case ACT_SIGMOID: return sigm_exact(z);
+    case ACT_SOFTPLUS: return z * A.p0 > A.p1 ? z : log1pf(expf(A.p0 * z)) / A.p0;
+    case ACT_MISH: return z * tanhf(z > 20.f ? z : log1pf(expf(z)));
+    case ACT_HARDTANH: return fminf(fmaxf(z, A.p0), A.p1);
+    case ACT_IDENTITY: return z;
+    default: return z * sigm_exact(z);   // ACT_SILU
+  }
+}
+__device__ __attribute__((noinline)) float act_d(const Act& A, float z) {
+  switch (A.k) {
+    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case ACT_LEAKY_RELU: return z > 0.f ? 1.f : A.p0;
+    case ACT_ELU: return z > 0.f ? 1.f : A.p0 * expf(z);
+    case ACT_CELU: return z > 0.f ? 1.f : expf(z / A.p0);
+    case ACT_SELU: return 1.0507009873554805f * (z > 0.f ? 1.f : 1.6732632423543772f * expf(z));
+    case ACT_GELU:
+      return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * expf(-0.5f * z * z);
+    case ACT_GELU_TANH: {
+      const float u = 0.79788456080286536f * (z + 0.044715f * z * z * z);
+      const float th = tanhf(u);
+      return 0.5f * (1.f + th) + 0.5f * z * (1.f - th * th) * 0.79788456080286536f * (1.f + 0.134145f * z * z);
+    }
+    case ACT_TANH: { const float th = tanhf(z); return 1.f - th * th; }
+    case ACT_SIGMOID: { const float s = sigm_exact(z); return s * (1.f - s); }
+    case ACT_SOFTPLUS: return z * A.p0 > A.p1 ? 1.f : sigm_exact(A.p0 * z);
+    case ACT_MISH: {
+      const float sp = z > 20.f ? z : log1pf(expf(z)), th = tanhf(sp);
+      return th + z * sigm_exact(z) * (1.f - th * th);
+    }
+    case ACT_HARDTANH: return (z > A.p0 && z < A.p1) ? 1.f : 0.f;
+    case ACT_IDENTITY: return 1.f;
+    default: { const float s = sigm_exact(z); return s * (1.f + z * (1.f - s)); }
+  }
+}
+// the kernels' SiLU forms where the instance is SiLU-only (GEN false) or the
+// layer's act is SiLU; the generic definition otherwise (wave-uniform branch)
+template <bool GEN>
+__device__ __forceinline__ float act_v(const Act& A, float z) {
+  if (!GEN || A.k == ACT_SILU) return silu_f(z);
+  return act_f(A, z);
+}
+// act(z) and act'(z) together (SiLU: one sigmoid for both, as the backward's
+// original forms: f = z s, d = s (1 + z (1 - s)))
+template <bool GEN>
+__device__ __forceinline__ void act_fd(const Act& A, float z, float& f, float& d) {
+  if (!GEN || A.k == ACT_SILU) {
+    const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-z));
+    f = z * s;
+    d = s * (1.f + z * (1.f - s));
+  } else {
+    f = act_f(A, z);
+    d = act_d(A, z);
+  }
+}
+// 4 scaled pre-activations a = K z of an MFMA chain (silu4s's contract); ik = 1 / K
+template <bool GEN>
+__device__ __forceinline__ f32x4 act4s(f32x4 a, float c, float K, float ik, const Act& A) {
+  if (!GEN || A.k == ACT_SILU) return silu4s(a, c, K);
+  return (f32x4){act_f(A, a[0] * ik), act_f(A, a[1] * ik), act_f(A, a[2] * ik), act_f(A, a[3] * ik)};
+}
+template <bool GEN>
+__device__ __forceinline__ float act_sc(float a, float c, float K, float ik, const Act& A) {
+  if (!GEN || A.k == ACT_SILU) return silu_sc(a, c, K);
+  return act_f(A, a * ik);
 }
 
 __device__ __forceinline__ float pbc1(float x, float b) { return x - rintf(x / b) * b; }
@@ -1308,9 +1422,10 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const float hbx = M.bx * 0.5f, hby = M.by * 0.5f, hbz = M.bz * 0.5f;
   // scaled SiLU constants (silu4s): c = -log2(e) / K
   constexpr float NLOG2E = -1.4426950408889634f;
-  const float c0 = NLOG2E * (PREC != PREC_F32 ? Lp[L.scl + 5] : 1.f);
-  const float c1 = NLOG2E * (PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f);
-  const float c2 = NLOG2E * (PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f);
+  const float ik0 = PREC != PREC_F32 ? Lp[L.scl + 5] : 1.f;   // 1 / K0 .. 1 / K2 (exact powers of two)
+  const float ik1 = PREC == PREC_F16X3 ? Lp[L.scl + 1] : 1.f;
+  const float ik2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
+  const float c0 = NLOG2E * ik0, c1 = NLOG2E * ik1, c2 = NLOG2E * ik2;
   constexpr bool MSG_LDS = Smem<H, NMAX, RB>::MSG_LDS;
   constexpr int MSP = Smem<H, NMAX, RB>::MSP;
   float* const scr = MSG_LDS ? &sm.u.msg[w][0] : nullptr;
@@ -1319,6 +1434,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const int vfl = VAR ? (int)Lp[L.vfl] : 0;
   const bool v_att = (vfl & EGCL_ATTENTION) != 0, v_nd = (vfl & EGCL_NORM_DIFF) != 0,
              v_tanh = (vfl & EGCL_TANH) != 0;
+  const Act act = VAR ? act_of(Lp + L.vfl + 1) : act_silu();   // act_fn (egcl.py:11)
 
   // split-precision range check: an fp16 / bf16 operand past its range makes the
   // MFMA products inf / NaN; the per-pair scalars where the reference's own ops
@@ -1441,7 +1557,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // (split-precision GEMM0 accumulators carry edge_nn.0's 2^s: unscaled in the bias fma)
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 y = silu4s((f32x4){x0[0][4 * g4], x0[0][4 * g4 + 1], x0[0][4 * g4 + 2], x0[0][4 * g4 + 3]}, c0, K0);
+      const f32x4 y = act4s<VAR>((f32x4){x0[0][4 * g4], x0[0][4 * g4 + 1], x0[0][4 * g4 + 2], x0[0][4 * g4 + 3]},
+                                 c0, K0, ik0, act);
 #pragma unroll
       for (int u = 0; u < 4; ++u) x0[0][4 * g4 + u] = y[u];
     }
@@ -1453,7 +1570,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     chain_prec_fill<PREC, NT, 2>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
-        const f32x4 y = silu4s((f32x4){x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3]}, c0, K0);
+        const f32x4 y = act4s<VAR>((f32x4){x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3]},
+                                   c0, K0, ik0, act);
 #pragma unroll
         for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = y[u];
       }
@@ -1461,7 +1579,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     STAMP(11);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 y = silu4s((f32x4){e[0][4 * g4], e[0][4 * g4 + 1], e[0][4 * g4 + 2], e[0][4 * g4 + 3]}, c1, K1);
+      const f32x4 y = act4s<VAR>((f32x4){e[0][4 * g4], e[0][4 * g4 + 1], e[0][4 * g4 + 2], e[0][4 * g4 + 3]},
+                                 c1, K1, ik1, act);
 #pragma unroll
       for (int u = 0; u < 4; ++u) e[0][4 * g4 + u] = y[u];
     }
@@ -1471,7 +1590,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4)
 #pragma unroll
-          for (int u = 0; u < 4; ++u) e[t][4 * g4 + u] = silu_sc(e[t][4 * g4 + u], c1, K1);
+          for (int u = 0; u < 4; ++u) e[t][4 * g4 + u] = act_sc<VAR>(e[t][4 * g4 + u], c1, K1, ik1, act);
       float d = 0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -1539,8 +1658,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
           if (seg_end) *slot = old + (f32x4){v[0], v[1], v[2], v[3]};
         }
         if (t + 1 < NT && !v_att) {
-          const f32x4 y = silu4s((f32x4){e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
-                                         e[t + 1][4 * g4 + 3]}, c1, K1);
+          const f32x4 y = act4s<VAR>((f32x4){e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
+                                             e[t + 1][4 * g4 + 3]}, c1, K1, ik1, act);
 #pragma unroll
           for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
         }
@@ -1552,8 +1671,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
           const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * tp + 8 * g4 + 4 * hh);
-          const f32x4 y = silu4s((f32x4){hc[tp][4 * g4], hc[tp][4 * g4 + 1], hc[tp][4 * g4 + 2], hc[tp][4 * g4 + 3]},
-                                 c2, K2);
+          const f32x4 y = act4s<VAR>((f32x4){hc[tp][4 * g4], hc[tp][4 * g4 + 1], hc[tp][4 * g4 + 2],
+                                             hc[tp][4 * g4 + 3]}, c2, K2, ik2, act);
 #pragma unroll
           for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
         }
@@ -1617,7 +1736,7 @@ __device__ __forceinline__ void node_partials_reduce(Smem<H, NMAX, RB>& sm, cons
 //   act         = silu(node_nn.0 [h, agg])                               (32 features)
 //   G partial   = node_nn.2[:, 32tp..] . act
 // and the NT partials are summed in fixed order (deterministic).
-template <int H, int NMAX, int RB>
+template <int H, int NMAX, int RB, bool VAR = false>
 __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                            int n, int nf, int tid, int r0, int rb) {
   constexpr int NT = H / 32;
@@ -1627,6 +1746,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
   const int j = lane & 31, hh = lane >> 5;
   const int nh = (nf + 1) >> 1;
   const rsrc_t W = weights_rsrc(Lp, L.total);
+  const Act act = VAR ? act_of(Lp + L.vfl + 1) : act_silu();
   for (int item = w; item < NT * NA; item += WAVES) {
     const int tp = item % NT, at = item / NT;
     const int a = at * 32 + j;              // row within the block
@@ -1646,7 +1766,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
       const f32x4 b1 = bload4(W, (f0 - 32 * tp) * 4, (L.bv1 + 32 * tp) * 4);   // lane part in voffset
       const f32x4 w2 = bload4(W, (f0 - 32 * tp) * 4, (L.wv2 + 32 * tp) * 4);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(acc[4 * g4 + u] + b1[u]);
+      for (int u = 0; u < 4; ++u) part += w2[u] * act_v<VAR>(act, acc[4 * g4 + u] + b1[u]);
     }
     part += __shfl_xor(part, 32, 64);
     if (hh == 0 && va) sm.u.nd.qp[tp][a] = part;
@@ -1670,7 +1790,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 b1 = bload4(W, (8 * g4 + 4 * hh) * 4, (L.bn1 + 32 * tp) * 4);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(acc[4 * g4 + u] + b1[u]);
+      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = act_v<VAR>(act, acc[4 * g4 + u] + b1[u]);
     }
     // node_nn.2 partial: rows q = rho(r, hh), only r < NFMAX / 2 (q < NFMAX) can be < nf
     f32x16 gacc = (f32x16)0.f;
@@ -1694,7 +1814,7 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
 
 // F16X3 node phase: same items and outputs as node_phase, all products on
 // v_mfma_f32_32x32x16_f16 with hi/lo split operands (atoms on the pair lanes).
-template <int H, int NMAX, int RB>
+template <int H, int NMAX, int RB, bool VAR = false>
 __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                               int n, int nf, int tid, int r0, int rb) {
   constexpr int NT = H / 32;
@@ -1705,6 +1825,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
   const int j = lane & 31, hh = lane >> 5;
   const rsrc_t W = weights_rsrc(Lp, L.total);
   const float inv_v1 = Lp[L.scl + 7], inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
+  const Act act = VAR ? act_of(Lp + L.vfl + 1) : act_silu();
   const int vo = lane * 32;
   // every fragment of the wave's first item is requested before the bias
   // staging barrier, so the L2 round trips overlap instead of serialising
@@ -1761,7 +1882,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
       const f32x4 b1 = ld4(sm.bias + f0);
       const f32x4 w2 = ld4(sm.bias + H + f0);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(acc[4 * g4 + u], inv_v1, b1[u]));
+      for (int u = 0; u < 4; ++u) part += w2[u] * act_v<VAR>(act, fmaf(acc[4 * g4 + u], inv_v1, b1[u]));
     }
     part += __shfl_xor(part, 32, 64);
     if (hh == 0 && va) sm.u.nd.qp[tp][a] = part;
@@ -1793,7 +1914,7 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
     for (int g4 = 0; g4 < 4; ++g4) {
       const f32x4 b1 = ld4(sm.bias + 2 * H + 32 * tp + 8 * g4 + 4 * hh);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
+      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = act_v<VAR>(act, fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
     }
     // node_nn.2 partial: rows q = rho(r, hh), only r < NFMAX / 2 (q < NFMAX) can be < nf
     f32x16 gacc = (f32x16)0.f;
@@ -1854,7 +1975,7 @@ struct NoiseSrc {
 
 // ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
 // returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
-template <int H, int NMAX, int RB>
+template <int H, int NMAX, int RB, bool VAR = false>
 __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const NoiseSrc noise,
                                 int a0, int n, int nf) {
   using S = Smem<H, NMAX, RB>;
@@ -1867,6 +1988,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
   const int tid = threadIdx.x;
   float* net = sm.u.net;
   float lq = 0.f;
+  const Act aact = VAR ? act_of(Dp + L.act) : act_silu();   // network.1 (argmax.py:7)
   // network.2.weight staged in the (still unused) edge_nn.0 fragment buffer: the
   // output loop then reads both operands as float4 from LDS
   constexpr bool WLDS = S::W1X_LDS && ACT % 4 == 0 && sizeof(sm.w1x) >= sizeof(float) * 2 * NFMAX * H;
@@ -1882,7 +2004,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
         for (int a = grp; a < cn; a += NG) {
           float v = b;
           for (int q = 0; q < nf; ++q) v += Dp[L.wa1t + q * H + k] * sm.h[(c0 + a) * NFP + q];
-          act[a * ACT + k] = silu_f(v);
+          act[a * ACT + k] = act_v<VAR>(aact, v);
         }
       }
     }

@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
 
   if (!REV) {
     if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-      ldj += argmax_dequant(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+      ldj += argmax_dequant<H, NMAX, RB, VAR>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
     } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
       for (int e = tid; e < n * nf; e += BLOCK) {
         const int a = e / nf, q = e - a * nf;
@@ -138,8 +138,8 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       }
       STAMP(4);
       {
-        if constexpr (PREC != PREC_F32) node_phase_x3(sm, Lp, L, n, nf, tid_l, r0, rb);   // fp32-accurate
-        else node_phase(sm, Lp, L, n, nf, tid_l, r0, rb);
+        if constexpr (PREC != PREC_F32) node_phase_x3<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid_l, r0, rb);   // fp32-accurate
+        else node_phase<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid_l, r0, rb);
       }
       STAMP(5);
       if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q

@@ -43,8 +43,8 @@ class LFIntegrator(BaseFlow):
             p = _lib.PRECISIONS[self.gemm_precision]
         except KeyError:
             raise ValueError(f"gemm_precision must be one of {sorted(_lib.PRECISIONS)}") from None
-        if any(isinstance(n, EGCL) and n.variant_flags() for n in self.networks):
-            p |= _lib.EGCL_VARIANTS      # attention / norm_diff / tanh layers: variant-capable kernels
+        if self._has_variants():
+            p |= _lib.EGCL_VARIANTS      # attention / norm_diff / tanh / act_fn layers: variant-capable kernels
         return p
 
     def make_networks(self, network):
@@ -128,7 +128,10 @@ class LFIntegrator(BaseFlow):
         return self._train_bufs
 
     def _has_variants(self):
-        return any(isinstance(n, EGCL) and n.variant_flags() for n in self.networks)
+        """Layers with constructor variants or a non-SiLU act_fn, or an ArgMax
+        dequantiser with a non-SiLU activation: the variant-capable kernels."""
+        return (any(isinstance(n, EGCL) and n.variant_flags() for n in self.networks)
+                or (isinstance(self.dequantize, ArgMax) and self.dequantize.generic_act()))
 
     def _check_trainable(self):
         """The HIP backward covers every EGCL constructor variant (attention,

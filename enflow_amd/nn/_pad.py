@@ -2,12 +2,13 @@
 
 The reference accepts any ``hidden_nf`` and any ``input_nf`` / ``output_nf``
 (enflow/nn/egcl.py:11, enflow/nn/argmax.py:6).  The kernels are compiled for
-hidden widths 32 / 64 / 128 and one node-feature width ``nf`` (<= 8) for both
+hidden widths 32 / 64 / 128 and one node-feature width ``nf`` (<= 16) for both
 the input and the output features.  Other shapes are embedded in the next
 compiled one with zero weights and biases, which is exact:
 
-* a padded hidden unit has pre-activation 0, SiLU(0) = 0, and zero outgoing
-  weights;
+* a padded hidden unit has pre-activation 0 and zero outgoing weights, so
+  whatever act_fn(0) is (SiLU(0) = 0, Sigmoid(0) = 0.5, Softplus(0) = log 2)
+  it reaches no output, and its adjoint (zero outgoing weights) is 0;
 * a padded input feature is a zero column of h with zero incoming weights;
 * a padded output feature of node_nn.2 has zero weights and bias (G's extra
   columns are 0 and are sliced away).

@@ -10,6 +10,7 @@ from torch import nn
 
 from .. import _lib
 from ..utils.helpers import one_hot, mol_ptr_from_counts
+from ._act import SILU, act_code
 from ._pad import ARGMAX_HDIMS, Geom, flat_padded, kernel_hidden
 
 
@@ -33,7 +34,18 @@ class ArgMax(nn.Module):
         width = width or self.kernel_hidden
         if width is None or width < self.hidden_nf:
             raise NotImplementedError(f"ArgMax hidden_nf {self.hidden_nf} past the kernel width {width}")
-        return flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.pad_geom(width), device)
+        flat = flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.pad_geom(width), device)
+        # ABI 10: [act kind, p0, p1, 0] of network.1 after the parameters (argmax.py:7)
+        kind, p0, p1 = self.act()
+        return torch.cat([flat, torch.tensor([float(kind), p0, p1, 0.0], dtype=torch.float32, device=device)])
+
+    def act(self):
+        """(kind, p0, p1) of the network's activation (ENFLOW_ACT_*)."""
+        return act_code(self.network[1])
+
+    def generic_act(self):
+        """True if the activation is not SiLU (the flow then runs its variant-capable kernels)."""
+        return self.act()[0] != SILU
 
     def pad_geom(self, width=None):
         nf = self.node_nf

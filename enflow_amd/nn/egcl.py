@@ -12,6 +12,7 @@ from torch import nn
 
 from .. import _lib
 from ..data.base import Edges
+from ._act import SILU, act_code, supported as act_supported
 from ._pad import EGCL_HDIMS, Geom, flat_padded, kernel_hidden
 
 
@@ -66,11 +67,13 @@ class EGCL(nn.Module):
     def hip_supported(self):
         """The HIP kernels implement every constructor flag of the reference
         (attention, norm_diff, tanh; ``clamp`` is stored and unused there too)
-        with the SiLU activation, input_nf and output_nf <= 16 and any hidden_nf
+        with the activations of nn/_act.py (SiLU, ReLU, LeakyReLU, ELU, CELU, SELU,
+        GELU, Tanh, Sigmoid, Softplus, Mish, Hardtanh / ReLU6, Identity),
+        input_nf and output_nf <= 16 and any hidden_nf
         <= 128 (hidden 32 / 64 / 128 and one feature width compiled, other
         shapes zero-padded)."""
         kh = self.kernel_hidden
-        if not (isinstance(self.act_fn, nn.SiLU) and 1 <= min(self.input_nf, self.output_nf)
+        if not (act_supported(self.act_fn) and 1 <= min(self.input_nf, self.output_nf)
                 and self.kernel_nf <= _lib.MAX_NODE_NF and kh is not None):
             return False
         L = _lib.lib(self.kernel_nf)
@@ -79,13 +82,17 @@ class EGCL(nn.Module):
     def _check_supported(self):
         if not self.hip_supported():
             raise NotImplementedError(
-                "enflow_amd EGCL kernels implement the SiLU activation, input_nf / output_nf <= 16 "
+                "enflow_amd EGCL kernels implement the torch activations of nn/_act.py, input_nf / output_nf <= 16 "
                 "and hidden_nf <= 128")
 
     def variant_flags(self):
         """ENFLOW_EGCL_* flags of this layer's constructor variants (0 = defaults)."""
         return ((_lib.EGCL_ATTENTION if self.attention else 0) | (_lib.EGCL_NORM_DIFF if self.norm_diff else 0)
-                | (_lib.EGCL_TANH if self.tanh else 0))
+                | (_lib.EGCL_TANH if self.tanh else 0) | (_lib.EGCL_ACT if self.act()[0] != SILU else 0))
+
+    def act(self):
+        """(kind, p0, p1) of act_fn (ENFLOW_ACT_*)."""
+        return act_code(self.act_fn)
 
     def raw_named(self):
         """(name, parameter) in the default-flag named_parameters() order the C
@@ -109,9 +116,15 @@ class EGCL(nn.Module):
     def _pack(self, raw, dst, device):
         L = _lib.lib(self.kernel_nf)
         att = self._att_raw(device)
-        _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.kernel_hidden, self.kernel_nf, self.variant_flags(),
-                                             _lib.ptr(att), _lib.ptr(dst), _lib.stream_ptr(device)),
-                   "enflow_pack_egcl_ex_f32")
+        kind, p0, p1 = self.act()
+        if kind == SILU:   # the ABI <= 9 entry (A/B tools load older builds too)
+            _lib.check(L.enflow_pack_egcl_ex_f32(_lib.ptr(raw), self.kernel_hidden, self.kernel_nf,
+                                                 self.variant_flags(), _lib.ptr(att), _lib.ptr(dst),
+                                                 _lib.stream_ptr(device)), "enflow_pack_egcl_ex_f32")
+            return
+        _lib.check(L.enflow_pack_egcl_act_f32(_lib.ptr(raw), self.kernel_hidden, self.kernel_nf, self.variant_flags(),
+                                              kind, p0, p1, _lib.ptr(att), _lib.ptr(dst), _lib.stream_ptr(device)),
+                   "enflow_pack_egcl_act_f32")
 
     def packed(self, device):
         """MFMA-fragment packed fp32 weights on `device` (cached, re-packed when

@@ -105,6 +105,7 @@ int enflow_pack_egcl_f32(const float* raw, int hidden_nf, int node_nf,
 #define ENFLOW_EGCL_ATTENTION 1   /* edge messages *= sigmoid(att_nn(messages)) */
 #define ENFLOW_EGCL_NORM_DIFF 2   /* force uses coord_diff / (|coord_diff| + 1) */
 #define ENFLOW_EGCL_TANH      4   /* phi = tanh(coord_nn(...)) */
+#define ENFLOW_EGCL_ACT       8   /* act_fn is not SiLU (egcl.py:11): kind + parameters packed */
 /* OR into gemm_precision of enflow_lf_forward_f32 / enflow_lf_reverse_f32 when
  * any layer carries ENFLOW_EGCL_* flags (selects the variant-capable kernels;
  * without it the flags in the packed layers are ignored). */
@@ -119,8 +120,38 @@ int enflow_pack_egcl_f32(const float* raw, int hidden_nf, int node_nf,
 int enflow_pack_egcl_ex_f32(const float* raw, int hidden_nf, int node_nf, int flags,
                             const float* att, float* packed, void* stream);
 
+/* Activations (act_fn of EGCL / ArgMax, enflow/nn/egcl.py:11, argmax.py:7):
+ * the torch module's elementwise function, with up to two parameters (p0, p1)
+ * as listed.  Forward and derivative definitions: flow_device.h (act_f / act_d). */
+#define ENFLOW_ACT_SILU        0
+#define ENFLOW_ACT_RELU        1
+#define ENFLOW_ACT_LEAKY_RELU  2   /* p0 = negative_slope */
+#define ENFLOW_ACT_ELU         3   /* p0 = alpha */
+#define ENFLOW_ACT_CELU        4   /* p0 = alpha */
+#define ENFLOW_ACT_SELU        5
+#define ENFLOW_ACT_GELU        6   /* approximate='none' (erf) */
+#define ENFLOW_ACT_GELU_TANH   7   /* approximate='tanh' */
+#define ENFLOW_ACT_TANH        8
+#define ENFLOW_ACT_SIGMOID     9
+#define ENFLOW_ACT_SOFTPLUS   10   /* p0 = beta, p1 = threshold */
+#define ENFLOW_ACT_MISH       11
+#define ENFLOW_ACT_HARDTANH   12   /* p0 = min_val, p1 = max_val (ReLU6 = 0, 6) */
+#define ENFLOW_ACT_IDENTITY   13
+
+/* enflow_pack_egcl_ex_f32 with the layer's act_fn (ABI 10): `flags` carries
+ * ENFLOW_EGCL_ACT exactly when act_kind != ENFLOW_ACT_SILU; every launch on
+ * such layers ORs ENFLOW_EGCL_VARIANTS into its precision / dequant word (the
+ * variant-capable kernels read the activation from the packed layer). */
+int enflow_pack_egcl_act_f32(const float* raw, int hidden_nf, int node_nf, int flags, int act_kind,
+                             float act_p0, float act_p1, const float* att, float* packed, void* stream);
+
 /* Pack ArgMax.network (enflow/nn/argmax.py:6-10): network.0.weight [H][nf],
- * network.0.bias [H], network.2.weight [2nf][H], network.2.bias [2nf]. */
+ * network.0.bias [H], network.2.weight [2nf][H], network.2.bias [2nf], then
+ * (ABI 10) four floats [act kind, p0, p1, 0] for network.1 (ENFLOW_ACT_*; the
+ * same trailing floats on every raw ArgMax vector this ABI takes: the
+ * dequantiser's forward, the flow backward's dequant_raw, the standalone
+ * ArgMax backward).  A non-SiLU ArgMax activation inside a flow needs
+ * ENFLOW_EGCL_VARIANTS on the launches, as the EGCL variants do. */
 int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,
                            float* packed, void* stream);
 

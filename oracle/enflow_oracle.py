@@ -68,6 +68,49 @@ def silu(x):
     return x / (1.0 + np.exp(-x))
 
 
+def activation(code):
+    """The elementwise function of an act_fn code (kind, p0, p1) -- the
+    ENFLOW_ACT_* numbering of include/enflow_hip.h; None = SiLU (the
+    reference's default act_fn, enflow/nn/egcl.py:11).  float64, torch's
+    definitions (torch.nn.{SiLU, ReLU, LeakyReLU, ELU, CELU, SELU, GELU, Tanh,
+    Sigmoid, Softplus, Mish, Hardtanh, Identity})."""
+    if code is None:
+        return silu
+    k, p0, p1 = int(code[0]), float(code[1]), float(code[2])
+    if k == 0:
+        return silu
+    if k == 1:
+        return lambda x: np.maximum(x, 0.0)
+    if k == 2:
+        return lambda x: np.where(x > 0, x, p0 * x)
+    if k == 3:
+        return lambda x: np.where(x > 0, x, p0 * np.expm1(np.minimum(x, 0.0)))
+    if k == 4:
+        return lambda x: np.where(x > 0, x, p0 * np.expm1(np.minimum(x, 0.0) / p0))
+    if k == 5:
+        a, s = 1.6732632423543772848170429916717, 1.0507009873554804934193349852946
+        return lambda x: s * np.where(x > 0, x, a * np.expm1(np.minimum(x, 0.0)))
+    if k == 6:
+        from scipy.special import erf
+        return lambda x: 0.5 * x * (1.0 + erf(x / math.sqrt(2.0)))
+    if k == 7:
+        c = math.sqrt(2.0 / math.pi)
+        return lambda x: 0.5 * x * (1.0 + np.tanh(c * (x + 0.044715 * x ** 3)))
+    if k == 8:
+        return np.tanh
+    if k == 9:
+        return lambda x: 1.0 / (1.0 + np.exp(-x))
+    if k == 10:
+        return lambda x: np.where(x * p0 > p1, x, np.log1p(np.exp(np.minimum(p0 * x, p1))) / p0)
+    if k == 11:
+        return lambda x: x * np.tanh(softplus(x))
+    if k == 12:
+        return lambda x: np.clip(x, p0, p1)
+    if k == 13:
+        return lambda x: x
+    raise ValueError(f"activation code {k}")
+
+
 def softplus(x):
     """torch.nn.functional.softplus(beta=1, threshold=20)."""
     return np.where(x > 20.0, x, np.log1p(np.exp(np.minimum(x, 20.0))))
@@ -182,6 +225,7 @@ def egcl_forward(p, h, row, col, cdiff, coords_weight=1.0):
     ``flags`` = (attention, norm_diff, tanh) and, with attention,
     ``att_nn.0.weight`` / ``att_nn.0.bias``.  Returns (Q [n,1], F [n,3], G [n,nf])."""
     attention, norm_diff, tanh = (bool(x) for x in p.get("flags", (0, 0, 0)))
+    silu = activation(p.get("act"))   # act_fn (egcl.py:11); SiLU by default
     n = h.shape[0]
     radial = np.sum(cdiff ** 2, axis=1, keepdims=True)                 # egcl.py:79
     if norm_diff:                                                        # egcl.py:82-84
@@ -213,7 +257,8 @@ def argmax_forward(p, h, eps):
     """ArgMax.forward (enflow/nn/argmax.py:13-25) with the Gaussian draw
     ``torch.randn(h.size())`` supplied as ``eps``.  Returns (z, log_q)."""
     nf = h.shape[1]
-    net = linear(silu(linear(h, p["network.0.weight"], p["network.0.bias"])),
+    act = activation(p.get("act"))    # act_fn (argmax.py:7)
+    net = linear(act(linear(h, p["network.0.weight"], p["network.0.bias"])),
                  p["network.2.weight"], p["network.2.bias"])
     log_scale, translate = net[:, :nf], net[:, nf:]
     u = translate + eps * np.exp(log_scale)

@@ -29,15 +29,30 @@ def _silu(x):
     return x * torch.sigmoid(x)
 
 
+def _activation(code):
+    """torch form of enflow_oracle.activation (same numbering)."""
+    if code is None:
+        return _silu
+    k, p0, p1 = int(code[0]), float(code[1]), float(code[2])
+    table = {
+        0: _silu, 1: F.relu, 2: lambda x: F.leaky_relu(x, p0), 3: lambda x: F.elu(x, p0),
+        4: lambda x: F.celu(x, p0), 5: F.selu, 6: lambda x: F.gelu(x), 7: lambda x: F.gelu(x, approximate="tanh"),
+        8: torch.tanh, 9: torch.sigmoid, 10: lambda x: F.softplus(x, p0, p1), 11: F.mish,
+        12: lambda x: F.hardtanh(x, p0, p1), 13: lambda x: x,
+    }
+    return table[k]
+
+
 def _pbc(x, box):
     """enflow/utils/helpers.py:7-8 (round has zero gradient)."""
     return x - torch.round(x / box) * box
 
 
-def _egcl(p, h, pos, row, col, eb, n, cw, flags=(False, False, False)):
+def _egcl(p, h, pos, row, col, eb, n, cw, flags=(False, False, False), act=None):
     """EGCL.forward (enflow/nn/egcl.py:57-92); ``flags`` = the constructor's
     (attention, norm_diff, tanh)."""
     attention, norm_diff, tanh = (bool(x) for x in flags)
+    _silu = _activation(act)                                                   # act_fn (egcl.py:11)
     cd = _pbc(pos[row] - pos[col], eb * 0.5)                                   # base.py:15-19
     radial = (cd ** 2).sum(1, keepdim=True)
     if norm_diff:                                                              # egcl.py:82-84
@@ -63,10 +78,10 @@ def _egcl(p, h, pos, row, col, eb, n, cw, flags=(False, False, False)):
     return q, f, g
 
 
-def _argmax(p, h, eps):
+def _argmax(p, h, eps, act=None):
     """ArgMax.forward (enflow/nn/argmax.py:13-25)."""
     nf = h.shape[1]
-    net = F.linear(_silu(F.linear(h, p["network.0.weight"], p["network.0.bias"])),
+    net = F.linear(_activation(act)(F.linear(h, p["network.0.weight"], p["network.0.bias"])),
                    p["network.2.weight"], p["network.2.bias"])
     ls, tr = net[:, :nf], net[:, nf:]
     u = tr + eps * ls.exp()
@@ -99,17 +114,17 @@ def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partit
 
     Returns (loss, ldj, [layer grad dicts], dequant grad dict, output state)."""
     t = lambda a: torch.tensor(np.asarray(a, dtype=np.float64))  # noqa: E731
-    P = [{k: t(v).requires_grad_(True) for k, v in p.items() if k != "flags"} for p in layers]
-    D = {k: t(v).requires_grad_(True) for k, v in dequant.items()}
+    P = [{k: t(v).requires_grad_(True) for k, v in p.items() if k not in ("flags", "act")} for p in layers]
+    D = {k: t(v).requires_grad_(True) for k, v in dequant.items() if k != "act"}
     mol_ptr = np.asarray(state["mol_ptr"], dtype=np.int64)
     n = int(mol_ptr[-1])
     box, r_cut = t(state["box"]), np.asarray(state["r_cut"], dtype=np.float64)
-    h, ldj = _argmax(D, t(state["h"]), t(eps))
+    h, ldj = _argmax(D, t(state["h"]), t(eps), dequant.get("act"))
     g, pos, vel = t(state["g"]), t(state["pos"]), t(state["vel"])
     for p, lp in zip(P, layers):
         row, col, eb = O.batch_edges(pos.detach().numpy(), state["box"], r_cut, mol_ptr)
         row_t, col_t = torch.as_tensor(row, dtype=torch.long), torch.as_tensor(col, dtype=torch.long)
-        q, f, gg = _egcl(p, h, pos, row_t, col_t, t(eb), n, coords_weight, lp.get("flags", (0, 0, 0)))
+        q, f, gg = _egcl(p, h, pos, row_t, col_t, t(eb), n, coords_weight, lp.get("flags", (0, 0, 0)), lp.get("act"))
         vel = torch.exp(q) * vel + f * dt
         g = g + gg * dt
         pos = _pbc(pos + vel * dt, box)

@@ -29,10 +29,24 @@ def load(name):
     return inp, out
 
 
+def act_module(code):
+    """torch activation module of an act_fn code (kind, p0, p1) -- the
+    ENFLOW_ACT_* numbering; None: nn.SiLU (the reference's default)."""
+    from torch import nn
+    if code is None:
+        return nn.SiLU()
+    k, p0, p1 = int(code[0]), float(code[1]), float(code[2])
+    return [nn.SiLU, nn.ReLU, lambda: nn.LeakyReLU(p0), lambda: nn.ELU(p0), lambda: nn.CELU(p0), nn.SELU,
+            nn.GELU, lambda: nn.GELU(approximate="tanh"), nn.Tanh, nn.Sigmoid, lambda: nn.Softplus(p0, p1),
+            nn.Mish, lambda: nn.Hardtanh(p0, p1), nn.Identity][k]()
+
+
 def layer_params(inp, i, dtype=np.float64):
     p = {k: inp[f"p{i}.{k}"].astype(dtype) for k in EGCL_KEYS}
     flags = layer_flags(inp, i)
     p["flags"] = flags
+    if f"p{i}.act" in inp:
+        p["act"] = tuple(float(x) for x in inp[f"p{i}.act"])
     if flags[0]:
         p.update({k: inp[f"p{i}.{k}"].astype(dtype) for k in ATT_KEYS})
     return p
@@ -43,14 +57,17 @@ def egcl_from_fixture(inp, i, nf, hid):
     import torch
     from enflow_amd.nn import EGCL
     att, nd, th = layer_flags(inp, i)
-    net = EGCL(nf, nf, hid, attention=att, norm_diff=nd, tanh=th)
+    net = EGCL(nf, nf, hid, attention=att, norm_diff=nd, tanh=th, act_fn=act_module(inp.get(f"p{i}.act")))
     keys = EGCL_KEYS + (ATT_KEYS if att else ())
     net.load_state_dict({k: torch.tensor(inp[f"p{i}.{k}"]) for k in keys})
     return net
 
 
 def dequant_params(inp, dtype=np.float64):
-    return {k: inp[f"dq.{k}"].astype(dtype) for k in ARGMAX_KEYS}
+    p = {k: inp[f"dq.{k}"].astype(dtype) for k in ARGMAX_KEYS}
+    if "dq.act" in inp:
+        p["act"] = tuple(float(x) for x in inp["dq.act"])
+    return p
 
 
 def state(inp, dtype=np.float64):
@@ -127,7 +144,7 @@ def flow_from_fixture(inp, device="cuda"):
 
     hid, nf, nl = int(inp["hid"]), inp["h"].shape[1], int(inp["n_layers"])
     nets = [egcl_from_fixture(inp, i, nf, hid) for i in range(nl)]
-    am = ArgMax(nf, hid)
+    am = ArgMax(nf, hid, act_fn=act_module(inp.get("dq.act")))
     am.load_state_dict({k: torch.tensor(inp[f"dq.{k}"]) for k in ARGMAX_KEYS})
     model = LFIntegrator(nets, am, dt=float(inp["dt"])).to(device)
     return model, data_from_fixture(inp, device)

@@ -131,7 +131,9 @@ def save(name, inputs, outputs):
     out = {}
     for k, v in inputs.items():
         v = np.asarray(v)
-        out["in_" + k] = v.astype(np.float32) if (v.dtype.kind == "f" and v.ndim > 0) else v
+        # act_fn codes keep their float64 parameters (the reference's module holds doubles)
+        keep = k.endswith(".act")
+        out["in_" + k] = v.astype(np.float32) if (v.dtype.kind == "f" and v.ndim > 0 and not keep) else v
     for k, v in outputs.items():
         out["out_" + k] = np.asarray(v, dtype=np.float64) if np.asarray(v).dtype.kind == "f" else np.asarray(v)
     path = os.path.join(HERE, name + ".npz")
@@ -149,14 +151,25 @@ def case_edges():
                                  "coord_diff": e.coord_diff.numpy()})
 
 
-def case_egcl(hid, seed, nf=5, name=None):
+def act_fn_of(code):
+    """torch activation module of an ENFLOW_ACT_* code (kind, p0, p1)."""
+    from torch import nn
+    k, p0, p1 = code
+    return [nn.SiLU, nn.ReLU, lambda: nn.LeakyReLU(p0), lambda: nn.ELU(p0), lambda: nn.CELU(p0), nn.SELU,
+            nn.GELU, lambda: nn.GELU(approximate="tanh"), nn.Tanh, nn.Sigmoid, lambda: nn.Softplus(p0, p1),
+            nn.Mish, lambda: nn.Hardtanh(p0, p1), nn.Identity][k]()
+
+
+def case_egcl(hid, seed, nf=5, name=None, act=None):
     torch.manual_seed(seed)
-    net = EGCL(nf, nf, hid).double()
+    net = (EGCL(nf, nf, hid) if act is None else EGCL(nf, nf, hid, act_fn=act_fn_of(act))).double()
     b = batch_inputs(4, [22, 9, 15, 3], nf, seed=seed, one_hot=False)
     d = ref_data(b)
     q, f, g = net(d.h, d.edges)
     inp = dict(b)
     inp.update(params_of(net, "p0."))
+    if act is not None:
+        inp["p0.act"] = np.array(act, dtype=np.float64)
     save(name or f"egcl_h{hid}", inp, {"Q": q.detach().numpy(), "F": f.detach().numpy(),
                                        "G": g.detach().numpy()})
 
@@ -193,15 +206,18 @@ def case_argmax(hid, seed):
                                  "reverse": rev.numpy()})
 
 
-def case_flow(hid, n_layers, sizes, seed, name, flags=None, nf=5):
-    """``flags``: per layer (attention, norm_diff, tanh), default flags when None."""
+def case_flow(hid, n_layers, sizes, seed, name, flags=None, nf=5, act=None, dq_act=None):
+    """``flags``: per layer (attention, norm_diff, tanh), default flags when None;
+    ``act`` / ``dq_act``: act_fn codes of the EGCL layers / the ArgMax (None: SiLU)."""
     torch.manual_seed(seed)
     dt = default_dt()
+    akw = {} if act is None else {"act_fn": act_fn_of(act)}
     if flags is None:
-        nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+        nets = [EGCL(nf, nf, hid, **akw) for _ in range(n_layers)]
     else:
-        nets = [EGCL(nf, nf, hid, attention=a, norm_diff=nd, tanh=th) for a, nd, th in flags]
-    model = LFIntegrator(nets, ArgMax(nf, hid), dt=dt)   # BaseFlow casts to float64
+        nets = [EGCL(nf, nf, hid, attention=a, norm_diff=nd, tanh=th, **akw) for a, nd, th in flags]
+    am = ArgMax(nf, hid) if dq_act is None else ArgMax(nf, hid, act_fn=act_fn_of(dq_act))
+    model = LFIntegrator(nets, am, dt=dt)   # BaseFlow casts to float64
     b = batch_inputs(len(sizes), sizes, nf, seed=seed)
     d = ref_data(b)
     torch.manual_seed(seed + 1)
@@ -231,23 +247,29 @@ def case_flow(hid, n_layers, sizes, seed, name, flags=None, nf=5):
         inp.update(params_of(net, f"p{i}."))
         if flags is not None:
             inp[f"p{i}.flags"] = np.array(flags[i], dtype=np.int32)
+        if act is not None:
+            inp[f"p{i}.act"] = np.array(act, dtype=np.float64)
     inp.update(params_of(model.dequantize, "dq."))
+    if dq_act is not None:
+        inp["dq.act"] = np.array(dq_act, dtype=np.float64)
     fwd.update(rev)
     save(name, inp, fwd)
 
 
-def case_train(hid, n_layers, sizes, seed, name, nf=5, flags=None):
+def case_train(hid, n_layers, sizes, seed, name, nf=5, flags=None, act=None, dq_act=None):
     """One training step of the reference (enflow/main.py:217-221):
     out, ldj = model(data); loss = nll(out, ldj); loss.backward() -- the
     parameter gradients of every EGCL layer and of the ArgMax dequantiser.
     ``flags``: per layer (attention, norm_diff, tanh), default flags when None."""
     torch.manual_seed(seed)
     dt = default_dt()
+    akw = {} if act is None else {"act_fn": act_fn_of(act)}
     if flags is None:
-        nets = [EGCL(nf, nf, hid) for _ in range(n_layers)]
+        nets = [EGCL(nf, nf, hid, **akw) for _ in range(n_layers)]
     else:
-        nets = [EGCL(nf, nf, hid, attention=a, norm_diff=nd, tanh=th) for a, nd, th in flags]
-    model = LFIntegrator(nets, ArgMax(nf, hid), dt=dt)   # BaseFlow casts to float64
+        nets = [EGCL(nf, nf, hid, attention=a, norm_diff=nd, tanh=th, **akw) for a, nd, th in flags]
+    am = ArgMax(nf, hid) if dq_act is None else ArgMax(nf, hid, act_fn=act_fn_of(dq_act))
+    model = LFIntegrator(nets, am, dt=dt)   # BaseFlow casts to float64
     b = batch_inputs(len(sizes), sizes, nf, seed=seed)
     d = ref_data(b)
     torch.manual_seed(seed + 1)
@@ -271,8 +293,12 @@ def case_train(hid, n_layers, sizes, seed, name, nf=5, flags=None):
         res.update({f"grad_p{i}.{k}": v.grad.numpy() for k, v in net.named_parameters()})
         if flags is not None:
             inp[f"p{i}.flags"] = np.array(flags[i], dtype=np.int32)
+        if act is not None:
+            inp[f"p{i}.act"] = np.array(act, dtype=np.float64)
     inp.update({f"dq.{k}": v.detach().numpy().astype(np.float32)
                 for k, v in model.dequantize.named_parameters()})
+    if dq_act is not None:
+        inp["dq.act"] = np.array(dq_act, dtype=np.float64)
     res.update({f"grad_dq.{k}": v.grad.numpy() for k, v in model.dequantize.named_parameters()})
     save(name, inp, res)
 
@@ -374,6 +400,21 @@ if __name__ == "__main__":
         case_flow(64, 3, [22, 9, 15, 3], 34, "lf_var_h64_L3",
                   flags=[(True, False, False), (False, True, True), (True, True, True)])
         case_flow(128, 2, [22, 22, 30], 35, "lf_var_h128_L2", flags=[(False, True, False), (True, False, True)])
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "act":
+        # act_fn other than SiLU (enflow/nn/egcl.py:11, enflow/nn/argmax.py:7); codes
+        # (kind, p0, p1) as ENFLOW_ACT_*: every kind through one EGCL forward each
+        codes = {"relu": (1, 0, 0), "leaky": (2, 0.05, 0), "elu": (3, 0.7, 0), "celu": (4, 1.3, 0),
+                 "selu": (5, 0, 0), "gelu": (6, 0, 0), "gelutanh": (7, 0, 0), "tanh": (8, 0, 0),
+                 "sigmoid": (9, 0, 0), "softplus": (10, 1.5, 20.0), "mish": (11, 0, 0), "relu6": (12, 0.0, 6.0),
+                 "identity": (13, 0, 0)}
+        for i, (tag, code) in enumerate(codes.items()):
+            case_egcl(32, 70 + i, act=code, name=f"egcl_act_{tag}")
+        case_flow(64, 2, [22, 9, 15], 90, "lf_act_tanh_h64_L2", act=(8, 0, 0), dq_act=(8, 0, 0))
+        case_flow(128, 2, [22, 13], 91, "lf_act_gelu_h128_L2", act=(6, 0, 0), dq_act=(9, 0, 0))
+        case_train(32, 2, [22, 9, 15], 92, "train_act_tanh_h32_L2", act=(8, 0, 0), dq_act=(8, 0, 0))
+        case_train(64, 2, [22, 17], 93, "train_act_elu_h64_L2", act=(3, 0.7, 0), dq_act=(10, 1.5, 20.0),
+                   flags=[(True, True, False), (False, False, True)])
         sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "wide_nf":
         # node_nf past 8 (the dataset decides it: enflow/main.py:148-151): the

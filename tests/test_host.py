@@ -38,7 +38,7 @@ def test_node_feature_library_selection():
     assert _lib.lib_path(5) == _lib.lib_path(None) == _lib.LIB_PATH
     assert _lib.lib_path(8) == _lib.LIB_PATH and _lib.lib_path(9) == _lib.LIB_NF16_PATH
     L16 = _lib.lib(16)
-    assert L16.enflow_abi_version() == 9 and L16.enflow_max_node_nf() == 16
+    assert L16.enflow_abi_version() == 10 and L16.enflow_max_node_nf() == 16
     assert L16.enflow_egcl_packed_size(128, 16) > 0 and L16.enflow_egcl_packed_size(128, 17) == -1
     # training: 2 nf + 1 <= 32 edge inputs (one output tile of the transposed edge_nn.0 GEMM)
     assert L16.enflow_lf_backward_workspace_size(4, 88, 15, 128, 2, 4 * 480) > 0
@@ -49,7 +49,7 @@ def test_node_feature_library_selection():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 9
+    assert L.enflow_abi_version() == 10
     assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
@@ -238,3 +238,28 @@ def test_feature_padding_is_exact_on_cpu(fin, fout):
     np.testing.assert_allclose(f.numpy(), fp.numpy(), rtol=1e-13, atol=1e-15)
     np.testing.assert_allclose(gg.numpy(), ggp[:, :fout].numpy(), rtol=1e-13, atol=1e-15)
     assert float(ggp[:, fout:].abs().max()) == 0.0 if g.F > fout else True
+
+
+def test_activation_codes_and_variant_flags():
+    """act_fn -> ENFLOW_ACT_* codes (include/enflow_hip.h); a non-SiLU act_fn
+    marks the layer ENFLOW_EGCL_ACT (variant-capable kernels), the ArgMax raw
+    vector carries the [kind, p0, p1, 0] trailer (ABI 10)."""
+    from torch import nn
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.nn._act import act_code
+    assert act_code(nn.SiLU()) == (0, 0.0, 0.0)
+    assert act_code(nn.LeakyReLU(0.2))[:2] == (2, 0.2)
+    assert act_code(nn.ReLU6()) == (12, 0.0, 6.0)
+    assert act_code(nn.GELU(approximate="tanh"))[0] == 7
+    assert act_code(nn.Softplus(2.0, 10.0)) == (10, 2.0, 10.0)
+    with pytest.raises(NotImplementedError):
+        act_code(nn.PReLU())
+    assert EGCL(5, 5, 32).variant_flags() == 0
+    assert EGCL(5, 5, 32, act_fn=nn.Tanh()).variant_flags() == _lib.EGCL_ACT
+    assert EGCL(5, 5, 32, act_fn=nn.Tanh()).hip_supported() in (True, False)   # needs only the library
+    assert not EGCL(5, 5, 32, act_fn=nn.PReLU()).hip_supported()
+    am = ArgMax(5, 32, act_fn=nn.ELU(0.5))
+    raw = am.kernel_raw("cpu")
+    assert raw.numel() == sum(p.numel() for p in am.parameters()) + 4
+    assert raw[-4:].tolist() == [3.0, 0.5, 0.0, 0.0]
+    assert am.generic_act() and not ArgMax(5, 32).generic_act()

@@ -33,8 +33,12 @@ def test_edges_quirk_is_exercised():
     assert non_identity > 0
 
 
+ACTS = ["relu", "leaky", "elu", "celu", "selu", "gelu", "gelutanh", "tanh", "sigmoid", "softplus", "mish",
+        "relu6", "identity"]
+
+
 @pytest.mark.parametrize("name", ["egcl_h32", "egcl_h128", "egcl_h64_att", "egcl_h32_nd_tanh", "egcl_h128_all",
-                                  "egcl_nf16_h128"])
+                                  "egcl_nf16_h128"] + [f"egcl_act_{a}" for a in ACTS])
 def test_egcl_matches_reference(name):
     """Default flags and the constructor variants (attention, norm_diff, tanh)."""
     inp, out = load(name)
@@ -57,7 +61,7 @@ def test_argmax_matches_reference():
 
 
 @pytest.mark.parametrize("name", ["lf_h32_L3", "lf_h64_L2", "lf_h128_L2", "lf_var_h64_L3", "lf_var_h128_L2",
-                                  "lf_nf12_h64_L2", "lf_nf16_h32_L2"])
+                                  "lf_nf12_h64_L2", "lf_nf16_h32_L2", "lf_act_tanh_h64_L2", "lf_act_gelu_h128_L2"])
 def test_lf_flow_matches_reference(name):
     inp, out = load(name)
     layers = [layer_params(inp, i) for i in range(n_layers(inp))]
@@ -83,7 +87,8 @@ def test_multiplicity_roundtrip():
 
 
 TRAIN_CASES = ["train_h32_L3", "train_h128_L2", "train_h64_L2", "train_var_h64_L2", "train_var_h32_L3",
-               "train_att_h64_L2", "train_att_h32_L3", "train_nf12_h32_L2", "train_nf15_h128_L2"]
+               "train_att_h64_L2", "train_att_h32_L3", "train_nf12_h32_L2", "train_nf15_h128_L2",
+               "train_act_tanh_h32_L2", "train_act_elu_h64_L2"]
 
 
 @pytest.mark.parametrize("name", TRAIN_CASES)
