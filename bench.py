@@ -253,10 +253,35 @@ class FlowRunner:
             raise RuntimeError(f"flow kernel error flag {int(self.err.item())}")
 
 
+PREWARM_S = 0.5   # untimed clock pre-warm (s) before the W warmup steps (--prewarm-s)
+
+
+def set_prewarm(seconds):
+    global PREWARM_S
+    PREWARM_S = max(0.0, float(seconds))
+
+
 def timed(step, steps, warmup, dist, device):
-    """W untimed steps, then K steps between barrier + synchronize on both
-    sides; returns the MAX elapsed seconds over ranks."""
+    """An untimed clock pre-warm (steps for PREWARM_S seconds: the MI355X
+    ramps its shader clock over the first ~20 launches), W
+    untimed steps, then K steps between barrier + synchronize on both sides;
+    returns the MAX elapsed seconds over ranks."""
     from enflow_amd.distributed import max_over_ranks
+    if PREWARM_S > 0:
+        # the same number of steps on every rank (a training step holds a
+        # collective): timed from 2 steps, max over ranks
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        n = min(4000, int(PREWARM_S / max((time.perf_counter() - t0) / 2, 1e-5)))
+        n = int(max_over_ranks(float(n), device)) if dist else n
+        for i in range(n):
+            step()
+            if i % 8 == 7:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
@@ -718,6 +743,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=30,
                     help="untimed steps first: the first ~20 launches run while the clock ramps up")
+    ap.add_argument("--prewarm-s", type=float, default=PREWARM_S,
+                    help="untimed clock pre-warm (seconds of steps) before the warmup steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--sync-errors", action="store_true",
                     help="train / lj_train: read the forward's error word before the forward returns (the module "
@@ -734,6 +761,7 @@ def main():
     ap.add_argument("--atoms", type=int, default=None,
                     help="train mode: atoms per molecule (default 64); lj mode: atoms per box (default 2944)")
     args = ap.parse_args()
+    set_prewarm(args.prewarm_s)
 
     if args.cpu_baseline_only:
         print(json.dumps(cpu_baseline(args.cpu_per_core)), flush=True)

@@ -2192,7 +2192,7 @@ struct BwdWs {
   size_t part_floats;
 };
 
-static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, long long prb) {
+static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, long long prb, int nbuf_cap = BWD_NBUF) {
   BwdWs W;
   size_t o = 0;
   const size_t P = (size_t)prb, A = (size_t)num_atoms;
@@ -2223,7 +2223,7 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.span = o;
   // fused layer chains of >= BWD_NBUF layers rotate BWD_NBUF buffers; the
   // large-system path (n_layers 0 here) and single-layer callers use two
-  W.nbuf = n_layers >= BWD_NBUF ? BWD_NBUF : 2;
+  W.nbuf = n_layers >= nbuf_cap ? nbuf_cap : 2;
   W.total = W.buf0 + (size_t)W.nbuf * W.span;
   return W;
 }
@@ -2474,6 +2474,13 @@ int64_t enflow_lf_backward_workspace_size(int num_mols, int num_atoms, int nf, i
   return (int64_t)(bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound).total * sizeof(float));
 }
 
+int64_t enflow_lf_backward_workspace_size_min(int num_mols, int num_atoms, int nf, int H, int n_layers,
+                                              int64_t pair_row_bound) {
+  if (num_mols < 0 || num_atoms < 0 || nf < 1 || nf > BWD_NFMAX || !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0)
+    return -1;
+  return (int64_t)(bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound, 2).total * sizeof(float));
+}
+
 int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf,
                                        const int32_t* mol_ptr, const float* h, const float* g,
                                        const float* pos, const float* vel, float kBT, float softening,
@@ -2516,7 +2523,10 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
       !adj_vel || !adj_ldj || !grad_layers || !workspace || !err_flag)
     return -1;
   if (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!dequant_raw || !h_data || !noise || !grad_dequant)) return -1;
-  const BwdWs Wl = bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound);
+  // BWD_NBUF rotating buffers when the workspace holds them, else two (the
+  // layer chain then waits for the weight-gradient pass two layers up)
+  BwdWs Wl = bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound);
+  if ((uint64_t)workspace_bytes < Wl.total * sizeof(float)) Wl = bwd_ws(num_mols, num_atoms, nf, H, n_layers, pair_row_bound, 2);
   if ((uint64_t)workspace_bytes < Wl.total * sizeof(float)) return -6;
   if (num_mols == 0) return 0;
   hipStream_t st = SB(stream);

@@ -8,6 +8,8 @@ enter the flow function as inputs, so ``loss.backward()`` fills every
 ``p.grad`` exactly like the reference's autograd, and DDP / optimisers / LR
 schedulers work on them unchanged (enflow/main.py:212-223).
 """
+import os
+
 import torch
 
 from .. import _lib
@@ -126,9 +128,17 @@ class _FlowFunction(torch.autograd.Function):
         else:
             prb = meta["pair_row_bound"]
             wsb = L.enflow_lf_backward_workspace_size(M, A, nf, hid, n_layers, prb)
+            if os.environ.get("ENFLOW_BWD_MIN_WS") == "1":     # memory-lean: two rotating buffers
+                wsb = L.enflow_lf_backward_workspace_size_min(M, A, nf, hid, n_layers, prb)
             if wsb < 0:
                 raise _lib.HipPathError("enflow_lf_backward_workspace_size rejected the batch")
-            ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            try:
+                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+            except torch.cuda.OutOfMemoryError:
+                # three rotating pair-row buffers do not fit: two (the layer chain
+                # then waits for the weight-gradient pass two layers up)
+                wsb = L.enflow_lf_backward_workspace_size_min(M, A, nf, hid, n_layers, prb)
+                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
             _lib.check(L.enflow_lf_backward_f32(
                 M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
                 _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd),

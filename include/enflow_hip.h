@@ -369,6 +369,12 @@ int enflow_pack_egcl_bwd_f32(const float* raw, int hidden_nf, int node_nf, float
  * over molecules of n_m (n_m - 1) rounded up to a multiple of 32. */
 int64_t enflow_lf_backward_workspace_size(int num_mols, int num_atoms, int node_nf, int hidden_nf,
                                           int n_layers, int64_t pair_row_bound);
+/* The smallest workspace enflow_lf_backward_f32 accepts (two rotating
+ * pair-row buffers instead of three: the layer chain then waits for the
+ * weight-gradient pass two layers up, ~3 % slower at the bench batch).  The
+ * backward uses three when workspace_bytes holds them. */
+int64_t enflow_lf_backward_workspace_size_min(int num_mols, int num_atoms, int node_nf, int hidden_nf,
+                                              int n_layers, int64_t pair_row_bound);
 
 /*
  * Alchemical_NLL backward (enflow/flow/loss.py:11-24): adjoints of the flow

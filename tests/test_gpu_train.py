@@ -12,6 +12,8 @@ Tolerance: gradients are float32 end to end through up to 8 coupling layers
 (the reference differentiates in float64); the bar is GRAD_TOL normwise per
 parameter tensor, the loss itself 1e-5 relative (north_star).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -152,12 +154,20 @@ def test_training_gradients_bitwise_reproducible():
     model = LFIntegrator([EGCL(nf, nf, hid) for _ in range(nl)], ArgMax(nf, hid), dt=default_dt()).cuda()
     eps = torch.tensor(np.random.default_rng(4).normal(size=b["h"].shape).astype(np.float32), device="cuda")
     grads = []
-    for _ in range(2):
-        data = Data.from_arrays(b, device="cuda")
-        _train_step(model, data, eps, default_kBT(), 0.1)
+    for lean in (False, False, True):
+        # the third step with the minimum workspace (two rotating pair-row buffers
+        # instead of three, enflow_lf_backward_workspace_size_min): same arithmetic
+        if lean:
+            os.environ["ENFLOW_BWD_MIN_WS"] = "1"
+        try:
+            data = Data.from_arrays(b, device="cuda")
+            _train_step(model, data, eps, default_kBT(), 0.1)
+        finally:
+            os.environ.pop("ENFLOW_BWD_MIN_WS", None)
         grads.append([p.grad.clone() for p in model.parameters()])
-    for g0, g1 in zip(*grads):
+    for g0, g1, g2 in zip(*grads):
         assert torch.equal(g0, g1)
+        assert torch.equal(g0, g2)
 
 
 def test_training_through_all_egcl_variants_vs_oracle():

@@ -91,6 +91,11 @@ def test_backward_sizes_and_argument_errors():
     assert L.enflow_egcl_bwd_packed_size(H, nf) >= 2 * H * H
     assert L.enflow_egcl_bwd_packed_size(96, nf) == -1
     assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480) > 4 * 480 * 5 * H * 4
+    # three rotating pair-row buffers for chains of >= 3 layers, two at the minimum
+    assert L.enflow_lf_backward_workspace_size_min(M, A, nf, H, nl, 4 * 480) < \
+        L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480)
+    assert L.enflow_lf_backward_workspace_size_min(M, A, nf, H, 2, 4 * 480) == \
+        L.enflow_lf_backward_workspace_size(M, A, nf, H, 2, 4 * 480)
     assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, -1) == -1
     # missing tape / buffers: rejected before any launch
     args = [M, A, 22, nf, H] + [None] * 8 + [nl, 1, None, None, None, 0.1, 1.0] + [None] * 7 + \
