@@ -35,9 +35,16 @@ class ArgMax(nn.Module):
         if width is None or width < self.hidden_nf:
             raise NotImplementedError(f"ArgMax hidden_nf {self.hidden_nf} past the kernel width {width}")
         flat = flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.pad_geom(width), device)
-        # ABI 10: [act kind, p0, p1, 0] of network.1 after the parameters (argmax.py:7)
-        kind, p0, p1 = self.act()
-        return torch.cat([flat, torch.tensor([float(kind), p0, p1, 0.0], dtype=torch.float32, device=device)])
+        # ABI 10: [act kind, p0, p1, 0] of network.1 after the parameters (argmax.py:7);
+        # the device copy is cached (a host-to-device copy per call would stall the
+        # stream once per training step)
+        code = self.act()
+        key = (str(device), code)
+        trailer = getattr(self, "_act_trailer", None)
+        if trailer is None or trailer[0] != key:
+            t = torch.tensor([float(code[0]), code[1], code[2], 0.0], dtype=torch.float32, device=device)
+            self._act_trailer = trailer = (key, t)
+        return torch.cat([flat, trailer[1]])
 
     def act(self):
         """(kind, p0, p1) of the network's activation (ENFLOW_ACT_*)."""
