@@ -2241,12 +2241,36 @@ struct AuxDev {
 };
 std::mutex g_aux_mu;
 AuxDev g_aux[64];
+#ifdef ENFLOW_CHAIN_PRIO
+// A/B: the layer chain on a high-priority stream of its own (the weight-gradient
+// passes on the default-priority aux stream fill the CUs it leaves)
+hipStream_t chain_stream(int dev) {
+  static hipStream_t s[64] = {};
+  if (!s[dev]) {
+    int lo = 0, hi = 0;
+    hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (hipStreamCreateWithPriority(&s[dev], hipStreamNonBlocking, hi) != hipSuccess) s[dev] = nullptr;
+  }
+  return s[dev];
+}
+#endif
 hipStream_t aux_stream(int dev) {
   if (!g_aux[dev].s) {   // created on `dev` (the caller's stream's device)
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+#ifdef ENFLOW_AUX_PRIO
+    // A/B: the weight-gradient passes at another stream priority than the
+    // layer chain (ENFLOW_AUX_PRIO = -1 / +1: lower / higher number = ...)
+    {
+      int lo = 0, hi = 0;
+      hipDeviceGetStreamPriorityRange(&lo, &hi);
+      const int pr = ENFLOW_AUX_PRIO > 0 ? hi : lo;
+      if (hipStreamCreateWithPriority(&g_aux[dev].s, hipStreamNonBlocking, pr) != hipSuccess) g_aux[dev].s = nullptr;
+    }
+#else
     if (hipStreamCreateWithFlags(&g_aux[dev].s, hipStreamNonBlocking) != hipSuccess) g_aux[dev].s = nullptr;
+#endif
     if (cur != dev) (void)hipSetDevice(cur);
   }
   return g_aux[dev].s;
@@ -2549,6 +2573,14 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
   for (int i = 0; i < 2 * n_layers + 1; ++i)
     if (!ev(i)) return -2;
 
+  hipStream_t st_caller = st;
+#ifdef ENFLOW_CHAIN_PRIO
+  hipStream_t sth = chain_stream(dev);
+  if (!sth || !ev(2 * n_layers)) return -2;
+  if (hipEventRecord(ev(2 * n_layers), st) != hipSuccess || hipStreamWaitEvent(sth, ev(2 * n_layers), 0) != hipSuccess)
+    return -2;
+  st = sth;
+#endif
   if (n_layers > 0)
     hipLaunchKernelGGL(pair_offsets_kernel, dim3(n_layers), dim3(BLOCK), 0, st, pair_counts, num_mols, offs);
 
@@ -2593,6 +2625,11 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
     if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;
   }
+#ifdef ENFLOW_CHAIN_PRIO
+  if (hipEventRecord(ev(2 * n_layers), st) != hipSuccess || hipStreamWaitEvent(st_caller, ev(2 * n_layers), 0) != hipSuccess)
+    return -2;
+#endif
+  st = st_caller;
   // join: every weight-gradient pass done before the dequantiser's (buffer 0 again) and the return
   if (n_layers > 0 && hipStreamWaitEvent(st, ev(1), 0) != hipSuccess) return -2;   // layer 0's pass (the last)
 

@@ -854,6 +854,12 @@ __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
 // their prefetch) are live; the operand split of the next k-slice and the
 // filler calls (4 NT per GEMM, the fp32 chain's granularity) are interleaved
 // between the MFMAs.
+#ifndef ENFLOW_FPM1
+#define ENFLOW_FPM1 2        // filler instructions per MFMA in GEMM1 (edge_nn.2) / GEMM2 (coord_nn.0)
+#endif
+#ifndef ENFLOW_FPM2
+#define ENFLOW_FPM2 6
+#endif
 #ifndef ENFLOW_X3_TPG
 #define ENFLOW_X3_TPG 1      // output tiles per step (2: 73 VGPR spills in the tile loop since the bias-in-accumulator SiLU)
 #endif
@@ -1567,7 +1573,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // ---- GEMM1: E^T = edge_nn.2 (egcl.py:20-24)
     f32x16 e[NT];
     acc_from_bias<NT>(e, sm.bias + H, hh);
-    chain_prec_fill<PREC, NT, 2>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
+    chain_prec_fill<PREC, NT, ENFLOW_FPM1>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
         const f32x4 y = act4s<VAR>((f32x4){x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3]},
@@ -1642,7 +1648,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     {
       f32x16 hc[NT];
       acc_from_bias<NT>(hc, sm.bias + 2 * H, hh);
-      chain_prec_fill<PREC, NT, 6>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
+      chain_prec_fill<PREC, NT, ENFLOW_FPM2>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
         const int t = step >> 2, g4 = step & 3;
         float v[4];
 #pragma unroll

@@ -48,6 +48,10 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   __shared__ Smem<H, NMAX, RB> sm;
   constexpr bool BLOCKED = RB < NMAX;
   MolRef M;
+#ifdef ENFLOW_PRIO
+  // A/B: static issue priority for one of the two workgroups sharing a CU
+  if (blockIdx.x & 1) __builtin_amdgcn_s_setprio(ENFLOW_PRIO);
+#endif
   STAMP_DECL
 #ifdef ENFLOW_SKEW
   // A/B experiment: offset the second resident workgroup of a CU so the two
