@@ -25,6 +25,9 @@
 #define NFMAX ENFLOW_NFMAX
 static_assert(NFMAX == 8 || NFMAX == 16, "ENFLOW_NFMAX must be 8 or 16");
 #define KS0MAX (NFMAX / 8 + 1)   // F16X3 GEMM0 k-slices (feature chunks of 8, + radial)
+#ifndef ENFLOW_MSG_MFMA
+#define ENFLOW_MSG_MFMA 1  // 1: split-precision message segment sums as selection-matrix MFMAs (edge_tiles)
+#endif
 #ifndef ENFLOW_MSG_LDS
 #define ENFLOW_MSG_LDS 0   // 1: message segment sums through a per-wave LDS scratch instead of DPP
                            // scans (measured 10 % slower: the serial reduce exposes LDS latency)
@@ -717,6 +720,9 @@ __device__ __forceinline__ void chain_gemm_wide(rsrc_t W, int off_floats, const 
 struct NoMid {
   __device__ __forceinline__ void operator()() const {}
 };
+struct NoLate {
+  __device__ __forceinline__ void operator()(int) const {}
+};
 
 // mid(): called once (NT == 4 only), outside the MFMA/filler scheduling groups,
 // after fillers 0 .. 2 NT - 1 and before filler 2 NT
@@ -804,6 +810,18 @@ __device__ __forceinline__ f32x16 mfma_f16(f32x4 a, f16x8 b, f32x16 c) {
 __device__ __forceinline__ f32x16 mfma_bf16(f32x4 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), b, c, 0, 0, 0);
 }
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q + p addresses row q / columns
+// 4p .. 4p + 3 of a 4 x 16 block of 16-bit elements; lane i receives column i
+// (element q = row q).  EXEC must be full.
+__device__ __forceinline__ s16x4 lds_tr16(const uint32_t* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(p));
+}
+__device__ __forceinline__ f16x8 cat_f16x8(s16x4 a, s16x4 b) {
+  return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
 // x = hi + lo in fp16.  ENFLOW_SPLIT_MIX: lo = f16(x - hi) by v_fma_mix{lo,hi}_f16
 // reading hi straight from its packed fp16 register (x * 1 - hi in one fused
 // op, one rounding), 1.5 VALU per element instead of 3 (convert hi back to
@@ -866,9 +884,16 @@ __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
 #ifndef ENFLOW_X3_DEPTH
 #define ENFLOW_X3_DEPTH 2    // fragment ring depth (prefetch distance + 1 steps)
 #endif
-template <int NT, int FPM, class Fill, class Mid = NoMid>
+struct NoSplit {
+  __device__ __forceinline__ void operator()(int, const f16x8&, const f16x8&) const {}
+};
+// late(step): called at every step 0 .. S-1 after the fillers (and as late(S),
+// late(S + 1) after the chain); onsplit(ts, hi, lo): the split operand of
+// k-slice ts (features 16 ts .. 16 ts + 15, rho order), as soon as it exists
+template <int NT, int FPM, class Fill, class Mid = NoMid, class Late = NoLate, class Split = NoSplit>
 __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                              int lane, Fill&& fill, Mid&& mid = NoMid{}) {
+                                              int lane, Fill&& fill, Mid&& mid = NoMid{}, Late&& late = NoLate{},
+                                              Split&& onsplit = NoSplit{}) {
   constexpr int TPG = NT >= ENFLOW_X3_TPG ? ENFLOW_X3_TPG : NT;
   constexpr int NGR = NT / TPG;
   constexpr int S = NT * 2 * NGR;
@@ -893,6 +918,7 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
     }
   f16x8 bh, bl;
   split_f16(X[0], 0, bh, bl);
+  onsplit(0, bh, bl);
 #pragma unroll
   for (int step = 0; step < S; ++step) {
     const int gi = step % NGR;
@@ -920,10 +946,12 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
 #pragma unroll
     for (int f = 0; f < FPS; ++f)
       if (step * FPS + f < FTOT) fill(step * FPS + f);
+    late(step);
     f16x8 nbh = bh, nbl = bl;
     if (step + 1 < S && (step + 1) % NGR == 0) {
       const int ts = (step + 1) / NGR;
       split_f16(X[ts >> 1], ts & 1, nbh, nbl);
+      onsplit(ts, nbh, nbl);
     }
 #pragma unroll
     for (int k = 0; k < 3 * TPG; ++k) {
@@ -934,6 +962,9 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
     bh = nbh;
     bl = nbl;
   }
+  late(S);
+  late(S + 1);
+  late(S + 2);
 }
 
 // acc[tp] += W[tp][t] X[t] in BF16: 2NT k-steps of NT MFMAs.
@@ -1118,9 +1149,21 @@ struct Smem {
   static constexpr bool MSG_LDS = ENFLOW_MSG_LDS && !BWD && NMAX == 32 && RB == 32;
   static constexpr int MSW = H < 64 ? H : 64;                         // features per reduce chunk
   static constexpr int MSP = MSW + 1;                                 // odd row stride: conflict-free
+  // <= 32-atom images, split precision: the message segment sums run on the
+  // matrix cores (edge_tiles): per wave the fp16 hi | lo image of one 32-feature
+  // tile of the messages, [32 pairs][34 dwords] (136-B rows: the pair-lane
+  // stores are 2-way, the transposed reads of 4 rows at most 2-way), the pair
+  // tile's selection words (f16 multiplicity << 16 | segment) and segment rows
+  static constexpr bool MSG_MMA = ENFLOW_MSG_MFMA && !MSG_LDS && !BWD && NMAX == 32 && RB == 32;
+  static constexpr int MIS = 34;
   union {
     int C[CW];                                                    // pair build (block rows x atoms)
     float msg[MSG_LDS ? WAVES : 1][MSG_LDS ? 32 * MSP : 1];       // edge tiles: per-wave message scratch
+    struct {
+      alignas(16) uint32_t img[MSG_MMA ? WAVES : 1][MSG_MMA ? 32 * MIS : 1];
+      alignas(16) uint32_t tb[MSG_MMA ? WAVES : 1][32];
+      int rt[MSG_MMA ? WAVES : 1][32];
+    } mm;                                                         // edge tiles: message MFMA operands
     struct { float qp[NDT][NDR]; float gp[NDT][NFMAX][NDR]; } nd;   // node phase partials
     float net[NETA * 2 * NFMAX];                                  // ArgMax outputs
     float nb[NBW];                                                // BWD: node adjoint rows
@@ -1433,6 +1476,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const float ik2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
   const float c0 = NLOG2E * ik0, c1 = NLOG2E * ik1, c2 = NLOG2E * ik2;
   constexpr bool MSG_LDS = Smem<H, NMAX, RB>::MSG_LDS;
+  constexpr bool MMA = PREC == PREC_F16X3 && !VAR && Smem<H, NMAX, RB>::MSG_MMA;   // VAR: +0.8 KB scratch
+  constexpr int MIS = Smem<H, NMAX, RB>::MIS;
   constexpr int MSP = Smem<H, NMAX, RB>::MSP;
   float* const scr = MSG_LDS ? &sm.u.msg[w][0] : nullptr;
   // constructor variants of the layer (wave-uniform; compiled in only for VAR
@@ -1474,7 +1519,22 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // neighbouring row of the same molecule, never turn it finite)
     const SegExec SE = seg_exec(row);
     SegMasks SM;
-    if constexpr (!MSG_LDS) SM = seg_masks(row);
+    if constexpr (!MSG_LDS && !MMA) SM = seg_masks(row);
+    int nseg = 0;
+    if constexpr (MMA) {
+      // the tile's segments: slot = index of the row run (invalid lanes are runs
+      // of their own with multiplicity 0); the selection word of pair j and the
+      // row of every slot go to the wave's tables, read back by segment lanes
+      const int row_prev = __shfl_up(row, 1, 32);
+      const bool start = j == 0 || row_prev != row;
+      const uint32_t S = (uint32_t)__ballot(start);
+      const int seg = __builtin_popcount(S & (uint32_t)((2ull << j) - 1ull)) - 1;
+      nseg = __builtin_popcount(S);
+      if (hh == 0) {
+        sm.u.mm.tb[w][j] = ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)c) << 16) | (uint32_t)seg;
+        if (start) sm.u.mm.rt[w][seg] = valid ? il : -1;
+      }
+    }
     const int row_next = __shfl_down(row, 1, 32);
     const bool seg_end = valid && (j == 31 || row_next != row);
     float* const dst_row = (ishead && row == headrow) ? &sm.head[w][0] : &sm.agg[(valid ? il : 0) * AST];
@@ -1645,7 +1705,107 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         }
       }
     };
-    {
+    if constexpr (MMA) {
+      // message segment sums on the matrix cores: agg[row(n)][f] += sum_p
+      // E[p][f] S[p][n], S[p][n] = c_p if pair p is in segment n -- one
+      // 32x32x16 MFMA per (32-feature tile, 16 pairs, hi | lo) with A = E^T
+      // (features x pairs) read transposed from the fp16 image that GEMM2's own
+      // operand split writes, B = S (pairs x segment slots).  The accumulator
+      // starts from the segment rows' aggregates and is stored back by the
+      // lanes of the tile's segments (lane = slot n: features 8 g4 + 4 hh + u).
+      f32x16 hc[NT];
+      acc_from_bias<NT>(hc, sm.bias + 2 * H, hh);
+      uint32_t* const img = &sm.u.mm.img[w][0];
+      const int ibase = (8 * hh + ((lane >> 2) & 3)) * MIS + 2 * (4 * ((lane >> 4) & 1) + (lane & 3));
+      f16x8 sel[2];
+      float* dstn = &sm.agg[0];
+      bool vn = false;
+      f32x16 Y;
+      s16x4 ar[4][2];
+      u32x4v tq[4];
+      int rn = -1;
+      // LDS reads are issued one step (a chain step's MFMAs) before their use
+      constexpr int MSTEP = NT >= 4 ? 2 : 1;   // tile reads at step a, MFMAs at a + MSTEP, stores after
+      auto late = [&](int step) {
+        if (step == 0) {
+          const uint32_t* const tb = &sm.u.mm.tb[w][0];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) tq[q] = *reinterpret_cast<const u32x4v*>(tb + 16 * (q >> 1) + 8 * hh + 4 * (q & 1));
+          rn = sm.u.mm.rt[w][j];
+        }
+        if (step == 1) {
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            const u32x4v q0 = tq[2 * ks], q1 = tq[2 * ks + 1];
+            const uint32_t wv[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+            u32x4v pk;
+#pragma unroll
+            for (int i2 = 0; i2 < 4; ++i2) {
+              const uint32_t a0 = (wv[2 * i2] & 0xffffu) == (uint32_t)j ? wv[2 * i2] >> 16 : 0u;
+              const uint32_t a1 = (wv[2 * i2 + 1] & 0xffffu) == (uint32_t)j ? wv[2 * i2 + 1] & 0xffff0000u : 0u;
+              pk[i2] = a0 | a1;
+            }
+            sel[ks] = __builtin_bit_cast(f16x8, pk);
+          }
+          vn = j < nseg && rn >= 0;
+          if (vn) dstn = (ishead && rn == headrow) ? &sm.head[w][0] : &sm.agg[rn * AST];
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const int a = (2 * t + 1) * NT;   // tile t's image is complete, tile t + 1 overwrites it at step a + NT - 1
+          if (step == a) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+              for (int rd = 0; rd < 2; ++rd) ar[k][rd] = lds_tr16(img + ibase + (16 * (k >> 1) + 4 * rd) * MIS + 16 * (k & 1));
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const f32x4 v = ld4(dstn + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+              for (int u = 0; u < 4; ++u) Y[4 * g4 + u] = v[u];
+            }
+          }
+          if (step == a + MSTEP) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(cat_f16x8(ar[k][0], ar[k][1]), sel[k >> 1], Y, 0, 0, 0);
+          }
+          if (step == a + MSTEP + 1 && vn) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) st4(dstn + 32 * t + 8 * g4 + 4 * hh, (f32x4){Y[4 * g4], Y[4 * g4 + 1],
+                                                                                     Y[4 * g4 + 2], Y[4 * g4 + 3]});
+          }
+        }
+      };
+      auto onsplit = [&](int ts, const f16x8& bh, const f16x8& bl) {
+        const u32x4v hv = __builtin_bit_cast(u32x4v, bh), lv = __builtin_bit_cast(u32x4v, bl);
+        uint32_t* const r = img + j * MIS + 2 * hh + 8 * (ts & 1);   // 4-feature unit 4 s + hh (+2, +8: lo)
+        *reinterpret_cast<u32x2v*>(r) = (u32x2v){hv[0], hv[1]};
+        *reinterpret_cast<u32x2v*>(r + 4) = (u32x2v){hv[2], hv[3]};
+        *reinterpret_cast<u32x2v*>(r + 16) = (u32x2v){lv[0], lv[1]};
+        *reinterpret_cast<u32x2v*>(r + 20) = (u32x2v){lv[2], lv[3]};
+      };
+      chain_x3_fill<NT, ENFLOW_FPM2>(W, L.wc1x, e, hc, lane, [&](int step) {
+        const int t = step >> 2, g4 = step & 3;
+        if (t + 1 < NT && !v_att) {
+          const f32x4 y = act4s<VAR>((f32x4){e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
+                                             e[t + 1][4 * g4 + 3]}, c1, K1, ik1, act);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
+        }
+      }, NoMid{}, late, onsplit);
+      // coord_nn.2 as a per-pair dot
+#pragma unroll
+      for (int tp = 0; tp < NT; ++tp)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 w2 = *reinterpret_cast<const f32x4*>(sm.bias + 3 * H + 32 * tp + 8 * g4 + 4 * hh);
+          const f32x4 y = act4s<VAR>((f32x4){hc[tp][4 * g4], hc[tp][4 * g4 + 1], hc[tp][4 * g4 + 2],
+                                             hc[tp][4 * g4 + 3]}, c2, K2, ik2, act);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
+        }
+    } else {
       f32x16 hc[NT];
       acc_from_bias<NT>(hc, sm.bias + 2 * H, hh);
       chain_prec_fill<PREC, NT, ENFLOW_FPM2>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
