@@ -968,15 +968,21 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
 }
 
 // acc[tp] += W[tp][t] X[t] in BF16: 2NT k-steps of NT MFMAs.
-template <int NT, int FPM, class Fill, class Mid = NoMid>
+// late / onsplit as chain_x3_fill (onsplit(ts): k-slice ts's operand is built)
+struct NoSplit1 {
+  __device__ __forceinline__ void operator()(int) const {}
+};
+template <int NT, int FPM, class Fill, class Mid = NoMid, class Late = NoLate, class Split = NoSplit1>
 __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
-                                               int lane, Fill&& fill, Mid&& mid = NoMid{}) {
+                                               int lane, Fill&& fill, Mid&& mid = NoMid{}, Late&& late = NoLate{},
+                                               Split&& onsplit = NoSplit1{}) {
   constexpr int S = 2 * NT;
   f32x4 cb[NT], nb[NT];
   const int vo = lane * 16;
 #pragma unroll
   for (int tp = 0; tp < NT; ++tp) cb[tp] = bload4(W, vo, (off_floats + (tp * NT * 2) * 256) * 4);
   bf16x8 b = to_bf16(X[0], 0);
+  onsplit(0);
 #pragma unroll
   for (int step = 0; step < S; ++step) {
     if (NT == 4 && step == 4) {
@@ -994,8 +1000,12 @@ __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f
     for (int tp = 0; tp < NT; ++tp) acc[tp] = mfma_bf16(cb[tp], b, acc[tp]);
     fill(2 * step);
     fill(2 * step + 1);
+    late(step);
     bf16x8 n2 = b;
-    if (step + 1 < S) n2 = to_bf16(X[(step + 1) >> 1], (step + 1) & 1);
+    if (step + 1 < S) {
+      n2 = to_bf16(X[(step + 1) >> 1], (step + 1) & 1);
+      onsplit(step + 1);
+    }
 #pragma unroll
     for (int k = 0; k < NT; ++k) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -1008,6 +1018,9 @@ __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f
       for (int tp = 0; tp < NT; ++tp) cb[tp] = nb[tp];
     }
   }
+  late(S);
+  late(S + 1);
+  late(S + 2);
 }
 
 // GEMM with the precision's chain; off_* are the packed sections of the matrix
@@ -1476,7 +1489,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const float ik2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
   const float c0 = NLOG2E * ik0, c1 = NLOG2E * ik1, c2 = NLOG2E * ik2;
   constexpr bool MSG_LDS = Smem<H, NMAX, RB>::MSG_LDS;
-  constexpr bool MMA = PREC == PREC_F16X3 && !VAR && Smem<H, NMAX, RB>::MSG_MMA;   // VAR: +0.8 KB scratch
+  constexpr bool MMA = PREC != PREC_F32 && !VAR && Smem<H, NMAX, RB>::MSG_MMA;   // VAR: +0.8 KB scratch
   constexpr int MIS = Smem<H, NMAX, RB>::MIS;
   constexpr int MSP = Smem<H, NMAX, RB>::MSP;
   float* const scr = MSG_LDS ? &sm.u.msg[w][0] : nullptr;
@@ -1724,8 +1737,12 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
       s16x4 ar[4][2];
       u32x4v tq[4];
       int rn = -1;
-      // LDS reads are issued one step (a chain step's MFMAs) before their use
-      constexpr int MSTEP = NT >= 4 ? 2 : 1;   // tile reads at step a, MFMAs at a + MSTEP, stores after
+      // LDS reads are issued one step (a chain step's MFMAs) before their use.
+      // Feature tile t's image is complete after k-slice 2 t + 1's split, at
+      // step (2 t + 1) AB - 1, and k-slice 2 t + 2 overwrites it at the end of
+      // step (2 t + 2) AB - 1 (AB = chain steps per k-slice)
+      constexpr int AB = PREC == PREC_F16X3 ? NT : 1;
+      constexpr int MSTEP = AB >= 4 ? 2 : 1;   // tile reads at step a, MFMAs at a + MSTEP, stores after
       auto late = [&](int step) {
         if (step == 0) {
           const uint32_t* const tb = &sm.u.mm.tb[w][0];
@@ -1752,7 +1769,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         }
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
-          const int a = (2 * t + 1) * NT;   // tile t's image is complete, tile t + 1 overwrites it at step a + NT - 1
+          const int a = (2 * t + 1) * AB;
           if (step == a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k)
@@ -1785,7 +1802,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         *reinterpret_cast<u32x2v*>(r + 16) = (u32x2v){lv[0], lv[1]};
         *reinterpret_cast<u32x2v*>(r + 20) = (u32x2v){lv[2], lv[3]};
       };
-      chain_x3_fill<NT, ENFLOW_FPM2>(W, L.wc1x, e, hc, lane, [&](int step) {
+      auto fillm = [&](int step) {
         const int t = step >> 2, g4 = step & 3;
         if (t + 1 < NT && !v_att) {
           const f32x4 y = act4s<VAR>((f32x4){e[t + 1][4 * g4], e[t + 1][4 * g4 + 1], e[t + 1][4 * g4 + 2],
@@ -1793,7 +1810,16 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
           for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
         }
-      }, NoMid{}, late, onsplit);
+      };
+      if constexpr (PREC == PREC_F16X3) {
+        chain_x3_fill<NT, ENFLOW_FPM2>(W, L.wc1x, e, hc, lane, fillm, NoMid{}, late, onsplit);
+      } else {   // bf16 GEMM2: the image gets an fp16 hi / lo split of its own
+        chain_b16_fill<NT, ENFLOW_FPM2>(W, L.wc1b, e, hc, lane, fillm, NoMid{}, late, [&](int ts) {
+          f16x8 bh, bl;
+          split_f16(e[ts >> 1], ts & 1, bh, bl);
+          onsplit(ts, bh, bl);
+        });
+      }
       // coord_nn.2 as a per-pair dot
 #pragma unroll
       for (int tp = 0; tp < NT; ++tp)

@@ -214,6 +214,35 @@ def test_ragged_and_edge_sizes_vs_oracle(sizes):
     assert abs(float(ldj) - ref_ldj) <= TOL * abs(ref_ldj)
 
 
+@pytest.mark.parametrize("prec", ["f16x3", "bf16"])
+@pytest.mark.parametrize("hid,r_cut,box", [(128, 1.6, None), (64, 2.2, None), (32, 1.6, None), (128, 3.0, 5.0)])
+def test_segment_layouts_vs_oracle(hid, r_cut, box, prec):
+    """The message segment sums' tile layouts (edge_tiles, ENFLOW_MSG_MFMA):
+    short cutoffs give rows of 0-3 pairs, so a 32-pair tile holds up to 32
+    row runs and isolated atoms leave gaps in the row sequence; a 5 A box at a
+    3 A cutoff gives periodic multiplicities > 1 (several images of one pair)."""
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    sizes = [22, 31, 9, 17, 22, 2]
+    b = _f32(make_molecules(len(sizes), sizes, nf=5, seed=int(10 * r_cut) + hid, r_cut_ang=r_cut, box_ang=box))
+    model = _make_model(hid, 5, 2, 7, default_dt())
+    model.gemm_precision = prec
+    d = Data.from_arrays(b, device=DEV)
+    e = d.edges
+    rows = e.row.cpu().numpy()
+    runs = 1 + int(np.count_nonzero(np.diff(rows))) if rows.size else 0
+    noise = torch.randn(d.h.shape, device=DEV)
+    with torch.no_grad():
+        o, ldj = model(d, noise=noise)
+    ref, ref_ldj = _oracle_flow(model, b, noise)
+    errs = {k: rel_err(getattr(o, k).cpu().numpy(), ref[k]) for k in ("h", "g", "pos", "vel")}
+    errs["ldj"] = abs(float(ldj) - ref_ldj) / abs(ref_ldj)
+    print(f"h{hid} r_cut {r_cut} box {box} {prec}: {rows.size} pairs in {runs} row runs, "
+          f"max multiplicity {int(np.max(np.unique(np.stack([rows, e.col.cpu().numpy()]), axis=1, return_counts=True)[1]))}:",
+          fmt(errs))
+    assert_all_within(errs, TOL if prec == "f16x3" else BF16_TOL)
+
+
 def floor_reverse_check(got, h_cont, want_exact=None, near=1e-5):
     """Floor.reverse (floor.py:13) after a float32 reverse: got must equal
     floor(h_cont) (the oracle's continuous reverse of the same float32 inputs)

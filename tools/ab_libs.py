@@ -36,7 +36,7 @@ def main():
         _lib.LIB_PATH = path
         model._layers_key = None
         model.dequantize._packed_key = None
-        ts = []
+        ev = []
         for _ in range(reps):
             for k in work:
                 work[k].copy_(inp[k])
@@ -52,15 +52,18 @@ def main():
                 _lib.ptr(ldj_mol), _lib.ptr(ldj), _lib.ptr(err), None, None, None, model._prec(),
                 _lib.stream_ptr(dev)), "enflow_lf_forward_f32")
             e1.record()
-            torch.cuda.synchronize()
-            ts.append(e0.elapsed_time(e1))
+            ev.append((e0, e1))
+        torch.cuda.synchronize()   # launches back to back: no idle gap lets the clocks drop
         outs[path] = (work["pos"].clone(), ldj.clone())
-        return ts
+        return [a.elapsed_time(b) for a, b in ev]
 
     res = {p: [] for p in libs}
     for p in libs:
         run(p, 3)          # warm-up / pack
-    for rnd in range(6):
+    for _ in range(int(os.environ.get("AB_PREWARM", "200")) // len(libs)):   # clocks up before the first timed round
+        for p in libs:
+            run(p, 1)
+    for rnd in range(int(os.environ.get("AB_ROUNDS", "6"))):
         for p in libs:
             res[p] += run(p, 5)
     base = outs[libs[0]]
