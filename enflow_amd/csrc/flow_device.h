@@ -1489,7 +1489,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   const float ik2 = PREC == PREC_F16X3 ? Lp[L.scl + 3] : 1.f;
   const float c0 = NLOG2E * ik0, c1 = NLOG2E * ik1, c2 = NLOG2E * ik2;
   constexpr bool MSG_LDS = Smem<H, NMAX, RB>::MSG_LDS;
-  constexpr bool MMA = PREC != PREC_F32 && !VAR && Smem<H, NMAX, RB>::MSG_MMA;   // VAR: +0.8 KB scratch
+  // VAR: +0.8 KB scratch; BIG (enflow_large.hip's row blocks): +0.6 KB scratch, 3x slower
+  constexpr bool MMA = PREC != PREC_F32 && !VAR && !BIG && Smem<H, NMAX, RB>::MSG_MMA;
   constexpr int MIS = Smem<H, NMAX, RB>::MIS;
   constexpr int MSP = Smem<H, NMAX, RB>::MSP;
   float* const scr = MSG_LDS ? &sm.u.msg[w][0] : nullptr;
