@@ -884,13 +884,17 @@ __device__ __forceinline__ bf16x8 to_bf16(const f32x16& X, int s) {
 #ifndef ENFLOW_X3_DEPTH
 #define ENFLOW_X3_DEPTH 2    // fragment ring depth (prefetch distance + 1 steps)
 #endif
+#ifndef ENFLOW_FWD_X3_DEPTH
+#define ENFLOW_FWD_X3_DEPTH 3   // the 4-wave <= 32-atom forward / reverse edge tiles: one L2 round trip more
+#endif                          // in flight (+1-2 %, bitwise equal; other instances spill more at 3)
 struct NoSplit {
   __device__ __forceinline__ void operator()(int, const f16x8&, const f16x8&) const {}
 };
 // late(step): called at every step 0 .. S-1 after the fillers (and as late(S),
 // late(S + 1) after the chain); onsplit(ts, hi, lo): the split operand of
 // k-slice ts (features 16 ts .. 16 ts + 15, rho order), as soon as it exists
-template <int NT, int FPM, class Fill, class Mid = NoMid, class Late = NoLate, class Split = NoSplit>
+template <int NT, int FPM, int DEP = ENFLOW_X3_DEPTH, class Fill, class Mid = NoMid, class Late = NoLate,
+          class Split = NoSplit>
 __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
                                               int lane, Fill&& fill, Mid&& mid = NoMid{}, Late&& late = NoLate{},
                                               Split&& onsplit = NoSplit{}) {
@@ -899,7 +903,7 @@ __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f3
   constexpr int S = NT * 2 * NGR;
   constexpr int FPS = (4 * NT) / S > 0 ? (4 * NT) / S : 1;
   constexpr int FTOT = 4 * NT;
-  constexpr int D = ENFLOW_X3_DEPTH;
+  constexpr int D = DEP;
   f32x4 rh[D][TPG], rl[D][TPG];
   const int vo = lane * 32;
   auto foff = [&](int step, int q) {
@@ -1024,10 +1028,10 @@ __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f
 }
 
 // GEMM with the precision's chain; off_* are the packed sections of the matrix
-template <int PREC, int NT, int FPM, class Fill, class Mid = NoMid>
+template <int PREC, int NT, int FPM, int DEP = ENFLOW_X3_DEPTH, class Fill, class Mid = NoMid>
 __device__ __forceinline__ void chain_prec_fill(rsrc_t W, int off_f32, int off_x3, int off_b16, const f32x16 (&X)[NT],
                                                 f32x16 (&acc)[NT], int lane, Fill&& fill, Mid&& mid = NoMid{}) {
-  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM>(W, off_x3, X, acc, lane, fill, mid);
+  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM, DEP>(W, off_x3, X, acc, lane, fill, mid);
   else if constexpr (PREC == PREC_BF16) chain_b16_fill<NT, FPM>(W, off_b16, X, acc, lane, fill, mid);
   else chain_gemm_fill<NT, FPM>(W, off_f32, X, acc, lane, fill, mid);
 }
@@ -1491,6 +1495,8 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   constexpr bool MSG_LDS = Smem<H, NMAX, RB>::MSG_LDS;
   // VAR: +0.8 KB scratch; BIG (enflow_large.hip's row blocks): +0.6 KB scratch, 3x slower
   constexpr bool MMA = PREC != PREC_F32 && !VAR && !BIG && Smem<H, NMAX, RB>::MSG_MMA;
+  // weight-fragment ring depth of GEMM1 / GEMM2 (the headline instance: 3)
+  constexpr int XD = (NMAX == 32 && RB == 32 && WAVES == 4 && !BIG) ? ENFLOW_FWD_X3_DEPTH : ENFLOW_X3_DEPTH;
   constexpr int MIS = Smem<H, NMAX, RB>::MIS;
   constexpr int MSP = Smem<H, NMAX, RB>::MSP;
   float* const scr = MSG_LDS ? &sm.u.msg[w][0] : nullptr;
@@ -1647,7 +1653,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // ---- GEMM1: E^T = edge_nn.2 (egcl.py:20-24)
     f32x16 e[NT];
     acc_from_bias<NT>(e, sm.bias + H, hh);
-    chain_prec_fill<PREC, NT, ENFLOW_FPM1>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
+    chain_prec_fill<PREC, NT, ENFLOW_FPM1, XD>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
         const f32x4 y = act4s<VAR>((f32x4){x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3]},
@@ -1813,7 +1819,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         }
       };
       if constexpr (PREC == PREC_F16X3) {
-        chain_x3_fill<NT, ENFLOW_FPM2>(W, L.wc1x, e, hc, lane, fillm, NoMid{}, late, onsplit);
+        chain_x3_fill<NT, ENFLOW_FPM2, XD>(W, L.wc1x, e, hc, lane, fillm, NoMid{}, late, onsplit);
       } else {   // bf16 GEMM2: the image gets an fp16 hi / lo split of its own
         chain_b16_fill<NT, ENFLOW_FPM2>(W, L.wc1b, e, hc, lane, fillm, NoMid{}, late, [&](int ts) {
           f16x8 bh, bl;
@@ -1835,7 +1841,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     } else {
       f32x16 hc[NT];
       acc_from_bias<NT>(hc, sm.bias + 2 * H, hh);
-      chain_prec_fill<PREC, NT, ENFLOW_FPM2>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
+      chain_prec_fill<PREC, NT, ENFLOW_FPM2, XD>(W, L.wc1f, L.wc1x, L.wc1b, e, hc, lane, [&](int step) {
         const int t = step >> 2, g4 = step & 3;
         float v[4];
 #pragma unroll
