@@ -1222,6 +1222,10 @@ __device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
     sm.cntrow[a] = 0;
     if constexpr (S::IMG_LDS) sm.near27[a] = 0u;
   }
+  if constexpr (!S::BLOCKED) {   // the whole molecule's count matrix, zeroed here: block_counts(.., zeroed)
+    const int words = S::PACKC ? (n * n + 1) / 2 : n * n;
+    for (int e = tid; e < words; e += BLOCK) sm.u.C[e] = 0;
+  }
   if constexpr (S::IMG_LDS) {   // the molecule's bounding box (n <= 32: one wave)
     if (tid < 64) {
       float lo[3], hi[3];
@@ -1319,11 +1323,13 @@ __device__ __forceinline__ void build_images(S& sm, const MolRef& M, int tid) {
 //     id_mapping, self pairs dropped), (d) compaction to (local row, col, mult)
 //     sorted by (row, col).
 template <class S>
-__device__ __forceinline__ void block_counts(S& sm, const MolRef& M, int tid, int r0, int rb) {
+__device__ __forceinline__ void block_counts(S& sm, const MolRef& M, int tid, int r0, int rb, bool zeroed = false) {
   const int n = M.n;
-  const int words = S::PACKC ? (rb * n + 1) / 2 : rb * n;
-  for (int e = tid; e < words; e += BLOCK) sm.u.C[e] = 0;
-  __syncthreads();
+  if (!zeroed) {   // (build_images zeroes the whole molecule's matrix before its barriers)
+    const int words = S::PACKC ? (rb * n + 1) / 2 : rb * n;
+    for (int e = tid; e < words; e += BLOCK) sm.u.C[e] = 0;
+    __syncthreads();
+  }
   const float r_sq = M.rc * M.rc;
   for (int e = tid; e < rb * n; e += BLOCK) {
     const int il = e / n, q = e - il * n;
@@ -1406,7 +1412,7 @@ __device__ __forceinline__ int block_compact(S& sm, int n, int tid, int rb, int 
 template <class S>
 __device__ __forceinline__ void build_block_pairs(S& sm, const MolRef& M, int tid, int r0, int rb) {
   static_assert(!S::BLOCKED, "blocked images compact in passes (block_compact)");
-  block_counts(sm, M, tid, r0, rb);
+  block_counts(sm, M, tid, r0, rb, r0 == 0 && rb == M.n);   // after build_images: already zeroed
   block_compact(sm, M.n, tid, rb, 0);
 }
 
