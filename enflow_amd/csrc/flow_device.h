@@ -1435,11 +1435,13 @@ __device__ __forceinline__ void build_pairs(S& sm, const MolRef& M, int tid) {
 template <bool BIG>
 __device__ __forceinline__ int pair_row(uint32_t pr) { return BIG ? (int)(pr & 31u) : (int)(pr & 0xffu); }
 
-template <int H, int NMAX, int RB, int PREC = PREC_F32, bool VAR = false, bool BIG = false>
+// pre(): run by every wave after its last tile, before the closing barrier (the
+// node phase's fragment requests, so their L2 round trip overlaps the wait)
+template <int H, int NMAX, int RB, int PREC = PREC_F32, bool VAR = false, bool BIG = false, class Pre = NoMid>
 __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                            const MolRef& M, int nf, int tid, int r0, int rb,
                                            bool zero_agg STAMP_ARGS, const float* __restrict__ cpos = nullptr,
-                                           const float* __restrict__ ch = nullptr) {
+                                           const float* __restrict__ ch = nullptr, Pre&& pre = NoMid{}) {
   constexpr int NT = H / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
@@ -1903,6 +1905,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     if (__ballot(range_bad))
       if (lane == 0) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
   }
+  pre();
   __syncthreads();
   STAMP(15);
   // ordered fix-up of rows that continue across a wave boundary
@@ -2019,26 +2022,14 @@ __device__ __forceinline__ void node_phase(Smem<H, NMAX, RB>& sm, const float* _
 
 // F16X3 node phase: same items and outputs as node_phase, all products on
 // v_mfma_f32_32x32x16_f16 with hi/lo split operands (atoms on the pair lanes).
-template <int H, int NMAX, int RB, bool VAR = false>
-__device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
-                                              int n, int nf, int tid, int r0, int rb) {
-  constexpr int NT = H / 32;
-  constexpr int NA = RB / 32;
-  constexpr int AST = Smem<H, NMAX, RB>::AST;
-  constexpr int KS = H / 16;
-  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
-  const int j = lane & 31, hh = lane >> 5;
-  const rsrc_t W = weights_rsrc(Lp, L.total);
-  const float inv_v1 = Lp[L.scl + 7], inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
-  const Act act = VAR ? act_of(Lp + L.vfl + 1) : act_silu();
-  const int vo = lane * 32;
-  // every fragment of the wave's first item is requested before the bias
-  // staging barrier, so the L2 round trips overlap instead of serialising
-  // every fragment of an item is requested up front (the node phase runs outside
-  // the tile loop's register budget): one L2 round trip per item, not one per k-step
+// node_phase_x3's weight fragments of one item (vel_scaling_nn.0, node_nn.0 h / agg
+// parts, node_nn.2): requested up front, one L2 round trip per item
+template <int H>
+struct NodeFrags {
+  static constexpr int NT = H / 32, KS = H / 16;
   f32x4 vh, vl, nh, nl, gfh[2], gfl[2], ah[KS], al[KS];
-  auto issue = [&](int it) {
-    const int tp = it % NT;
+  __device__ __forceinline__ void issue(rsrc_t W, const EgclLayout& L, int lane, int item) {
+    const int tp = item % NT, vo = lane * 32;
     vh = bload4(W, vo, (L.wv1x + tp * 512) * 4);
     vl = bload4(W, vo + 16, (L.wv1x + tp * 512) * 4);
     nh = bload4(W, vo, (L.wn1hx + tp * 512) * 4);
@@ -2053,8 +2044,44 @@ __device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float
       ah[d] = bload4(W, vo, (L.wn1ax + (tp * KS + d) * 512) * 4);
       al[d] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + d) * 512) * 4);
     }
-  };
-  if (w < NT * NA) issue(w);
+  }
+};
+
+template <int H, int NMAX, int RB, bool VAR = false>
+__device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp,
+                                                const EgclLayout& L, int n, int nf, int tid, int r0, int rb,
+                                                NodeFrags<H>& F, bool issued);
+// issued: the caller requested this wave's first item (F.issue(.., wave)) before
+// the edge tiles' closing barrier, so its L2 round trip overlaps the wait there
+template <int H, int NMAX, int RB, bool VAR = false>
+__device__ __forceinline__ void node_phase_x3(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
+                                              int n, int nf, int tid, int r0, int rb) {
+  NodeFrags<H> F;
+  node_phase_x3_f<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid, r0, rb, F, false);
+}
+template <int H, int NMAX, int RB, bool VAR>
+__device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp,
+                                                const EgclLayout& L, int n, int nf, int tid, int r0, int rb,
+                                                NodeFrags<H>& F, bool issued) {
+  constexpr int NT = H / 32;
+  constexpr int NA = RB / 32;
+  constexpr int AST = Smem<H, NMAX, RB>::AST;
+  constexpr int KS = H / 16;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
+  const int j = lane & 31, hh = lane >> 5;
+  const rsrc_t W = weights_rsrc(Lp, L.total);
+  const float inv_v1 = Lp[L.scl + 7], inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
+  const Act act = VAR ? act_of(Lp + L.vfl + 1) : act_silu();
+  // every fragment of the wave's first item is requested before the bias
+  // staging barrier (or earlier, by the caller), so the L2 round trips overlap
+  // instead of serialising
+  f32x4 &vh = F.vh, &vl = F.vl, &nh = F.nh, &nl = F.nl;
+  auto& gfh = F.gfh;
+  auto& gfl = F.gfl;
+  auto& ah = F.ah;
+  auto& al = F.al;
+  auto issue = [&](int it) { F.issue(W, L, lane, it); };
+  if (!issued && w < NT * NA) issue(w);
   // vel_scaling_nn.0 / .2 and node_nn.0 biases staged in LDS (edge_tiles' bias
   // image is free now)
   for (int k = tid; k < H; k += BLOCK) {

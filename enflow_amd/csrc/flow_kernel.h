@@ -132,7 +132,17 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
         atomicAdd(&A.stats[0], (unsigned long long)tot);
         atomicAdd(&A.stats[1], edges);
       }
-      edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS);
+      // the node phase's first fragments, requested as each wave leaves its tiles
+      // (the whole-molecule split-precision image: one edge_tiles pass per layer)
+      NodeFrags<H> nfr;
+      constexpr bool EARLY = !BLOCKED && PREC != PREC_F32;
+      const int wv = __builtin_amdgcn_readfirstlane(tid_l >> 6);
+      auto pre = [&] {
+        if constexpr (EARLY) {
+          if (wv < (H / 32) * (RB / 32)) nfr.issue(weights_rsrc(Lp, L.total), L, tid_l & 63, wv);
+        }
+      };
+      edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS, nullptr, nullptr, pre);
       if constexpr (BLOCKED) {   // blocks with more pairs than the buffer: further passes
         constexpr int PC = Smem<H, NMAX, RB>::PC;
         for (int p0 = PC; p0 < tot; p0 += PC) {
@@ -142,7 +152,8 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       }
       STAMP(4);
       {
-        if constexpr (PREC != PREC_F32) node_phase_x3<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid_l, r0, rb);   // fp32-accurate
+        if constexpr (PREC != PREC_F32)   // fp32-accurate
+          node_phase_x3_f<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid_l, r0, rb, nfr, EARLY);
         else node_phase<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid_l, r0, rb);
       }
       STAMP(5);
