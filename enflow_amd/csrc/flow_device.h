@@ -893,33 +893,63 @@ struct NoSplit {
 // late(step): called at every step 0 .. S-1 after the fillers (and as late(S),
 // late(S + 1) after the chain); onsplit(ts, hi, lo): the split operand of
 // k-slice ts (features 16 ts .. 16 ts + 15, rho order), as soon as it exists
+// The fragment ring of chain_x3_fill; x3_prologue requests its first D - 1
+// steps, which a caller can do well before the chain (chain_x3_fill_r), so that
+// L2 round trip overlaps other work instead of opening the chain
+template <int NT, int DEP>
+struct X3Ring {
+  static constexpr int TPG = NT >= ENFLOW_X3_TPG ? ENFLOW_X3_TPG : NT;
+  static constexpr int NGR = NT / TPG;
+  static constexpr int S = NT * 2 * NGR;
+  f32x4 rh[DEP][TPG], rl[DEP][TPG];
+  __device__ __forceinline__ static int foff(int off_floats, int step, int q) {
+    const int gi = step % NGR, ts = step / NGR;
+    const int tp = gi * TPG + q;
+    return (off_floats + ((tp * NT + (ts >> 1)) * 2 + (ts & 1)) * 512) * 4;
+  }
+};
+template <int NT, int DEP>
+__device__ __forceinline__ void x3_prologue(X3Ring<NT, DEP>& R, rsrc_t W, int off_floats, int lane) {
+  using RG = X3Ring<NT, DEP>;
+  const int vo = lane * 32;
+#pragma unroll
+  for (int d = 0; d < DEP - 1; ++d)
+    if (d < RG::S) {
+#pragma unroll
+      for (int q = 0; q < RG::TPG; ++q) {
+        R.rh[d][q] = bload4(W, vo, RG::foff(off_floats, d, q));
+        R.rl[d][q] = bload4(W, vo + 16, RG::foff(off_floats, d, q));
+      }
+    }
+}
+template <int NT, int FPM, int DEP, class Fill, class Mid = NoMid, class Late = NoLate, class Split = NoSplit>
+__device__ __forceinline__ void chain_x3_fill_r(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
+                                                int lane, X3Ring<NT, DEP>& R, Fill&& fill, Mid&& mid = NoMid{},
+                                                Late&& late = NoLate{}, Split&& onsplit = NoSplit{});
 template <int NT, int FPM, int DEP = ENFLOW_X3_DEPTH, class Fill, class Mid = NoMid, class Late = NoLate,
           class Split = NoSplit>
 __device__ __forceinline__ void chain_x3_fill(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
                                               int lane, Fill&& fill, Mid&& mid = NoMid{}, Late&& late = NoLate{},
                                               Split&& onsplit = NoSplit{}) {
-  constexpr int TPG = NT >= ENFLOW_X3_TPG ? ENFLOW_X3_TPG : NT;
-  constexpr int NGR = NT / TPG;
-  constexpr int S = NT * 2 * NGR;
+  X3Ring<NT, DEP> R;
+  x3_prologue(R, W, off_floats, lane);
+  chain_x3_fill_r<NT, FPM, DEP>(W, off_floats, X, acc, lane, R, fill, mid, late, onsplit);
+}
+template <int NT, int FPM, int DEP, class Fill, class Mid, class Late, class Split>
+__device__ __forceinline__ void chain_x3_fill_r(rsrc_t W, int off_floats, const f32x16 (&X)[NT], f32x16 (&acc)[NT],
+                                                int lane, X3Ring<NT, DEP>& R, Fill&& fill, Mid&& mid, Late&& late,
+                                                Split&& onsplit) {
+  using RG = X3Ring<NT, DEP>;
+  constexpr int TPG = RG::TPG;
+  constexpr int NGR = RG::NGR;
+  constexpr int S = RG::S;
   constexpr int FPS = (4 * NT) / S > 0 ? (4 * NT) / S : 1;
   constexpr int FTOT = 4 * NT;
   constexpr int D = DEP;
-  f32x4 rh[D][TPG], rl[D][TPG];
+  auto& rh = R.rh;
+  auto& rl = R.rl;
   const int vo = lane * 32;
-  auto foff = [&](int step, int q) {
-    const int gi = step % NGR, ts = step / NGR;
-    const int tp = gi * TPG + q;
-    return (off_floats + ((tp * NT + (ts >> 1)) * 2 + (ts & 1)) * 512) * 4;
-  };
-#pragma unroll
-  for (int d = 0; d < D - 1; ++d)
-    if (d < S) {
-#pragma unroll
-      for (int q = 0; q < TPG; ++q) {
-        rh[d][q] = bload4(W, vo, foff(d, q));
-        rl[d][q] = bload4(W, vo + 16, foff(d, q));
-      }
-    }
+  auto foff = [&](int step, int q) { return RG::foff(off_floats, step, q); };
   f16x8 bh, bl;
   split_f16(X[0], 0, bh, bl);
   onsplit(0, bh, bl);
@@ -1572,6 +1602,9 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     const float dz = pbc1(sm.pos[i * 3 + 2] - cp(2), hbz);
     const float radial = dx * dx + dy * dy + dz * dz;                 // egcl.py:79
 
+    // GEMM1's first fragments requested now: their L2 round trip overlaps GEMM0
+    X3Ring<NT, XD> ring1;
+    if constexpr (PREC == PREC_F16X3) x3_prologue(ring1, W, L.we2x, lane);
     // ---- GEMM0: X0^T = edge_nn.0.weight . [h_i, h_j, radial]^T  (egcl.py:57-58)
     //      9 fixed k-steps (zero-padded past nf): 4 h_i pairs, 4 h_j pairs, radial;
     //      h rows are zero-padded in LDS, so padded steps multiply zeros
@@ -1661,7 +1694,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     // ---- GEMM1: E^T = edge_nn.2 (egcl.py:20-24)
     f32x16 e[NT];
     acc_from_bias<NT>(e, sm.bias + H, hh);
-    chain_prec_fill<PREC, NT, ENFLOW_FPM1, XD>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, [&](int step) {
+    auto fill1 = [&](int step) {
       const int t = (step >> 2) + 1, g4 = step & 3;
       if (t < NT) {
         const f32x4 y = act4s<VAR>((f32x4){x0[t][4 * g4], x0[t][4 * g4 + 1], x0[t][4 * g4 + 2], x0[t][4 * g4 + 3]},
@@ -1669,7 +1702,12 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
         for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = y[u];
       }
-    });
+    };
+    if constexpr (PREC == PREC_F16X3) chain_x3_fill_r<NT, ENFLOW_FPM1, XD>(W, L.we2x, x0, e, lane, ring1, fill1);
+    else chain_prec_fill<PREC, NT, ENFLOW_FPM1, XD>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, fill1);
+    // GEMM2's first fragments (the message-MFMA path) requested before e's activation
+    X3Ring<NT, XD> ring2;
+    if constexpr (PREC == PREC_F16X3 && MMA) x3_prologue(ring2, W, L.wc1x, lane);
     STAMP(11);
 #pragma unroll
     for (int g4 = 0; g4 < 4; ++g4) {
@@ -1827,7 +1865,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         }
       };
       if constexpr (PREC == PREC_F16X3) {
-        chain_x3_fill<NT, ENFLOW_FPM2, XD>(W, L.wc1x, e, hc, lane, fillm, NoMid{}, late, onsplit);
+        chain_x3_fill_r<NT, ENFLOW_FPM2, XD>(W, L.wc1x, e, hc, lane, ring2, fillm, NoMid{}, late, onsplit);
       } else {   // bf16 GEMM2: the image gets an fp16 hi / lo split of its own
         chain_b16_fill<NT, ENFLOW_FPM2>(W, L.wc1b, e, hc, lane, fillm, NoMid{}, late, [&](int ts) {
           f16x8 bh, bl;
