@@ -21,6 +21,7 @@ def main():
     c = bench.MODES[os.environ.get("AB_MODE", "forward")]
     from enflow_amd.data.synthetic import make_molecules
     model = bench.build_model(dev, c["layers"])
+    c = dict(c, mols=int(os.environ.get("AB_MOLS", c["mols"])))   # e.g. AB_MOLS=128: the latency instance
     inp = bench.batch_tensors(make_molecules(c["mols"], c["atoms"], nf=bench.NF, seed=1000, chain=c["chain"]), dev)
     model.gemm_precision = c["prec"]
     mols, atoms = c["mols"], c["atoms"]
