@@ -1790,7 +1790,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
       s16x4 ar[4][2];
       u32x4v tq[4];
       int rn = -1;
-      // LDS reads are issued one step (a chain step's MFMAs) before their use.
+      // LDS reads are issued MSTEP chain steps (their MFMAs) before their use.
       // Feature tile t's image is complete after k-slice 2 t + 1's split, at
       // step (2 t + 1) AB - 1, and k-slice 2 t + 2 overwrites it at the end of
       // step (2 t + 2) AB - 1 (AB = chain steps per k-slice)
