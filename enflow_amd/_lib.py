@@ -27,6 +27,7 @@ PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
 EGCL_ATTENTION, EGCL_NORM_DIFF, EGCL_TANH, EGCL_ACT = 1, 2, 4, 8   # ENFLOW_EGCL_* (include/enflow_hip.h)
 EGCL_VARIANTS = 0x100                                  # OR into gemm_precision
+BWD_F32 = 0x200                                        # ENFLOW_BWD_F32: OR into the backward's dequant_kind
 
 _i, _i64, _f, _p = ctypes.c_int, ctypes.c_int64, ctypes.c_float, ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -137,8 +138,27 @@ def lib(nf=None):
             fn = getattr(handle, name)
             fn.restype = res
             fn.argtypes = args
+        if _lat_threshold[0] is not None and hasattr(handle, "enflow_set_latency_threshold"):
+            handle.enflow_set_latency_threshold(_lat_threshold[0])
         _libs[path] = handle
     return handle
+
+
+_lat_threshold = [None]
+
+
+def set_latency_threshold(max_mols):
+    """Route fused <= 32-atom launches of at most `max_mols` molecules to the
+    8-wave latency instance (-1: the device's CU count, the default; 0: never).
+    The C setting is per library (enflow_set_latency_threshold): this applies
+    it to every loaded library and to any loaded later.  Returns the previous
+    setting (None: never set from Python)."""
+    prev = _lat_threshold[0]
+    _lat_threshold[0] = int(max_mols)
+    for h in _libs.values():
+        if hasattr(h, "enflow_set_latency_threshold"):
+            h.enflow_set_latency_threshold(int(max_mols))
+    return prev
 
 
 def ptr(t):
@@ -226,6 +246,8 @@ class KernelTimer:
 
 
 _pending = []
+# launches re-run with fp32 GEMMs after an ENFLOW_ERR_RANGE (inference and training; tests read it)
+FP32_RERUNS = [0]
 
 
 def defer_err(err_flag):
@@ -248,6 +270,20 @@ def check_pending():
         ev, host = _pending.pop(0)
         ev.synchronize()
         _raise_code(int(host.item()))
+
+
+def take_err(err_flag):
+    """Read (synchronises) and zero a non-zero device error word; returns the
+    code without raising and without touching queued (deferred) words."""
+    e = int(err_flag.item())
+    if e:
+        err_flag.zero_()
+    return e
+
+
+def raise_code(e):
+    """Raise for an error code read by take_err (no-op for 0)."""
+    _raise_code(e)
 
 
 def raise_on_err(err_flag, reset=False):
@@ -287,5 +323,6 @@ def _raise_code(e):
     if e & ERR_TOO_MANY_FEATURES:
         raise HipPathError(f"node_nf larger than the kernels' feature width (at most {MAX_NODE_NF})")
     if e & ERR_RANGE:
-        raise RangeError("the split-precision (f16x3 / bf16) GEMMs produced a non-finite result: an "
-                                 "operand is past the fp16 / bf16 range; run with gemm_precision='f32'")
+        raise RangeError("a split-precision (f16x3 / bf16) GEMM operand left the range its split "
+                         "represents at fp32 accuracy (an fp16 / bf16 overflow, or a layer whose "
+                         "operand is entirely below 2^-7 in f16x3); run with gemm_precision='f32'")

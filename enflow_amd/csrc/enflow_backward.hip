@@ -1196,6 +1196,7 @@ struct OuterDesc {
   const float* Lp;           // RECOMP_*: the layer's packed forward weights
   int nf;                    // RECOMP_X0: node features (xin row layout)
   const float* actp;         // the layer's act_fn (kind, p0, p1; packed layer + vfl + 1), NULL: SiLU
+  int f32r;                  // RECOMP_*: recompute on the fp32 MFMA (the ENFLOW_BWD_F32 backward)
 };
 // RECOMP_X0: X = silu(pre0), pre0 = edge_nn.0 . xin + be1 (the X source is xin, width ldx);
 // RECOMP_PC: DY = rowv * silu'(pc), pc = coord_nn.0 . X + bc1 (X read; no DY source), and
@@ -1407,7 +1408,11 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 #endif
 static_assert(ENFLOW_OUTER_X3 == 1, "pair-row weight gradients run on outer_x3_kernel (recomputed operands)");
 
-template <int H, int RCM, bool GEN = false>
+// F32R (the ENFLOW_BWD_F32 backward): the recomputed operands come from the
+// fp32 MFMA on the forward's fp32 fragments (we1f / wc1f), as that backward's
+// own recompute -- an f16x3 split of operands that are entirely small would
+// lose the accuracy the fp32 re-run was made for.
+template <int H, int RCM, bool GEN = false, bool F32R = false>
 __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int nbi, int r0, int r1,
                                               float (*sd)[128][OX_LD], float (*sx)[128][OX_LD]) {
   constexpr int NT = H / 32;
@@ -1434,7 +1439,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   // loaded once per workgroup and kept in registers (RECOMP_X0)
   // (the first k-step's; nf = 8's second k-step is read when used)
   f32x4 wfh = (f32x4)0.f, wfl = (f32x4)0.f;
-  if constexpr (rcm == RECOMP_X0) {
+  if constexpr (rcm == RECOMP_X0 && !F32R) {
     if (w < NT) {
       wfh = bload4(W, lane * 32, (L.we1x + (w * KS0MAX) * 512) * 4);
       wfl = bload4(W, lane * 32 + 16, (L.we1x + (w * KS0MAX) * 512) * 4);
@@ -1450,7 +1455,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   // ds_write_b128 (float4 e4 = q * 256 + tid: column e4 / 8, rows 4 (e4 % 8) ..),
   // 4x fewer memory instructions than one dword per row; ra4 / xa4 the 4 rows'
   // factors, raj row j's (the recompute's lane row)
-  struct Stage { float rd[16], rx[16], ra, xa; bool pv; f32x4 ra4, xa4; float raj; };
+  struct Stage { float rd[16], rx[16], ra, xa; bool pv; f32x4 ra4, xa4; float raj; const float* xb; };
   Stage S0;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
   // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
@@ -1463,6 +1468,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
     G.pv = pv;
     G.ra = 0.f;
     G.xa = 1.f;
+    G.xb = xblk;
 #if ENFLOW_OX_VEC
     if (rcm == RECOMP_PC) G.raj = pv ? D.rowv[rb + j] : 0.f;
     if constexpr (rcm != RECOMP_X0) {
@@ -1508,7 +1514,9 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         G.rd[q] = (pv && c < M) ? dblk[(unsigned)(q * 256 + tid)] : 0.f;
       }
     }
-    if constexpr (rcm == RECOMP_X0) {
+    if constexpr (rcm == RECOMP_X0 && F32R) {
+      // the fp32 GEMM0 reads its operands from the xin rows in lstore (G.xb)
+    } else if constexpr (rcm == RECOMP_X0) {
       // GEMM0's B operand of lane (row j, half hh), as the layer backward builds it
       // (k order gemm0_col): rx[8 ks + u] = k-slice ks, half 0 = h_i's features
       // 8 ks + u, half 1 = h_j's (+ radial in slot 7 of the last slice when that is
@@ -1599,7 +1607,33 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
 #pragma unroll
       for (int q = 0; q < 16; ++q) sd[buf][8 * q + (tid >> 5)][tid & 31] = G.rd[q];
     }
-    if constexpr (rcm == RECOMP_X0) {
+    if constexpr (rcm == RECOMP_X0 && F32R) {
+      if (w < NT) {   // output tile w of pre0 -> act -> X, fp32 MFMA (the forward's f32 GEMM0 k order)
+        f32x16 x = (f32x16)0.f;
+#pragma unroll
+        for (int s = 0; s < NFMAX + 1; ++s) {
+          int col = -1;
+          if (s < NFMAX / 2) {
+            const int f = 2 * s + hh;
+            if (f < nf) col = f;
+          } else if (s < NFMAX) {
+            const int f = 2 * (s - NFMAX / 2) + hh;
+            if (f < nf) col = nf + f;
+          } else if (hh == 0) {
+            col = 2 * nf;
+          }
+          const float b = (G.pv && col >= 0) ? G.xb[col * 32 + j] : 0.f;
+          x = mfma32(bload(W, lane * 4, (L.we1f + (w * (NFMAX + 1) + s) * 64) * 4), b, x);
+        }
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * w + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(D.Lp + L.be1 + f0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) sx[buf][f0 + u][j] = G.pv ? act_v<GEN>(act, x[4 * g4 + u] + b[u]) : 0.f;
+        }
+      }
+    } else if constexpr (rcm == RECOMP_X0) {
       if (w < NT) {   // output tile w of pre0 -> silu -> X
         const int ks_n = gemm0_ksteps(nf);
         f32x16 x = (f32x16)0.f;
@@ -1650,7 +1684,35 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   // tile w), DY = aphi * silu'(pc) into LDS, d wc2 partial += aphi * silu(pc)
   float (&wacc2)[16] = wacc;   // RECOMP_PC's d wc2 partials (lane = row, registers = features)
   auto recomp_pc = [&](int buf, const Stage& G) {
-    if (w < NT) {
+    if (F32R && w < NT) {   // fp32 chain of output tile w on wc1f (the forward's f32 k order)
+      f32x16 cacc = (f32x16)0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x16 X;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) X[r] = sx[buf][32 * t + rho(r, hh)][j];
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const f32x4 a4 = bload4(W, lane * 16, (L.wc1f + ((w * NT + t) * 4 + rg) * 256) * 4);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) cacc = mfma32(a4[u], X[4 * rg + u], cacc);
+        }
+      }
+      const float ra = ENFLOW_OX_VEC ? G.raj : G.ra;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int f0 = 32 * w + 8 * g4 + 4 * hh;
+        const f32x4 b = ld4(D.Lp + L.bc1 + f0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float z = cacc[4 * g4 + u] + b[u];
+          float fz, dz;
+          act_fd<GEN>(act, z, fz, dz);
+          wacc2[4 * g4 + u] = fmaf(ra, fz, wacc2[4 * g4 + u]);
+          sd[buf][f0 + u][j] = ra * dz;
+        }
+      }
+    } else if (w < NT) {
       // coord_nn.0's fragments of output tile w, requested half a chain at a time
       // (two L2 round trips per stage; resident they would cost 64 VGPRs across
       // the stage)
@@ -1824,7 +1886,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   }
 }
 
-template <bool GEN = false>
+template <bool GEN = false, bool F32R = false>
 __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBatch ob) {
   const int bid = blockIdx.x;
   const int k = find_desc(ob, bid);
@@ -1840,13 +1902,13 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
   // recomputed operands need the layer's hidden width at compile time
   // (one register allocation per branch: the modes' staged operands differ)
   if (D.recomp == RECOMP_X0) {
-    if (D.N == 128) outer_x3_body<128, RECOMP_X0, GEN>(D, chunk, nbi, r0, r1, sd, sx);
-    else if (D.N == 64) outer_x3_body<64, RECOMP_X0, GEN>(D, chunk, nbi, r0, r1, sd, sx);
-    else outer_x3_body<32, RECOMP_X0, GEN>(D, chunk, nbi, r0, r1, sd, sx);
+    if (D.N == 128) outer_x3_body<128, RECOMP_X0, GEN, F32R>(D, chunk, nbi, r0, r1, sd, sx);
+    else if (D.N == 64) outer_x3_body<64, RECOMP_X0, GEN, F32R>(D, chunk, nbi, r0, r1, sd, sx);
+    else outer_x3_body<32, RECOMP_X0, GEN, F32R>(D, chunk, nbi, r0, r1, sd, sx);
   } else if (D.recomp == RECOMP_PC) {
-    if (D.N == 128) outer_x3_body<128, RECOMP_PC, GEN>(D, chunk, nbi, r0, r1, sd, sx);
-    else if (D.N == 64) outer_x3_body<64, RECOMP_PC, GEN>(D, chunk, nbi, r0, r1, sd, sx);
-    else outer_x3_body<32, RECOMP_PC, GEN>(D, chunk, nbi, r0, r1, sd, sx);
+    if (D.N == 128) outer_x3_body<128, RECOMP_PC, GEN, F32R>(D, chunk, nbi, r0, r1, sd, sx);
+    else if (D.N == 64) outer_x3_body<64, RECOMP_PC, GEN, F32R>(D, chunk, nbi, r0, r1, sd, sx);
+    else outer_x3_body<32, RECOMP_PC, GEN, F32R>(D, chunk, nbi, r0, r1, sd, sx);
   } else {
     outer_x3_body<128, RECOMP_NONE, GEN>(D, chunk, nbi, r0, r1, sd, sx);
   }
@@ -2301,6 +2363,7 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.Lp = nullptr;
   D.nf = 0;
   D.actp = nullptr;
+  D.f32r = 0;
   D.chunk = tiled ? OA_CHUNK : OA_CHUNK_ATOM;
   D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
   D.rows_dev = rows_dev; D.rows_static = rows_static;
@@ -2351,9 +2414,13 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
       swg += ob.start[k + 1] - ob.start[k];
       sub.start[++sub.nd] = swg;
     }
-    bool gen = false;
-    for (int k = 0; k < sub.nd; ++k) gen |= sub.d[k].actp != nullptr;
-    if (swg > 0 && gen) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel<true>, dim3(swg), dim3(256), 0, st, sub));
+    bool gen = false, f32r = false;
+    for (int k = 0; k < sub.nd; ++k) {
+      gen |= sub.d[k].actp != nullptr;
+      f32r |= sub.d[k].f32r != 0;
+    }
+    if (swg > 0 && f32r) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL((outer_x3_kernel<true, true>), dim3(swg), dim3(256), 0, st, sub));
+    else if (swg > 0 && gen) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel<true>, dim3(swg), dim3(256), 0, st, sub));
     else if (swg > 0) ENFLOW_TIMED("outer_x3_kernel", st, hipLaunchKernelGGL(outer_x3_kernel<false>, dim3(swg), dim3(256), 0, st, sub));
   }
   (void)wg;
@@ -2387,7 +2454,7 @@ static int run_outer(OuterBatch& ob, int wg, hipStream_t st) {
 // rows) and atom rows, straight into the torch parameter layout G.
 static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const int32_t* prow, int prb,
                               bool variants, float* G, const float* Rp, const RawEgcl& R, const float* hx,
-                              int num_atoms, int nf, int H, const float* Lp) {
+                              int num_atoms, int nf, int H, const float* Lp, bool f32b = false) {
     OuterBatch ob;
     ob.nd = 0;
     int wg = 0;
@@ -2398,12 +2465,14 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     // edge_nn.2: X = silu(pre0), pre0 recomputed from the xin rows
     // the layer's act_fn (variant layers; packed layer + vfl + 1): the recomputed
     // activations and their derivatives follow it (NULL: SiLU instances)
-    const float* actp = variants ? Lp + egcl_layout(H, nf).vfl + 1 : nullptr;
+    // (the fp32 backward always runs the generic instances)
+    const float* actp = (variants || f32b) ? Lp + egcl_layout(H, nf).vfl + 1 : nullptr;
     add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.xin, XW, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
     ob.d[ob.nd - 1].recomp = RECOMP_X0;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
     ob.d[ob.nd - 1].actp = actp;
+    ob.d[ob.nd - 1].f32r = f32b;
     // coord_nn.0: X = silu(pre_e) = the message; DY = aphi * wc2 * silu'(pc), pc recomputed from X
     add_desc(ob, wg, nullptr, H, H, wb + Wl.pe, H, H, prow, 0, prb, part,
              G + R.Wc1, G + R.bc1, PAIR_OUTER);
@@ -2416,6 +2485,7 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
     ob.d[ob.nd - 1].actp = actp;
+    ob.d[ob.nd - 1].f32r = f32b;
     // coord_nn.2: d wc2 = sum_rows aphi silu(pc), folded into coord_nn.0's pass (its partials
     // written there; this descriptor only sizes them and feeds the reduction)
     add_desc(ob, wg, wb + Wl.aphi, 1, 1, nullptr, H, H, prow, 0, prb, part, G + R.wc2, nullptr, 3);
@@ -2537,8 +2607,10 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
                             void* workspace, int64_t workspace_bytes, int64_t pair_row_bound,
                             int32_t* err_flag, void* stream,
                             const float* eg_dQ, const float* eg_dF, const float* eg_dG) {
-  // dequant_kind may carry ENFLOW_EGCL_VARIANTS: layers with norm_diff / tanh flags
+  // dequant_kind may carry ENFLOW_EGCL_VARIANTS (layers with norm_diff / tanh
+  // flags) and ENFLOW_BWD_F32 (the tape of an fp32-GEMM forward: fp32 backward)
   const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
+  const bool f32b = (dequant_kind & ENFLOW_BWD_F32) != 0;
   dequant_kind &= 0xff;
   if (num_mols < 0 || num_atoms < 0 || max_mol_atoms < 0 || max_mol_atoms > 64 || nf < 1 || nf > BWD_NFMAX ||
       !hid_ok_b(H) || n_layers < 0 || pair_row_bound < 0 || pair_row_bound > 0x7fffffffLL)
@@ -2604,7 +2676,11 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
     A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
     A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
-    if (variants) {
+    if (f32b) {   // generic (VAR) instance: any flags / act_fn
+#define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true, PREC_F32>), dim3(num_mols), dim3(BLOCK), 0, st, A))
+      DISPATCH_HN_B(H, max_mol_atoms, CALL);
+#undef CALL
+    } else if (variants) {
 #define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);
 #undef CALL
@@ -2620,7 +2696,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
                                       grad_layers + (size_t)l * R.total_bwd, A.Rp, R,
                                       tape + tape_layout(num_atoms, nf, H, n_layers).hx +
                                           (size_t)l * num_atoms * (nf + H),
-                                      num_atoms, nf, H, A.Lp);
+                                      num_atoms, nf, H, A.Lp, f32b);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
     if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;
@@ -2705,6 +2781,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
                                   int64_t pair_row_bound, int32_t* err_flag, void* stream, const float* eg_dQ,
                                   const float* eg_dF, const float* eg_dG) {
   const bool variants = (dequant_kind & ENFLOW_EGCL_VARIANTS) != 0;
+  const bool f32b = (dequant_kind & ENFLOW_BWD_F32) != 0;
   dequant_kind &= 0xff;
   const int64_t need = enflow_lf_backward_large_workspace_size(num_mols, num_atoms, max_mol_atoms, nf, H,
                                                                pair_row_bound);
@@ -2775,7 +2852,8 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
     A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
 #define CALLB(HH)                                                                                              \
   do {                                                                                                         \
-    if (variants) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, true, ENFLOW_BWD_PREC, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
+    if (f32b) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, true, PREC_F32, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
+    else if (variants) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, true, ENFLOW_BWD_PREC, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
     else ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, 32, false, ENFLOW_BWD_PREC, true>), dim3(grid), dim3(BLOCK), 0, st, A)); \
   } while (0)
     if (H == 32) CALLB(32);
@@ -2792,7 +2870,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
       return -2;
     const int rc = layer_weight_grads(st2, Wl, wb, tot_l, prb, variants, grad_layers + (size_t)l * R.total_bwd,
                                       A.Rp, R, tape + T.hx + (size_t)l * num_atoms * (nf + H), num_atoms, nf, H,
-                                      A.Lp);
+                                      A.Lp, f32b);
     if (rc) return rc;
     if (hipEventRecord(ev(2 * l + 1), st2) != hipSuccess) return -2;
     if (serial && hipStreamWaitEvent(st, ev(2 * l + 1), 0) != hipSuccess) return -2;
@@ -2856,7 +2934,7 @@ int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int
   float* zero = ag + al64((size_t)num_atoms * nf);
   if (hipMemsetAsync(zero, 0, 64 * sizeof(float), SB(stream)) != hipSuccess) return -2;
   return lf_backward_impl(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, tape, pair_counts, layer,
-                          layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | (egcl_flags ? ENFLOW_EGCL_VARIANTS : 0),
+                          layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | ((egcl_flags & 0xff) ? ENFLOW_EGCL_VARIANTS : 0) | (egcl_flags & ENFLOW_BWD_F32),
                           nullptr, nullptr, nullptr, 0.f, cw, adj_h, ag, adj_pos, avel, zero, grad_layer, nullptr,
                           workspace, workspace_bytes, pair_row_bound, err_flag, stream, adj_Q, adj_F, adj_G);
 }
@@ -2888,7 +2966,7 @@ int enflow_egcl_backward_large_f32(int num_mols, int num_atoms, int max_mol_atom
   float* zero = ag + al64((size_t)num_atoms * nf);
   if (hipMemsetAsync(zero, 0, 64 * sizeof(float), SB(stream)) != hipSuccess) return -2;
   return lf_backward_large_impl(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, tape, layer,
-                                layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | (egcl_flags ? ENFLOW_EGCL_VARIANTS : 0),
+                                layer_bwd, layer_raw, 1, ENFLOW_DEQUANT_NONE | ((egcl_flags & 0xff) ? ENFLOW_EGCL_VARIANTS : 0) | (egcl_flags & ENFLOW_BWD_F32),
                                 nullptr, nullptr, nullptr, 0.f, cw, adj_h, ag, adj_pos, avel, zero, grad_layer,
                                 nullptr, workspace, w, pair_row_bound, err_flag, stream, adj_Q, adj_F, adj_G);
 }

@@ -468,13 +468,21 @@ static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs
 // CU) for <= 32-atom molecules when the batch has at most `threshold`
 // molecules; -1 (default): the device's CU count, i.e. whenever the 256-thread
 // kernel's two-per-CU slots would not all be busy for one round.
+// The threshold is a per-library setting (libenflow_hip.so and _nf16.so each
+// hold one; enflow_amd._lib.set_latency_threshold sets every loaded library).
 static int g_lat_threshold = -1;
+static int g_cus[64];   // CU count per device ordinal (0: not queried yet), cached off the launch path
 static int lat_threshold_now() {
   if (g_lat_threshold >= 0) return g_lat_threshold;
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
-  return cus;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (dev < 0 || dev >= 64) return 0;
+  if (g_cus[dev] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 0;
+    g_cus[dev] = cus;
+  }
+  return g_cus[dev];
 }
 
 template <int HH, int NN, int RBB, bool REV>

@@ -334,6 +334,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   if (tid < 32) sm.cntrow[tid] = tid < rb ? B.cntrow[g0 + tid] : 0;
   if (tid == 0) {
     sm.err = 0;
+    sm.big = 0u;
     int acc = 0;
     for (int a = 0; a < rb; ++a) { roff[a] = acc; acc += B.npairs[g0 + a]; }
     for (int a = rb; a <= 32; ++a) roff[a] = acc;
@@ -362,6 +363,9 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   }
   if constexpr (PREC != PREC_F32) node_phase_x3<H, 32, 32, VAR>(sm, B.layer, L, rb, nf, tid, 0, rb);
   else node_phase<H, 32, 32, VAR>(sm, B.layer, L, rb, nf, tid, 0, rb);
+  if constexpr (PREC == PREC_F16X3) {   // small-operand guard of the row block (BIGK_*)
+    if (tid == 0 && small_operands(sm.big)) sm.err |= ENFLOW_ERR_RANGE;
+  }
   if (tid == 0 && sm.err) atomicOr(B.err, sm.err);   // edge tiles' range check (split precision)
 
   const bool tape = mode == 0 && B.tape != nullptr;

@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 10
+#define ENFLOW_ABI 11
 #ifndef WAVES
 #define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
 #endif
@@ -433,7 +433,7 @@ __device__ __forceinline__ float sigm_exact(float x) { return 1.f / (1.f + expf(
 // as calls, the generic path costs a call per element and the SiLU path nothing.
 __device__ __attribute__((noinline)) float act_f(const Act& A, float z) {
   switch (A.k) {
-    case ACT_RELU: return z > 0.f ? z : 0.f;
+    case ACT_RELU: return z < 0.f ? 0.f : z;   // NaN stays NaN (torch.relu)
     case ACT_LEAKY_RELU: return z > 0.f ? z : A.p0 * z;
     case ACT_ELU: return z > 0.f ? z : A.p0 * expm1f(z);
     case ACT_CELU: return z > 0.f ? z : A.p0 * expm1f(z / A.p0);
@@ -447,14 +447,14 @@ __device__ __attribute__((noinline)) float act_f(const Act& A, float z) {
     case ACT_SIGMOID: return sigm_exact(z);
     case ACT_SOFTPLUS: return z * A.p0 > A.p1 ? z : log1pf(expf(A.p0 * z)) / A.p0;
     case ACT_MISH: return z * tanhf(z > 20.f ? z : log1pf(expf(z)));
-    case ACT_HARDTANH: return fminf(fmaxf(z, A.p0), A.p1);
+    case ACT_HARDTANH: return __builtin_isnan(z) ? z : fminf(fmaxf(z, A.p0), A.p1);   // NaN stays NaN
     case ACT_IDENTITY: return z;
     default: return z * sigm_exact(z);   // ACT_SILU
   }
 }
 __device__ __attribute__((noinline)) float act_d(const Act& A, float z) {
   switch (A.k) {
-    case ACT_RELU: return z > 0.f ? 1.f : 0.f;
+    case ACT_RELU: return z <= 0.f ? 0.f : 1.f;   // threshold_backward: where(z <= 0, 0, grad)
     case ACT_LEAKY_RELU: return z > 0.f ? 1.f : A.p0;
     case ACT_ELU: return z > 0.f ? 1.f : A.p0 * expf(z);
     case ACT_CELU: return z > 0.f ? 1.f : expf(z / A.p0);
@@ -473,7 +473,7 @@ __device__ __attribute__((noinline)) float act_d(const Act& A, float z) {
       const float sp = z > 20.f ? z : log1pf(expf(z)), th = tanhf(sp);
       return th + z * sigm_exact(z) * (1.f - th * th);
     }
-    case ACT_HARDTANH: return (z > A.p0 && z < A.p1) ? 1.f : 0.f;
+    case ACT_HARDTANH: return (z <= A.p0 || z >= A.p1) ? 0.f : 1.f;   // hardtanh_backward's mask
     case ACT_IDENTITY: return 1.f;
     default: { const float s = sigm_exact(z); return s * (1.f + z * (1.f - s)); }
   }
@@ -822,6 +822,38 @@ __device__ __forceinline__ s16x4 lds_tr16(const uint32_t* p) {
 __device__ __forceinline__ f16x8 cat_f16x8(s16x4 a, s16x4 b) {
   return __builtin_bit_cast(f16x8, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
 }
+
+// F16X3 small-operand guard.  A split x = hi + lo holds x to fp32 accuracy
+// only while lo = x - hi is a normal fp16, i.e. |x| >~ 2^-3: activation
+// operands carry no power-of-two scale, so an operand whose values are ALL
+// small loses relative accuracy (1e-3: ~1.7e-5 normwise per GEMM).  Per
+// molecule (row block) and layer, each GEMM operand kind records whether any
+// of its values reached 2^-7 (fp16 exponent field >= 8: bit 13 or 14 of a hi
+// half set; OR of the packed hi words, two words per v_or3); a kind that never
+// did flags ENFLOW_ERR_RANGE and the host re-runs the launch with fp32 GEMMs.
+// Unflagged, the worst case is an operand whose max is just above 2^-7:
+// ~2e-6 normwise per GEMM.
+#define ENFLOW_BIG_BITS 0x60006000u
+enum {
+  BIGK_X0 = 1,      // edge_nn.0 input [h_i, h_j, radial]
+  BIGK_Y0 = 2,      // edge_nn.2 input act(edge_nn.0 ..)
+  BIGK_M = 4,       // coord_nn.0 input (the messages)
+  BIGK_HV = 8,      // vel_scaling_nn.0 input h
+  BIGK_HA = 16,     // node_nn.0 input [h, agg]
+  BIGK_NH = 32,     // node_nn.2 input act(node_nn.0 ..)
+  BIGK_EDGE = 64,   // the block ran edge tiles
+  BIGK_NODE = 128   // the block ran node items
+};
+__device__ __forceinline__ uint32_t or_hi(uint32_t acc, const f16x8& bh) {
+  const u32x4v v = __builtin_bit_cast(u32x4v, bh);
+  return acc | v[0] | v[1] | v[2] | v[3];
+}
+// the kinds that ran but never saw a value >= 2^-7
+__device__ __forceinline__ bool small_operands(uint32_t big) {
+  const uint32_t need = ((big & BIGK_EDGE) ? (BIGK_X0 | BIGK_Y0 | BIGK_M) : 0u) |
+                        ((big & BIGK_NODE) ? (BIGK_HV | BIGK_HA | BIGK_NH) : 0u);
+  return (big & need) != need;
+}
 // x = hi + lo in fp16.  ENFLOW_SPLIT_MIX: lo = f16(x - hi) by v_fma_mix{lo,hi}_f16
 // reading hi straight from its packed fp16 register (x * 1 - hi in one fused
 // op, one rounding), 1.5 VALU per element instead of 3 (convert hi back to
@@ -830,23 +862,36 @@ __device__ __forceinline__ f16x8 cat_f16x8(s16x4 a, s16x4 b) {
 #define ENFLOW_SPLIT_MIX 1
 #endif
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t split_lo2(float x0, float x1, uint32_t hi) {
-  uint32_t lo;
-  asm("v_fma_mixlo_f16 %0, %1, 1.0, -%3 op_sel_hi:[0,0,1]\n\t"
-      "v_fma_mixhi_f16 %0, %2, 1.0, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
-      : "=&v"(lo) : "v"(x0), "v"(x1), "v"(hi));
-  return lo;
+// The four lo words of a k-slice in ONE statement that ends with `s_nop 1`:
+// its last v_fma_mix writes a VGPR an MFMA reads as its B operand, and hipcc
+// pads no VALU-write -> MFMA-read hazard (2 wait states) for an asm output
+// (cdna_hip_programming.md §5.7 item 2; tools/asm_hazard_scan.py check (b):
+// as four statements the large-system kernel read the last word 1 state after
+// its write).
+#define ENFLOW_MIX2(D, A, B, H)                                                   \
+  "v_fma_mixlo_f16 " D ", " A ", 1.0, -" H " op_sel_hi:[0,0,1]\n\t"              \
+  "v_fma_mixhi_f16 " D ", " B ", 1.0, -" H " op_sel:[0,0,1] op_sel_hi:[0,0,1]\n\t"
+__device__ __forceinline__ void split_lo8(const float (&x)[8], const uint32_t (&h)[4], uint32_t (&l)[4]) {
+  asm(ENFLOW_MIX2("%0", "%4", "%5", "%12") ENFLOW_MIX2("%1", "%6", "%7", "%13")
+      ENFLOW_MIX2("%2", "%8", "%9", "%14") ENFLOW_MIX2("%3", "%10", "%11", "%15")
+      "s_nop 1"
+      : "=&v"(l[0]), "=&v"(l[1]), "=&v"(l[2]), "=&v"(l[3])
+      : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(x[4]), "v"(x[5]), "v"(x[6]), "v"(x[7]),
+        "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
 }
+#undef ENFLOW_MIX2
 __device__ __forceinline__ void split_f16(const f32x16& X, int s, f16x8& hi, f16x8& lo) {
 #if ENFLOW_SPLIT_MIX
   uint32_t h[4], l[4];
+  float x[8];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const float x0 = X[8 * s + 2 * j], x1 = X[8 * s + 2 * j + 1];
-    const f16x2 hp = {(_Float16)x0, (_Float16)x1};          // v_cvt_pk_f16_f32 (RNE)
+    x[2 * j] = X[8 * s + 2 * j];
+    x[2 * j + 1] = X[8 * s + 2 * j + 1];
+    const f16x2 hp = {(_Float16)x[2 * j], (_Float16)x[2 * j + 1]};   // v_cvt_pk_f16_f32 (RNE)
     h[j] = __builtin_bit_cast(uint32_t, hp);
-    l[j] = split_lo2(x0, x1, h[j]);
   }
+  split_lo8(x, h, l);
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   hi = __builtin_bit_cast(f16x8, (u32x4){h[0], h[1], h[2], h[3]});
   lo = __builtin_bit_cast(f16x8, (u32x4){l[0], l[1], l[2], l[3]});
@@ -1058,10 +1103,11 @@ __device__ __forceinline__ void chain_b16_fill(rsrc_t W, int off_floats, const f
 }
 
 // GEMM with the precision's chain; off_* are the packed sections of the matrix
-template <int PREC, int NT, int FPM, int DEP = ENFLOW_X3_DEPTH, class Fill, class Mid = NoMid>
+template <int PREC, int NT, int FPM, int DEP = ENFLOW_X3_DEPTH, class Fill, class Mid = NoMid, class Split = NoSplit>
 __device__ __forceinline__ void chain_prec_fill(rsrc_t W, int off_f32, int off_x3, int off_b16, const f32x16 (&X)[NT],
-                                                f32x16 (&acc)[NT], int lane, Fill&& fill, Mid&& mid = NoMid{}) {
-  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM, DEP>(W, off_x3, X, acc, lane, fill, mid);
+                                                f32x16 (&acc)[NT], int lane, Fill&& fill, Mid&& mid = NoMid{},
+                                                Split&& onsplit = NoSplit{}) {
+  if constexpr (PREC == PREC_F16X3) chain_x3_fill<NT, FPM, DEP>(W, off_x3, X, acc, lane, fill, mid, NoLate{}, onsplit);
   else if constexpr (PREC == PREC_BF16) chain_b16_fill<NT, FPM>(W, off_b16, X, acc, lane, fill, mid);
   else chain_gemm_fill<NT, FPM>(W, off_f32, X, acc, lane, fill, mid);
 }
@@ -1188,6 +1234,7 @@ struct Smem {
   int npairs;                         // pairs in the buffer (this pass)
   int ptotal;                         // pairs of the whole block
   int err;
+  uint32_t big;                       // BIGK_* seen this layer / row block (F16X3 small-operand guard)
   float red[WAVES];
   static constexpr int NDT = BWD ? 1 : NT, NDR = BWD ? 1 : RB;
   // <= 32-atom images (and the large-system row blocks): the edge tiles' message
@@ -1551,10 +1598,18 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   // sigmoid) are tested here, everything else propagates to the outputs, which
   // the kernels test as well (ENFLOW_ERR_RANGE)
   bool range_bad = false;
+  constexpr bool GUARD = PREC == PREC_F16X3;   // small-operand guard (BIGK_*)
+  uint32_t bigw = 0u;                          // wave-uniform
   STAMP(8);
   for (int tile = t0; tile < t1; ++tile) {
     const int p = tile * 32 + j;
     const bool valid = p < P;
+    uint32_t o0 = 0u, o1 = 0u, o2 = 0u;   // OR of the operands' packed fp16 hi words
+    const uint32_t vmask = valid ? ENFLOW_BIG_BITS : 0u;   // padding lanes (row 0's atoms) do not count
+    // each kind's word is tested right after its GEMM (one VGPR live through one chain)
+    auto seen_big = [&](uint32_t o, uint32_t kind) {
+      if constexpr (GUARD) bigw |= __ballot((o & vmask) != 0u) ? kind : 0u;
+    };
     const uint32_t pr = valid ? sm.pairs[p] : 0u;
     const int il = pair_row<BIG>(pr);
     const int jl = BIG ? (int)((pr >> 5) & 0x3fffffu) : (int)((pr >> 8) & 0xffu);
@@ -1635,6 +1690,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         }
         f16x8 bh, bl;
         split_f16(in, 0, bh, bl);
+        if constexpr (GUARD) o0 = or_hi(o0, bh);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
           f32x4 ah, al;
@@ -1680,6 +1736,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
       }
     }
     STAMP(9);
+    seen_big(o0, BIGK_X0);
     // x0 tile 0 activated now, tiles 1.. as fillers of GEMM1's steps on tile t-1
     // (split-precision GEMM0 accumulators carry edge_nn.0's 2^s: unscaled in the bias fma)
 #pragma unroll
@@ -1703,8 +1760,11 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = y[u];
       }
     };
-    if constexpr (PREC == PREC_F16X3) chain_x3_fill_r<NT, ENFLOW_FPM1, XD>(W, L.we2x, x0, e, lane, ring1, fill1);
+    if constexpr (PREC == PREC_F16X3)
+      chain_x3_fill_r<NT, ENFLOW_FPM1, XD>(W, L.we2x, x0, e, lane, ring1, fill1, NoMid{}, NoLate{},
+                                           [&](int, const f16x8& bh, const f16x8&) { o1 = or_hi(o1, bh); });
     else chain_prec_fill<PREC, NT, ENFLOW_FPM1, XD>(W, L.we2f, L.we2x, L.we2b, x0, e, lane, fill1);
+    seen_big(o1, BIGK_Y0);
     // GEMM2's first fragments (the message-MFMA path) requested before e's activation
     X3Ring<NT, XD> ring2;
     if constexpr (PREC == PREC_F16X3 && MMA) x3_prologue(ring2, W, L.wc1x, lane);
@@ -1848,6 +1908,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
         }
       };
       auto onsplit = [&](int ts, const f16x8& bh, const f16x8& bl) {
+        if constexpr (GUARD) o2 = or_hi(o2, bh);
         const u32x4v hv = __builtin_bit_cast(u32x4v, bh), lv = __builtin_bit_cast(u32x4v, bl);
         uint32_t* const r = img + j * MIS + 2 * hh + 8 * (ts & 1);   // 4-feature unit 4 s + hh (+2, +8: lo)
         *reinterpret_cast<u32x2v*>(r) = (u32x2v){hv[0], hv[1]};
@@ -1873,6 +1934,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
           onsplit(ts, bh, bl);
         });
       }
+      seen_big(o2, BIGK_M);
       // coord_nn.2 as a per-pair dot
 #pragma unroll
       for (int tp = 0; tp < NT; ++tp)
@@ -1908,8 +1970,11 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
 #pragma unroll
           for (int u = 0; u < 4; ++u) e[t + 1][4 * g4 + u] = y[u];
         }
-      }, [&] { reduce_chunk(0); });
+      }, [&] { reduce_chunk(0); }, [&](int, const f16x8& bh, const f16x8&) {
+        if constexpr (GUARD) o2 = or_hi(o2, bh);
+      });
       reduce_chunk(NT == 4 ? 1 : 0);
+      seen_big(o2, BIGK_M);
       // coord_nn.2 as a per-pair dot
 #pragma unroll
       for (int tp = 0; tp < NT; ++tp)
@@ -1942,6 +2007,9 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   if constexpr (PREC != PREC_F32) {
     if (__ballot(range_bad))
       if (lane == 0) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
+  }
+  if constexpr (GUARD) {
+    if (lane == 0 && t1 > t0) atomicOr(&sm.big, bigw | (uint32_t)BIGK_EDGE);
   }
   pre();
   __syncthreads();
@@ -2120,6 +2188,7 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
   auto& al = F.al;
   auto issue = [&](int it) { F.issue(W, L, lane, it); };
   if (!issued && w < NT * NA) issue(w);
+  uint32_t bigw = 0u;   // small-operand guard (BIGK_*), wave-uniform
   // vel_scaling_nn.0 / .2 and node_nn.0 biases staged in LDS (edge_tiles' bias
   // image is free now)
   for (int k = tid; k < H; k += BLOCK) {
@@ -2140,6 +2209,8 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
     for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && 8 * hh + jj < nf) ? sm.h[ag * NFP + 8 * hh + jj] : 0.f;
     f16x8 hh16, hl16;
     split_f16(hin, 0, hh16, hl16);
+    const uint32_t oh = or_hi(0u, hh16);
+    uint32_t oa = oh, on = 0u;
     // vel_scaling_nn: Q partial over this wave's 32 hidden features
     f32x16 acc = (f32x16)0.f;
     acc = mfma_f16(vh, hh16, acc);
@@ -2176,6 +2247,7 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
       }
       f16x8 bh, bl;
       split_f16(av, 0, bh, bl);
+      oa = or_hi(oa, bh);
       acc = mfma_f16(ah[ks], bh, acc);
       acc = mfma_f16(ah[ks], bl, acc);
       acc = mfma_f16(al[ks], bh, acc);
@@ -2192,9 +2264,16 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
     for (int s2 = 0; s2 < 2; ++s2) {
       f16x8 bh, bl;
       split_f16(acc, s2, bh, bl);
+      on = or_hi(on, bh);
       gacc = mfma_f16(gfh[s2], bh, gacc);
       gacc = mfma_f16(gfh[s2], bl, gacc);
       gacc = mfma_f16(gfl[s2], bh, gacc);
+    }
+    {   // padding atoms do not count
+      const uint32_t vm = va ? ENFLOW_BIG_BITS : 0u;
+      bigw |= (__ballot((oh & vm) != 0u) ? (uint32_t)BIGK_HV : 0u) |
+              (__ballot((oa & vm) != 0u) ? (uint32_t)BIGK_HA : 0u) |
+              (__ballot((on & vm) != 0u) ? (uint32_t)BIGK_NH : 0u);
     }
     if (item + WAVES < NT * NA) issue(item + WAVES);
     if (va) {
@@ -2205,6 +2284,7 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
       }
     }
   }
+  if (lane == 0 && w < NT * NA) atomicOr(&sm.big, bigw | (uint32_t)BIGK_NODE);
   __syncthreads();
   node_partials_reduce(sm, Lp, L, nf, tid, r0, rb);
 }
@@ -2413,7 +2493,10 @@ __device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowA
     if (what & LOAD_H) sm.h[e] = q < nf ? hin[src] : 0.f;
     if (what & LOAD_VELG) sm.g[e] = q < nf ? gin[src] : 0.f;
   }
-  if (tid == 0) sm.err = 0;
+  if (tid == 0) {
+    sm.err = 0;
+    sm.big = 0u;
+  }
   __syncthreads();
   if ((what & LOAD_POS) && n > 0) {
     M.bx = sm.boxa[0];

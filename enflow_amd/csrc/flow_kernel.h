@@ -157,6 +157,12 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
         else node_phase<H, NMAX, RB, VAR>(sm, Lp, L, n, nf, tid_l, r0, rb);
       }
       STAMP(5);
+      if constexpr (PREC == PREC_F16X3) {   // every F16X3 operand kind saw a value >= 2^-7 (BIGK_*)?
+        if (tid == 0) {
+          if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_RANGE;
+          sm.big = 0u;   // next written after this layer's / block's barriers
+        }
+      }
       if (!REV && A.tape != nullptr) {   // training tape: layer-input state + message sums + Q
         const TapeLayout T = tape_layout(A.num_atoms, nf, H, A.n_layers);
         const size_t la = (size_t)l * A.num_atoms + M.a0 + r0;

@@ -57,6 +57,8 @@ class _FlowFunction(torch.autograd.Function):
         flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"], meta["max_n"],
                              meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts, prec=prec,
                              src=src, ticket=st[1:])
+        # an fp32-GEMM forward's tape gets the fp32-GEMM backward (ENFLOW_BWD_F32)
+        ctx.bwd_f32 = (prec & 0xff) == _lib.PREC_F32
         # queue the backward's weight packing (cached on the parameters' versions,
         # which cannot change before this graph's backward) and the dequantiser's
         # flat parameters behind the forward kernel, ahead of the error check's sync
@@ -71,10 +73,25 @@ class _FlowFunction(torch.autograd.Function):
             if getattr(flow, "defer_error_check", False):
                 # no host sync: the word is read at the start of this graph's
                 # backward (before anything consumes the outputs' gradients) or
-                # at the next check
+                # at the next check; an ENFLOW_ERR_RANGE then raises (the outputs
+                # were consumed already, so the step cannot be re-run)
                 _lib.defer_err(err)
             else:
-                _lib.raise_on_err(err)      # the reference raises inside forward
+                _lib.check_pending()        # an older deferred word is not this launch's
+                e = _lib.take_err(err)
+                if e == _lib.ERR_RANGE and (prec & 0xff) != _lib.PREC_F32:
+                    # a split-precision operand left its range (an fp16 overflow, or an
+                    # operand entirely below 2^-7): the step's forward again with fp32
+                    # GEMMs, same inputs and draws, and the fp32 backward on its tape
+                    prec = (prec & ~0xff) | _lib.PREC_F32
+                    counts.zero_()
+                    flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"],
+                                         meta["max_n"], meta["noise"], ldj_mol, ldj, err, tape=tape,
+                                         pair_counts=counts, prec=prec, src=src, ticket=st[1:])
+                    ctx.bwd_f32 = True
+                    _lib.FP32_RERUNS[0] += 1
+                    e = _lib.take_err(err)
+                _lib.raise_code(e)          # the reference raises inside forward
         ctx.flow, ctx.meta, ctx.kind = flow, meta, kind
         ctx.n_params = len(params)
         ctx.save_for_backward(h_in, tape, counts)
@@ -109,7 +126,7 @@ class _FlowFunction(torch.autograd.Function):
             dq_raw = ctx.dq_raw
             grad_dq = torch.empty_like(dq_raw)
         err = torch.zeros(1, dtype=torch.int32, device=dev)
-        kindv = kind | (_lib.EGCL_VARIANTS if flow._has_variants() else 0)
+        kindv = kind | (_lib.EGCL_VARIANTS if flow._has_variants() else 0) | (_lib.BWD_F32 if ctx.bwd_f32 else 0)
         if meta["large"]:
             # the forward counted each layer's pair rows on the device: size the
             # workspace by their maximum (one small read; large systems only)
@@ -136,9 +153,16 @@ class _FlowFunction(torch.autograd.Function):
                 ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
             except torch.cuda.OutOfMemoryError:
                 # three rotating pair-row buffers do not fit: two (the layer chain
-                # then waits for the weight-gradient pass two layers up)
+                # then waits for the weight-gradient pass two layers up); the failed
+                # request's cached blocks are released first
+                torch.cuda.empty_cache()
                 wsb = L.enflow_lf_backward_workspace_size_min(M, A, nf, hid, n_layers, prb)
-                ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                try:
+                    ws = torch.empty(max(wsb, 1), dtype=torch.uint8, device=dev)
+                except torch.cuda.OutOfMemoryError as exc:
+                    raise torch.cuda.OutOfMemoryError(
+                        f"enflow_amd backward workspace ({wsb / 2**30:.2f} GiB with two rotating pair-row "
+                        "buffers, the ENFLOW_BWD_MIN_WS=1 size) does not fit: train on a smaller batch") from exc
             _lib.check(L.enflow_lf_backward_f32(
                 M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
                 _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd),
@@ -306,6 +330,31 @@ class _EGCLFunction(torch.autograd.Function):
                 _lib.ptr(meta["box"]), _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1,
                 _lib.DEQUANT_NONE, None, None, 0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol), _lib.ptr(ldj),
                 _lib.ptr(err), None, _lib.ptr(tape), _lib.ptr(counts), prec, st), "enflow_lf_forward_f32 (EGCL tape)")
+        bwd_flags = net.variant_flags()
+        e = _lib.take_err(err)
+        if e == _lib.ERR_RANGE:
+            # the f16x3 tape lost its range (overflow, or an operand entirely below
+            # 2^-7): the tape again with fp32 GEMMs, and the fp32 backward on it
+            prec = (prec & ~0xff) | _lib.PREC_F32
+            bwd_flags |= _lib.BWD_F32
+            hw.copy_(h), pw.copy_(pos), gw.zero_(), vw.zero_(), counts.zero_()
+            _lib.FP32_RERUNS[0] += 1
+            if large:
+                _lib.check(L.enflow_lf_forward_large_f32(
+                    M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                    _lib.ptr(meta["box"]), _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1,
+                    _lib.DEQUANT_NONE, None, None, 0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol),
+                    _lib.ptr(ldj), _lib.ptr(err), prec, _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(lws), lws.numel(),
+                    st), "enflow_lf_forward_large_f32 (EGCL tape, fp32)")
+            else:
+                _lib.check(L.enflow_lf_forward_f32(
+                    M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
+                    _lib.ptr(meta["box"]), _lib.ptr(hw), _lib.ptr(gw), _lib.ptr(pw), _lib.ptr(vw), _lib.ptr(fwd), 1,
+                    _lib.DEQUANT_NONE, None, None, 0.0, 0.0, float(net.coords_weight), _lib.ptr(ldj_mol),
+                    _lib.ptr(ldj), _lib.ptr(err), None, _lib.ptr(tape), _lib.ptr(counts), prec, st),
+                    "enflow_lf_forward_f32 (EGCL tape, fp32)")
+            e = _lib.take_err(err)
+        _lib.raise_code(e)
         raw = torch.cat([net.kernel_raw(dev), net._att_raw(dev) if net.attention else torch.zeros(hid + 1, device=dev)])
         bwd = torch.empty(max(L.enflow_egcl_bwd_packed_size(hid, nf), 1), dtype=torch.float32, device=dev)
         _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw), hid, nf, _lib.ptr(bwd), st), "enflow_pack_egcl_bwd_f32")
@@ -335,14 +384,14 @@ class _EGCLFunction(torch.autograd.Function):
             _lib.check(L.enflow_egcl_backward_large_f32(
                 M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
                 _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(fwd), _lib.ptr(bwd), _lib.ptr(raw),
-                net.variant_flags(), float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af), _lib.ptr(ag),
+                bwd_flags, float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af), _lib.ptr(ag),
                 _lib.ptr(dh), _lib.ptr(dpos), _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err), st),
                 "enflow_egcl_backward_large_f32")
         else:
             _lib.check(L.enflow_egcl_backward_f32(
                 M, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(meta["r_cut"]),
                 _lib.ptr(meta["box"]), _lib.ptr(tape), _lib.ptr(counts), _lib.ptr(fwd), _lib.ptr(bwd),
-                _lib.ptr(raw), net.variant_flags(), float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af),
+                _lib.ptr(raw), bwd_flags, float(net.coords_weight), _lib.ptr(aq), _lib.ptr(af),
                 _lib.ptr(ag), _lib.ptr(dh), _lib.ptr(dpos), _lib.ptr(grad), _lib.ptr(ws), wsb, prb, _lib.ptr(err),
                 st), "enflow_egcl_backward_f32")
         _lib.raise_on_err(err)

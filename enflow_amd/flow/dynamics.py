@@ -276,21 +276,23 @@ class LFIntegrator(BaseFlow):
         ldj = torch.empty(1, dtype=torch.float32, device=dev)
         st = _lib.status_word(dev) if check_errors else torch.zeros(2, dtype=torch.int32, device=dev)
         prec = self._prec()
+        if check_errors:
+            _lib.check_pending()     # an older deferred error is not this launch's
         while True:
             self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
                                  s["max_n"], noise, ldj_mol, ldj, st[:1], src=s["src"], noise_key=key,
                                  ticket=st[1:], prec=prec)
             if not check_errors:
                 break
-            try:
-                _lib.raise_on_err(st[:1], reset=True)
-                break
-            except _lib.RangeError:
-                # an fp16 / bf16 operand overflowed: the same launch with fp32 GEMMs
-                # (same noise key, same inputs) returns the reference's result
-                if (prec & 0xff) == _lib.PREC_F32:
-                    raise
+            e = _lib.take_err(st[:1])
+            if _retry_fp32(e, prec):
+                # a split-precision operand left its range: the same launch with fp32
+                # GEMMs (same noise key, same inputs) returns the reference's result
                 prec = _fp32_prec(prec)
+                _lib.FP32_RERUNS[0] += 1
+                continue
+            _lib.raise_code(e)
+            break
         dt = data.h.dtype
         data.h, data.g = s["h"].to(dt), s["g"].to(dt)
         data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
@@ -309,19 +311,21 @@ class LFIntegrator(BaseFlow):
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         L = _lib.lib(nf)
         prec = self._prec()
+        if check_errors:
+            _lib.check_pending()
         while True:
             self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
                                  s["max_n"], idx, mx, err, src=s["src"], prec=prec)
             if not check_errors:
                 break
-            try:
-                _lib.raise_on_err(err, reset=True)
-                break
-            except _lib.RangeError:      # as in forward: re-run with fp32 GEMMs
-                if (prec & 0xff) == _lib.PREC_F32:
-                    raise
+            e = _lib.take_err(err)
+            if _retry_fp32(e, prec):     # as in forward: re-run with fp32 GEMMs
                 prec = _fp32_prec(prec)
                 mx.zero_()
+                _lib.FP32_RERUNS[0] += 1
+                continue
+            _lib.raise_code(e)
+            break
         dt = data.h.dtype
         if kind == _lib.DEQUANT_ARGMAX:
             width = int(mx.item()) + 1
@@ -334,6 +338,12 @@ class LFIntegrator(BaseFlow):
         data.g = s["g"].to(dt)
         data.pos, data.vel = s["pos"].to(data.pos.dtype), s["vel"].to(data.vel.dtype)
         return data
+
+
+def _retry_fp32(e, prec):
+    """The launch's own word says only ENFLOW_ERR_RANGE and the GEMMs were not
+    fp32 yet: re-run with fp32 GEMMs (any other bit is raised as is)."""
+    return e == _lib.ERR_RANGE and (prec & 0xff) != _lib.PREC_F32
 
 
 def _fp32_prec(prec):

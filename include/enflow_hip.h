@@ -37,8 +37,10 @@ extern "C" {
 #define ENFLOW_ERR_FEW_IMAGES       2  /* reference would IndexError (base.py:137) */
 #define ENFLOW_ERR_TOO_MANY_FEATURES 4
 #define ENFLOW_ERR_RANGE            8  /* f16x3 / bf16 GEMM path produced a non-finite output
-                                          (an operand past the fp16 / bf16 range): rerun
-                                          with ENFLOW_PREC_F32 */
+                                          (an operand past the fp16 / bf16 range), or (ABI 11,
+                                          f16x3) a GEMM operand of a molecule / row block was
+                                          entirely below 2^-7 in magnitude (its fp16 lo parts
+                                          subnormal): rerun with ENFLOW_PREC_F32 */
 
 /* Precision of the flow's two H x H edge GEMMs (edge_nn.2, coord_nn.0); all
  * other arithmetic is fp32 in every mode.  See DESIGN.md for the error model. */
@@ -57,7 +59,11 @@ extern "C" {
  * forward / reverse -- enflow_lf_forward_io_f32 (in-kernel dequantiser draws, in-launch
  * log|detJ| reduction), enflow_lf_reverse_io_f32; 9: ENFLOW_ERR_RANGE also flagged for a
  * non-finite phi / attention logit before tanh / clamp / sigmoid, the clamp passes NaN like
- * torch.clamp, latency instances of the fused flow kernel, enflow_set_latency_threshold). */
+ * torch.clamp, latency instances of the fused flow kernel, enflow_set_latency_threshold; 10: act_fn
+ * kinds (enflow_pack_egcl_act_f32, the ArgMax activation trailer), node_nf up to 16 in
+ * libenflow_hip_nf16.so; 11: ENFLOW_ERR_RANGE also flags an f16x3 GEMM operand that is entirely
+ * small, ENFLOW_BWD_F32 -- the fp32-GEMM backward for a tape recorded by an ENFLOW_PREC_F32
+ * forward). */
 int enflow_abi_version(void);
 
 /* Batches of <= 32-atom molecules with at most this many molecules run the
@@ -409,8 +415,13 @@ int enflow_alchemical_nll_backward_f32(int num_mols, int num_atoms, int max_mol_
  *   workspace         : >= enflow_lf_backward_workspace_size bytes
  *   dequant_kind      : ENFLOW_DEQUANT_*, OR-ed with ENFLOW_EGCL_VARIANTS when
  *                       any layer carries ENFLOW_EGCL_* flags (attention,
- *                       norm_diff, tanh: all differentiated)
+ *                       norm_diff, tanh: all differentiated), and with
+ *                       ENFLOW_BWD_F32 when the tape came from an
+ *                       ENFLOW_PREC_F32 forward (the fp32-GEMM backward: the
+ *                       f16x3 one recomputes the forward's activations in
+ *                       f16x3, which an ENFLOW_ERR_RANGE re-run must avoid)
  */
+#define ENFLOW_BWD_F32 0x200
 int enflow_lf_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
                            const int32_t* mol_ptr, const float* r_cut, const float* box,
                            const float* tape, const int32_t* pair_counts,
@@ -456,7 +467,8 @@ int enflow_lf_backward_large_f32(int num_mols, int num_atoms, int max_mol_atoms,
  * grad_layer (one layer in the layers_raw layout of enflow_lf_backward_f32).
  * tape / pair_counts: written by a one-layer enflow_lf_forward_f32 on the same
  * h / pos (dequant NONE, dt 0); layer / layer_bwd / layer_raw: that layer
- * packed; egcl_flags: its ENFLOW_EGCL_* flags.  Molecules of <= 64 atoms. */
+ * packed; egcl_flags: its ENFLOW_EGCL_* flags (| ENFLOW_BWD_F32: the tape is from an
+ * ENFLOW_PREC_F32 forward).  Molecules of <= 64 atoms. */
 int64_t enflow_egcl_backward_workspace_size(int num_mols, int num_atoms, int node_nf, int hidden_nf,
                                             int64_t pair_row_bound);
 int enflow_egcl_backward_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,

@@ -108,18 +108,25 @@ def _nll(h, g, pos, vel, ldj, mol_ptr, kBT, softening, partition_func):
 
 
 def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partition_func=10.0,
-                         coords_weight=1.0):
+                         coords_weight=1.0, dequant_kind="argmax"):
     """Loss of one training step and d loss / d parameter for every EGCL layer
     (list of dicts, EGCL_PARAM_NAMES) and the ArgMax dequantiser (dict).
+    dequant_kind "floor" (enflow/nn/floor.py:15-16): h + dequant_scale * eps with
+    eps the U[0, 1) draw, log|detJ| starts at 0; ``dequant`` is then the scale
+    and the dequantiser gradient dict is empty.
 
     Returns (loss, ldj, [layer grad dicts], dequant grad dict, output state)."""
     t = lambda a: torch.tensor(np.asarray(a, dtype=np.float64))  # noqa: E731
     P = [{k: t(v).requires_grad_(True) for k, v in p.items() if k not in ("flags", "act")} for p in layers]
-    D = {k: t(v).requires_grad_(True) for k, v in dequant.items() if k != "act"}
+    floor = dequant_kind == "floor"
+    D = {} if floor else {k: t(v).requires_grad_(True) for k, v in dequant.items() if k != "act"}
     mol_ptr = np.asarray(state["mol_ptr"], dtype=np.int64)
     n = int(mol_ptr[-1])
     box, r_cut = t(state["box"]), np.asarray(state["r_cut"], dtype=np.float64)
-    h, ldj = _argmax(D, t(state["h"]), t(eps), dequant.get("act"))
+    if floor:
+        h, ldj = t(state["h"]) + float(dequant) * t(eps), t(0.0)
+    else:
+        h, ldj = _argmax(D, t(state["h"]), t(eps), dequant.get("act"))
     g, pos, vel = t(state["g"]), t(state["pos"]), t(state["vel"])
     for p, lp in zip(P, layers):
         row, col, eb = O.batch_edges(pos.detach().numpy(), state["box"], r_cut, mol_ptr)

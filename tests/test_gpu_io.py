@@ -9,7 +9,9 @@ import torch
 
 from _fixtures import load, flow_from_fixture, rel_err, assert_all_within
 
-pytestmark = pytest.mark.gpu
+# every test on both fused-kernel instances (conftest.kernel_instance: the
+# 4-wave throughput build and the 8-wave latency build)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
 DEV = "cuda:0"
 
 

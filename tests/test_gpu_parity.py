@@ -12,7 +12,9 @@ from oracle import enflow_oracle as O
 from _fixtures import (load, layer_params, dequant_params, state, n_layers, rel_err, scalar_rel, worst_of, assert_all_within,
                        flow_from_fixture, data_from_fixture, egcl_from_fixture, EGCL_KEYS, ARGMAX_KEYS)
 
-pytestmark = pytest.mark.gpu
+# every test on both fused-kernel instances (conftest.kernel_instance: the
+# 4-wave throughput build and the 8-wave latency build)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
 TOL = 1e-5
 DEV = "cuda:0"
 
@@ -315,7 +317,7 @@ def test_molecule_past_fused_image_takes_large_path():
 # benchmark-size configuration: size-independent properties + sampled oracle
 # ---------------------------------------------------------------------------
 @pytest.fixture(scope="module")
-def bench_run():
+def bench_run(kernel_instance):
     from enflow_amd.data import Data
     from enflow_amd.data.synthetic import make_molecules, default_dt
     b = _f32(make_molecules(1024, 22, nf=5, seed=123))
@@ -378,6 +380,43 @@ def test_bench_config_reverse_vs_oracle(bench_run):
             worst[k] = worst_of([worst[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), ref[k])])
     print(f"bench config reverse, {len(SAMPLE)} molecules vs oracle:", fmt(worst))
     assert_all_within(worst, TOL)
+
+
+def test_bench_config_f32_gemms_sampled_vs_oracle(bench_run, kernel_instance):
+    """configs[1] shape with gemm_precision f32 (the exact fp32 MFMA chains) on
+    the instance under test: sampled molecules vs the oracle."""
+    b, model, d, noise, _, _ = bench_run
+    model.gemm_precision = "f32"
+    try:
+        with torch.no_grad():
+            o, _ = model(d.clone(), noise=noise)
+    finally:
+        model.gemm_precision = "f16x3"
+    worst = {k: 0.0 for k in ("h", "g", "pos", "vel")}
+    for m in SAMPLE[::4]:
+        sub, a0, a1 = _sub(b, m)
+        ref, _ = _oracle_flow(model, sub, noise[a0:a1])
+        for k in worst:
+            worst[k] = worst_of([worst[k], rel_err(getattr(o, k)[a0:a1].cpu().numpy(), ref[k])])
+    print(f"[{kernel_instance}] bench config f32 GEMMs, {len(SAMPLE[::4])} molecules vs oracle:", fmt(worst))
+    assert_all_within(worst, TOL)
+
+
+@pytest.mark.parametrize("mols", [6, 1024])
+def test_kernel_instance_selected(mols, kernel_instance):
+    """The latency threshold routes a <= 32-atom batch to the instance under
+    test (kernel names from the per-launch HIP-event timing)."""
+    from enflow_amd import _lib
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(mols, 22, nf=5, seed=5))
+    model = _make_model(32, 5, 2, 3, default_dt())
+    with _lib.KernelTimer() as t, torch.no_grad():
+        model(Data.from_arrays(b, device=DEV))
+    names = set(t.stats)
+    want = "lf_flow_kernel<fwd,lat>" if kernel_instance == "8-wave" else "lf_flow_kernel<fwd>"
+    print(f"[{kernel_instance}] {mols} molecules ran {sorted(names)}")
+    assert want in names, names
 
 
 BF16_L8_TOL = 1e-4     # bf16 generate at 8 layers (configs[2]), normwise per tensor; measured 2.6e-5 (r02a)

@@ -11,7 +11,9 @@ import torch
 from oracle import enflow_oracle as O
 from _fixtures import rel_err, normwise, worst_of, assert_all_within
 
-pytestmark = pytest.mark.gpu
+# every test on both fused-kernel instances (conftest.kernel_instance: the
+# 4-wave throughput build and the 8-wave latency build)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
 DEV = "cuda:0"
 
 

@@ -37,6 +37,7 @@ def _train_step(model, data, eps, kBT, softening):
     return loss, ldj
 
 
+@pytest.mark.usefixtures("kernel_instance")   # the training forward of <= 32-atom batches: both instances
 @pytest.mark.parametrize("name", ["train_h32_L3", "train_h128_L2", "train_h64_L2",
                                   "train_var_h64_L2", "train_var_h32_L3",    # var: EGCL(norm_diff, tanh)
                                   "train_att_h64_L2", "train_att_h32_L3"])   # att: + attention

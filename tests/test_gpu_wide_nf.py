@@ -17,7 +17,9 @@ from oracle import enflow_oracle as O
 from _fixtures import (load, flow_from_fixture, data_from_fixture, egcl_from_fixture, layer_params, state, n_layers,
                        rel_err, normwise, worst_of, assert_all_within)
 
-pytestmark = pytest.mark.gpu
+# every test on both fused-kernel instances (conftest.kernel_instance: the
+# 4-wave throughput build and the 8-wave latency build)
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
 TOL = 1e-5
 GRAD_TOL = 1e-4
 DEV = "cuda:0"

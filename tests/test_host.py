@@ -38,7 +38,7 @@ def test_node_feature_library_selection():
     assert _lib.lib_path(5) == _lib.lib_path(None) == _lib.LIB_PATH
     assert _lib.lib_path(8) == _lib.LIB_PATH and _lib.lib_path(9) == _lib.LIB_NF16_PATH
     L16 = _lib.lib(16)
-    assert L16.enflow_abi_version() == 10 and L16.enflow_max_node_nf() == 16
+    assert L16.enflow_abi_version() == 11 and L16.enflow_max_node_nf() == 16
     assert L16.enflow_egcl_packed_size(128, 16) > 0 and L16.enflow_egcl_packed_size(128, 17) == -1
     # training: 2 nf + 1 <= 32 edge inputs (one output tile of the transposed edge_nn.0 GEMM)
     assert L16.enflow_lf_backward_workspace_size(4, 88, 15, 128, 2, 4 * 480) > 0
@@ -49,7 +49,7 @@ def test_node_feature_library_selection():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 10
+    assert L.enflow_abi_version() == 11
     assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
@@ -268,3 +268,34 @@ def test_activation_codes_and_variant_flags():
     assert raw.numel() == sum(p.numel() for p in am.parameters()) + 4
     assert raw[-4:].tolist() == [3.0, 0.5, 0.0, 0.0]
     assert am.generic_act() and not ArgMax(5, 32).generic_act()
+
+
+def test_asm_hazard_scan_gate_on_synthetic_assembly(tmp_path):
+    """tools/asm_hazard_scan.py (the build gate of enflow_amd/build.py): an MFMA
+    result read inside an asm block too early, and an asm-written VGPR read as
+    an MFMA operand 1 state later, are flagged; the padded forms are not."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("asm_hazard_scan", os.path.join(ROOT, "tools", "asm_hazard_scan.py"))
+    scan = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(scan)
+
+    def hits(body):
+        p = tmp_path / "k.s"
+        p.write_text("_Z1kv:\n" + "\n".join("\t" + ln for ln in body) + "\n")
+        return [h[1] for h in scan.scan(str(p))]
+
+    mfma = "v_mfma_f32_32x32x16_f16 v[0:15], v[16:19], v[20:23], v[0:15]"
+    read = [";;#ASMSTART", "v_exp_f32 v30, v3", ";;#ASMEND"]
+    assert hits([mfma] + read) == ["mfma-result read in asm"]
+    assert hits([mfma, "s_nop 7", "s_nop 3"] + read) == []                   # 12 states
+    f32 = "v_mfma_f32_32x32x2_f32 v[0:15], v16, v17, v[0:15]"
+    assert hits([f32, "s_nop 7", "s_nop 3"] + read) == ["mfma-result read in asm"]   # 16-pass: 18 states
+    write = [";;#ASMSTART", "v_fma_mixlo_f16 v23, v40, 1.0, -v6 op_sel_hi:[0,0,1]", ";;#ASMEND"]
+    assert hits(write + ["v_add_f32 v50, v51, v52", mfma]) == ["asm write read by mfma"]
+    assert hits(write[:2] + ["s_nop 1", ";;#ASMEND", mfma]) == []
+
+
+def test_product_build_refuses_diagnostic_switches():
+    from enflow_amd import build
+    with pytest.raises(ValueError):
+        build.build(out=build.OUT, defines=("ENFLOW_STAMPS",))
