@@ -15,8 +15,9 @@ LIB_PATH = os.environ.get("ENFLOW_LIB") or os.path.join(_HERE, "libenflow_hip.so
 LIB_NF16_PATH = os.environ.get("ENFLOW_LIB_NF16") or os.path.join(_HERE, "libenflow_hip_nf16.so")
 BASE_NFMAX = 8
 MAX_NODE_NF = 16
-# the backward's transposed edge_nn.0 GEMM has one 32-row output tile: 2 nf + 1 <= 32
-TRAIN_MAX_NODE_NF = 15
+# training takes every node_nf of the libraries (nf 16: the radial row of the
+# backward's transposed edge_nn.0 GEMM, past its 32-row tile, is a separate dot)
+TRAIN_MAX_NODE_NF = 16
 
 ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2

@@ -197,7 +197,10 @@ __host__ __device__ inline int xin_width(int nf) { return (2 * nf + 1 + 15) & ~1
 constexpr int CSTR = NFMAX + 4;   // colc row: d h_j [NFMAX], d pos_j [3], pad
 // the transposed edge_nn.0 GEMM (d [h_i, h_j, radial]) has one 32-row output
 // tile: training needs 2 nf + 1 <= 32
-constexpr int BWD_NFMAX = NFMAX < 15 ? NFMAX : 15;
+// node_nf the backward takes: every feature of the build (nf 16: the radial
+// row of the transposed edge_nn.0 GEMM, q = 2 nf = 32, lies past its 32-row
+// output tile and is a separate dot product, see lf_layer_bwd_kernel GEMM5)
+constexpr int BWD_NFMAX = NFMAX;
 
 // <= 80 KB at (H, NMAX) = (128, 64): two workgroups per CU.  The node-MLP
 // adjoint rows go through LDS a chunk of Smem::NBCH atoms at a time, in the
@@ -210,6 +213,7 @@ struct BwdSmem {
   float apos[NMAX * 3], avel[NMAX * 3], aF[NMAX * 3];
   float aQ[NMAX];
   uint32_t nmax[NMAX / 32];   // per atom tile: max |d pre(node_nn.0)| (float bits)
+  float wrad[NFMAX == 16 ? H : 1];   // nf 16: edge_nn.0.weight[:, 2 nf] (the radial column)
 };
 
 // Adjoint tiles span many decades (coord_nn.2 starts at gain 0.001), so before
@@ -661,6 +665,9 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     sm.bias[H + k] = B.Lp[L.be2 + k];
     sm.bias[2 * H + k] = B.Lp[L.bc1 + k];
     sm.bias[3 * H + k] = B.Lp[L.wc2 + k];
+    if constexpr (NFMAX == 16) {
+      if (2 * nf + 1 > 32) sb.wrad[k] = Rp[R.We1 + k * (2 * nf + 1) + 2 * nf];
+    }
   }
   if constexpr (!BIG) build_pairs(sm, M, tid);   // same positions as the forward -> same pairs (reuses sm.u)
 
@@ -1024,8 +1031,9 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       STAMP(11);
       // GEMM5: d [h_i, h_j, radial] = edge_nn.0.weight^T d pre0   (rows q < 2nf+1)
       f32x16 ain = (f32x16)0.f;
+      float sc5 = 1.f;
       if constexpr (PREC == PREC_F16X3) {
-        const float sc5 = tile_pow2_scale(ax);   // ax already stored unscaled
+        sc5 = tile_pow2_scale(ax);   // ax already stored unscaled
 #pragma unroll
         for (int tp = 0; tp < NT; ++tp)
 #pragma unroll
@@ -1051,6 +1059,25 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       }
       STAMP(12);
       float arad = 0.f;
+      // nf 16: the radial row q = 2 nf = 32 is past the 32-row tile: a dot product
+      // of d pre0 (this lane half's features, scaled by 1 / sc5 in f16x3) with
+      // the radial column, the two halves summed, held by lane half 0
+      float arad16 = 0.f;
+      if constexpr (NFMAX == 16) {
+        if (2 * nf + 1 > 32) {
+          float s = 0.f;
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+              const f32x4 wr = ld4(sb.wrad + 32 * t + 8 * g4 + 4 * hh);
+#pragma unroll
+              for (int u = 0; u < 4; ++u) s = fmaf(ax[t][4 * g4 + u], wr[u], s);
+            }
+          s += __shfl_xor(s, 32, 64);
+          arad16 = hh == 0 ? s * sc5 : 0.f;
+        }
+      }
       if (valid) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -1061,6 +1088,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
             else atomicAdd(&wacc[jl * EW + q - nf], ain[r]);
           } else if (q == 2 * nf) arad = ain[r];
         }
+        if (NFMAX == 16 && 2 * nf + 1 > 32) arad = arad16;
       }
       // d coord_diff (radial = |cd|^2, trans = cd * phi), d pos_i += ., d pos_j -= .
       const float sF = hh == 0 ? c * phi : 0.f;
@@ -1455,7 +1483,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   // ds_write_b128 (float4 e4 = q * 256 + tid: column e4 / 8, rows 4 (e4 % 8) ..),
   // 4x fewer memory instructions than one dword per row; ra4 / xa4 the 4 rows'
   // factors, raj row j's (the recompute's lane row)
-  struct Stage { float rd[16], rx[16], ra, xa; bool pv; f32x4 ra4, xa4; float raj; const float* xb; };
+  struct Stage { float rd[16], rx[16], ra, xa; bool pv; f32x4 ra4, xa4; float raj; const float* xb; float rad; };
   Stage S0;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
   // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
@@ -1529,7 +1557,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         }
         if (hh && nf <= 7) G.rx[7] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
         G.rx[8] = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
-      } else {   // nf <= 15 (BWD_NFMAX): at most two k-slices
+      } else {   // features in two k-slices; nf 8 / 16: the radial in a slice of its own
         const int nch = gemm0_nch(nf);
 #pragma unroll
         for (int u = 0; u < 16; ++u) {
@@ -1537,10 +1565,12 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
           G.rx[u] = (pv && f < nf && u < 8 * nch) ? xblk[q * 32 + j] : 0.f;
         }
         const float rad = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
+        G.rad = 0.f;
         if (gemm0_radial_slot7(nf)) {
           if (hh) G.rx[8 * nch - 1] = rad;
         } else if (hh == 0) {
-          G.rx[8] = rad;   // nf == 8: the radial's own slice
+          if (nch == 1) G.rx[8] = rad;   // nf == 8: the radial's own (second) slice
+          else G.rad = rad;              // nf == 16: the third slice
         }
       }
     } else {
@@ -1645,14 +1675,15 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
             if (ks == 1 && hh == 0) in[0] = G.rx[8];
           } else {
 #pragma unroll
-            for (int u = 0; u < 8; ++u) in[u] = ks == 0 ? G.rx[u] : G.rx[8 + u];
+            for (int u = 0; u < 8; ++u) in[u] = ks == 0 ? G.rx[u] : (ks == 1 ? G.rx[8 + u] : 0.f);
+            if (ks == 2) in[0] = G.rad;   // nf 16's radial slice (0 on lane half 1)
           }
           f16x8 bh, bl;
           split_f16(in, 0, bh, bl);
           f32x4 ah = wfh, al = wfl;
-          if (ks == 1) {
-            ah = bload4(W, lane * 32, (L.we1x + (w * KS0MAX + 1) * 512) * 4);
-            al = bload4(W, lane * 32 + 16, (L.we1x + (w * KS0MAX + 1) * 512) * 4);
+          if (ks >= 1) {
+            ah = bload4(W, lane * 32, (L.we1x + (w * KS0MAX + ks) * 512) * 4);
+            al = bload4(W, lane * 32 + 16, (L.we1x + (w * KS0MAX + ks) * 512) * 4);
           }
           x = mfma_f16(ah, bh, x);
           x = mfma_f16(ah, bl, x);

@@ -425,6 +425,11 @@ if __name__ == "__main__":
         case_train(32, 2, [22, 9, 15], 64, "train_nf12_h32_L2", nf=12)
         case_train(128, 2, [22, 17], 65, "train_nf15_h128_L2", nf=15)
         sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "nf16_train":
+        # node_nf 16 training (2 nf + 1 = 33 edge_nn.0 inputs: the radial row past
+        # the transposed GEMM's 32-row tile)
+        case_train(64, 2, [22, 17], 66, "train_nf16_h64_L2", nf=16)
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "train":
         case_train(32, 3, [22, 9, 15, 3], 21, "train_h32_L3")
         case_train(128, 2, [22, 22], 22, "train_h128_L2")

@@ -4,7 +4,7 @@ dataset (enflow/main.py:148-151: EGCL(node_nf, node_nf, hidden_nf),
 ArgMax(node_nf, ...)), so any width is legal there.
 
 Goldens from the reference itself (tests/golden/make_golden.py wide_nf):
-flows at node_nf 12 / 16, an EGCL at 16, training steps at 12 / 15; the
+flows at node_nf 12 / 16, an EGCL at 16, training steps at 12 / 15 / 16; the
 large-system kernels (molecules past the fused image, and training past 64
 atoms) against the CPU oracles.  Tolerances as tests/test_gpu_parity.py /
 tests/test_gpu_train.py: outputs 1e-5 (max-abs relative per tensor),
@@ -87,8 +87,11 @@ def test_wide_egcl_matches_reference():
     assert_all_within(errs, TOL)
 
 
-@pytest.mark.parametrize("name", ["train_nf12_h32_L2", "train_nf15_h128_L2"])
+@pytest.mark.parametrize("name", ["train_nf12_h32_L2", "train_nf15_h128_L2", "train_nf16_h64_L2"])
 def test_wide_training_gradients_match_reference(name):
+    """node_nf 12 / 15 / 16 training steps vs the reference's loss.backward()
+    (nf 16: 2 nf + 1 = 33 edge_nn.0 inputs; the backward's radial row lies past
+    the transposed GEMM's 32-row tile and is its own dot product)."""
     from enflow_amd.flow import Alchemical_NLL
     inp, ref = load(name)
     model, data = flow_from_fixture(inp, DEV)
@@ -108,15 +111,30 @@ def test_wide_training_gradients_match_reference(name):
     assert_all_within(errs, GRAD_TOL)
 
 
-def test_node_nf_16_training_is_refused_inference_runs():
-    """The transposed edge_nn.0 GEMM of the backward has one 32-row output tile
-    (2 node_nf + 1 <= 32): node_nf 16 trains nowhere, and says so."""
-    from enflow_amd.flow import Alchemical_NLL
-    inp, _ = load("lf_nf16_h32_L2")
-    model, data = flow_from_fixture(inp, DEV)
-    with pytest.raises(NotImplementedError):
-        out, ldj = model(data, noise=torch.tensor(inp["eps"], device=DEV))
-        Alchemical_NLL(kBT=float(inp["kBT"]), softening=float(inp["softening"]))(out, ldj).backward()
+def test_node_nf_16_standalone_egcl_backward_vs_oracle():
+    """EGCL(16, 16, 128) alone with autograd (the one-layer tape and backward of
+    the 16-feature library) vs the float64 gradient oracle's EGCL."""
+    import torch
+    from oracle import enflow_oracle_grad as OG
+    inp, _ = load("egcl_nf16_h128")
+    nf, hid = 16, 128
+    net = egcl_from_fixture(inp, 0, nf, hid).to(DEV)
+    d = data_from_fixture(inp, DEV)
+    h = d.h.clone().requires_grad_(True)
+    q, f, g = net(h, d.edges)
+    (q.sum() + (f * f).sum() + (g * g).sum()).backward()
+    p = {k: v.detach().double().cpu().requires_grad_(True) for k, v in net.named_parameters()}
+    ht = torch.tensor(inp["h"], dtype=torch.float64, requires_grad=True)
+    row, col, eb = O.batch_edges(inp["pos"].astype(np.float64), inp["box"].astype(np.float64),
+                                 inp["r_cut"].astype(np.float64), inp["mol_ptr"])
+    pos = torch.tensor(inp["pos"], dtype=torch.float64)
+    qq, ff, gg = OG._egcl(p, ht, pos, torch.as_tensor(row), torch.as_tensor(col), torch.tensor(eb),
+                          int(inp["mol_ptr"][-1]), 1.0)
+    (qq.sum() + (ff * ff).sum() + (gg * gg).sum()).backward()
+    errs = {k: normwise(v.grad.cpu().numpy(), p[k].grad.numpy()) for k, v in net.named_parameters()}
+    errs["h"] = normwise(h.grad.cpu().numpy(), ht.grad.numpy())
+    print("egcl nf16 backward vs gradient oracle:", f"{worst_of(errs):.2e}")
+    assert_all_within(errs, GRAD_TOL)
 
 
 def _chains(sizes, seed, nf):

@@ -40,9 +40,12 @@ def test_node_feature_library_selection():
     L16 = _lib.lib(16)
     assert L16.enflow_abi_version() == 11 and L16.enflow_max_node_nf() == 16
     assert L16.enflow_egcl_packed_size(128, 16) > 0 and L16.enflow_egcl_packed_size(128, 17) == -1
-    # training: 2 nf + 1 <= 32 edge inputs (one output tile of the transposed edge_nn.0 GEMM)
+    # training: every node_nf of the build (nf 16's radial row past the transposed
+    # edge_nn.0 GEMM's 32-row tile is a dot product of its own), not past it
     assert L16.enflow_lf_backward_workspace_size(4, 88, 15, 128, 2, 4 * 480) > 0
-    assert L16.enflow_lf_backward_workspace_size(4, 88, 16, 128, 2, 4 * 480) == -1
+    assert L16.enflow_lf_backward_workspace_size(4, 88, 16, 128, 2, 4 * 480) > 0
+    assert L16.enflow_lf_backward_workspace_size(4, 88, 17, 128, 2, 4 * 480) == -1
+    assert _lib.TRAIN_MAX_NODE_NF == 16
     with pytest.raises(NotImplementedError):
         _lib.lib_path(17)
 

@@ -87,7 +87,7 @@ def test_multiplicity_roundtrip():
 
 
 TRAIN_CASES = ["train_h32_L3", "train_h128_L2", "train_h64_L2", "train_var_h64_L2", "train_var_h32_L3",
-               "train_att_h64_L2", "train_att_h32_L3", "train_nf12_h32_L2", "train_nf15_h128_L2",
+               "train_att_h64_L2", "train_att_h32_L3", "train_nf12_h32_L2", "train_nf15_h128_L2", "train_nf16_h64_L2",
                "train_act_tanh_h32_L2", "train_act_elu_h64_L2"]
 
 

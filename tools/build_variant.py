@@ -24,8 +24,11 @@ def main():
     obj = os.path.join(out_dir, f"{tu.split('.')[0]}_{name}.o")
     base = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include")]
     subprocess.run(base + flags + ["-c", os.path.join(ROOT, "enflow_amd", "csrc", tu), "-o", obj], check=True)
-    others = [LIB + "." + s + ".o" for s in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip",
-                                            "enflow_timing.hip", "enflow_latency.hip") if s != tu]
+    sys.path.insert(0, ROOT)
+    from enflow_amd.build import obj_dir
+    odir = obj_dir(LIB)   # the product build's objects (enflow_amd/build/libenflow_hip_so)
+    others = [os.path.join(odir, s + ".o") for s in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip",
+                                                     "enflow_timing.hip", "enflow_latency.hip") if s != tu]
     so = os.path.join(out_dir, f"libenflow_{name}.so")
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, obj] + others, check=True)
     print(so)
