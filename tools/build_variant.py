@@ -1,7 +1,7 @@
 """Build an A/B variant of libenflow_hip.so: enflow_flow.hip recompiled with
 extra -D defines / hipcc flags, linked with the product build's other objects.
 
-    python tools/build_variant.py NAME [--tu backward] [-DFOO=1 | -fflag ...]   ->  enflow_amd/var/libenflow_NAME.so
+    python tools/build_variant.py NAME [--tu backward] [-DFOO=1 | -fflag ...]   ->  ab_libs/libenflow_NAME.so
 
 --tu NAME recompiles enflow_NAME.hip instead (backward: the training kernels, latency: the
 8-wave flow instances).
@@ -19,7 +19,7 @@ def main():
     tu = "enflow_flow.hip"
     if flags[:1] == ["--tu"]:
         tu, flags = f"enflow_{flags[1]}.hip", flags[2:]
-    out_dir = os.path.join(ROOT, "enflow_amd", "var")
+    out_dir = os.path.join(ROOT, "ab_libs")   # shipped to the GPU box (enflow_amd/var is gpurun-ignored)
     os.makedirs(out_dir, exist_ok=True)
     obj = os.path.join(out_dir, f"{tu.split('.')[0]}_{name}.o")
     base = ["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(ROOT, "include")]
