@@ -165,6 +165,8 @@ struct BwdArgs {
   float* aphi;       // [P]    d phi                                 (DY of coord_nn.2)
   float* patt;       // [P]    att of the pair (VAR; 1 without attention): X of coord_nn.0 is e * att
   float* dlogit;     // [P]    d att_nn logit (VAR; 0 without attention) (DY of att_nn.0)
+  float* tmax;       // [P / 32][TMX_W] per 32-row tile: max |operand| of the pair-row weight-gradient
+                     // products (TMX_*), the scales outer_x3_kernel puts on a whole chunk
   float* su;         // atom rows [A][H] silu(vel_scaling_nn.0)      (X of vel_scaling_nn.2)
   float* au;         // [A][H] d pre(vel_scaling_nn.0)               (DY of vel_scaling_nn.0)
   float* sn;         // [A][H] silu(node_nn.0)                       (X of node_nn.2)
@@ -192,6 +194,8 @@ struct BwdArgs {
   float* colc;                // [pair rows][CSTR] out
   long long prb;              // pair rows allocated
 };
+// per-tile operand maxima (BwdArgs::tmax): X / DY of edge_nn.0, edge_nn.2, coord_nn.0
+enum { TMX_XIN = 0, TMX_DP0 = 1, TMX_X1 = 2, TMX_DPE = 3, TMX_MSG = 4, TMX_DPC = 5, TMX_W = 8 };
 // edge_nn.0 input rows [h_i, h_j, radial]: 2 nf + 1 columns rounded up to 16
 __host__ __device__ inline int xin_width(int nf) { return (2 * nf + 1 + 15) & ~15; }
 constexpr int CSTR = NFMAX + 4;   // colc row: d h_j [NFMAX], d pos_j [3], pad
@@ -221,13 +225,17 @@ struct BwdSmem {
 // tile's max |x| in [2^12, 2^13): hi / lo parts stay normal fp16.  Returns the
 // exact inverse scale.
 template <int NT>
-__device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
+__device__ __forceinline__ float lane_absmax(const f32x16 (&X)[NT]) {
   float m = 0.f;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(X[t][r]));
-  m = wave_max(m);
+  return m;
+}
+// m: the wave's max |x| over X (wave-uniform)
+template <int NT>
+__device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT], float m) {
   int ex = 0;
   if (m > 0.f && isfinite(m)) {
     frexpf(m, &ex);
@@ -238,6 +246,10 @@ __device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) X[t] *= s;
   return ldexpf(1.f, -ex);
+}
+template <int NT>
+__device__ __forceinline__ float tile_pow2_scale(f32x16 (&X)[NT]) {
+  return tile_pow2_scale(X, wave_max(lane_absmax(X)));
 }
 
 
@@ -748,6 +760,14 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       }
       const int gt = (pp0 >> 5) + tile;   // tile index within the molecule's / block's rows
       const size_t Rw = prow0 + (size_t)(pp0 + p);
+      // the tile's max |operand| of each weight-gradient product (outer_x3_kernel's
+      // chunk scales): wave-reduced, lane 0 stores
+      float* const tmx = B.tmax + ((prow0 >> 5) + (size_t)gt) * TMX_W;
+      auto put_max = [&](int op, float m) {
+        m = wave_max(m);
+        if (lane == 0) tmx[op] = m;
+        return m;
+      };
       const int tsb = gt * H * 128;   // tile byte offset in an H-wide array (16-wide: / (H / 16))
       float cx, cy, cz;   // column atom position
       if constexpr (BIG) {
@@ -769,12 +789,15 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       const float radial = dx * dx + dy * dy + dz * dz;
 
       // X row of edge_nn.0: [h_i, h_j, radial]
+      float mxin = valid ? radial : 0.f;
       auto xin_col = [&](int q) -> float {
         float v = 0.f;
         if (q < nf) v = sm.h[i * NFP + q];
         else if (q < 2 * nf) v = colh(q - nf);
         else if (q == 2 * nf) v = radial;
-        return valid ? v : 0.f;
+        v = valid ? v : 0.f;
+        mxin = fmaxf(mxin, fabsf(v));
+        return v;
       };
       if constexpr (NFMAX == 8) {
 #pragma unroll
@@ -787,6 +810,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
           for (int u = 0; u < 8; ++u)
             ST_OUT(rxin, (hh * 256 + j) * 4, gt * XW * 128 + (16 * c16 + u) * 128, xin_col(16 * c16 + 8 * hh + u));
       }
+      put_max(TMX_XIN, mxin);
 
       // GEMM0 (recompute): pre0 = edge_nn.0 [h_i, h_j, radial] + be1.  Run twice per
       // tile (here, and again for silu'(pre0) after GEMM4) instead of parking pre0
@@ -868,6 +892,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = act_v<VAR>(act, x0[t][4 * g4 + u] + b[u]);
         }
+      put_max(TMX_X1, lane_absmax(x0));
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(5);
       // GEMM1 (recompute): e = silu(edge_nn.2 x1 + be2); pre_e stored
@@ -903,6 +928,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) ev[t] *= att;
       }
+      put_max(TMX_MSG, lane_absmax(ev));
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(6);
       // GEMM2 (recompute): phi = coord_nn.2 silu(coord_nn.0 e + bc1)
@@ -912,6 +938,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       chain_prec_fill<PREC, NT, 1>(W, L.wc1f, L.wc1x, L.wc1b, ev, cv, lane, nofill);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pre_e rows landed
       float part = 0.f;
+      float mdz = 0.f;   // max |silu'(c)| (DY of coord_nn.0 = d phi * silu'(c))
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -922,14 +949,17 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const float z = fmaf(cv[t][4 * g4 + u], inv2, b[u]);
+            float dz;
             if (!VAR || act.k == ACT_SILU) {
               const float s = sigmoid_f(z);
               part = fmaf(w2[u], z * s, part);   // pc is not stored: outer_x3_kernel recomputes it
-              cv[t][4 * g4 + u] = w2[u] * s * (1.f + z * (1.f - s));   // wc2 * silu'(c)
+              dz = s * (1.f + z * (1.f - s));    // silu'(c)
             } else {
               part = fmaf(w2[u], act_f(act, z), part);
-              cv[t][4 * g4 + u] = w2[u] * act_d(act, z);
+              dz = act_d(act, z);
             }
+            mdz = fmaxf(mdz, fabsf(dz));
+            cv[t][4 * g4 + u] = w2[u] * dz;      // wc2 * silu'(c)
           }
         }
       float phi = part + __shfl_xor(part, 32, 64);
@@ -947,6 +977,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       if (v_tanh) aph *= 1.f - phi * phi;                       // d of coord_nn.2's output
       if (hh == 0 && !(ENFLOW_BWD_ABLATE & 1)) B.aphi[Rw] = aph;
       if (VAR && hh == 0) B.patt[Rw] = att;
+      put_max(TMX_DPC, mdz * fabsf(aph));
       // d pre(coord_nn.0) = dphi * wc2 * silu'(c)   (not stored: outer_acc rebuilds it from pc)
 #pragma unroll
       for (int t = 0; t < NT; ++t) cv[t] *= aph;
@@ -1010,7 +1041,8 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) ax[t] = (f32x16)0.f;
       float sc4 = 1.f;
-      if constexpr (PREC == PREC_F16X3) sc4 = tile_pow2_scale(ae);   // ae already stored unscaled
+      const float mdpe = put_max(TMX_DPE, lane_absmax(ae));
+      if constexpr (PREC == PREC_F16X3) sc4 = tile_pow2_scale(ae, mdpe);   // ae already stored unscaled
       chain_prec_fill<PREC, NT, 1>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, nofill);
       STAMP(10);
       gemm0(rl);   // pre0 again (bitwise the first pass's)
@@ -1032,8 +1064,9 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       // GEMM5: d [h_i, h_j, radial] = edge_nn.0.weight^T d pre0   (rows q < 2nf+1)
       f32x16 ain = (f32x16)0.f;
       float sc5 = 1.f;
+      const float mdp0 = put_max(TMX_DP0, lane_absmax(ax));
       if constexpr (PREC == PREC_F16X3) {
-        sc5 = tile_pow2_scale(ax);   // ax already stored unscaled
+        sc5 = tile_pow2_scale(ax, mdp0);   // ax already stored unscaled
 #pragma unroll
         for (int tp = 0; tp < NT; ++tp)
 #pragma unroll
@@ -1225,6 +1258,8 @@ struct OuterDesc {
   int nf;                    // RECOMP_X0: node features (xin row layout)
   const float* actp;         // the layer's act_fn (kind, p0, p1; packed layer + vfl + 1), NULL: SiLU
   int f32r;                  // RECOMP_*: recompute on the fp32 MFMA (the ENFLOW_BWD_F32 backward)
+  const float* tmaxA;        // outer_x3_kernel: the producer's per-tile max |DY| / max |X| (BwdArgs::tmax
+  const float* tmaxB;        //   + TMX_*, stride TMX_W)
 };
 // RECOMP_X0: X = silu(pre0), pre0 = edge_nn.0 . xin + be1 (the X source is xin, width ldx);
 // RECOMP_PC: DY = rowv * silu'(pc), pc = coord_nn.0 . X + bc1 (X read; no DY source), and
@@ -1416,10 +1451,14 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
 // F16X3 form of outer_acc_kernel for the tile-blocked pair rows (M > 1): the
 // stage's DY / X tiles go to LDS column-major ([column][row], rows contiguous),
 // so an MFMA operand (8 consecutive rows of one column) is one ds_read_b128
-// pair.  Per stage and wave each operand block gets a power-of-two scale
-// (max |x| -> [2^12, 2^13), as the layer backward's adjoint tiles) before the
-// hi / lo split; the stage's three-product sums land in a scratch accumulator
-// that is added to the running one with the exact inverse scale.
+// pair.  Each operand gets one power-of-two scale per chunk (max |x| of the
+// chunk -> [2^12, 2^13), as the layer backward's adjoint tiles) before the
+// hi / lo split: the chunk maximum is the max over the per-tile maxima the
+// layer backward stored (BwdArgs::tmax), so no stage computes a maximum, the
+// three products accumulate straight into acc, and the exact inverse scales
+// are applied once to the finished sums.  (Per element the split keeps ~22
+// bits relative to the chunk maximum; rows far below it lose low bits that
+// the sum could not hold anyway.)
 //
 // Recomputed operands (OuterDesc::recomp) trade HBM bytes for MFMAs: the layer
 // backward stores neither pre(edge_nn.0) nor pre(coord_nn.0) (2 x H floats per
@@ -1795,33 +1834,32 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   };
   const bool use_m1 = mh * 64 + 32 < M, use_n0 = n0 + nh * 64 < N, use_n1 = n0 + nh * 64 + 32 < N;
   const bool live = mh * 64 < M && use_n0;
+  // the chunk's scales (one per operand, from the producer's per-tile maxima):
+  // max |x| of the chunk -> [2^12, 2^13) before the hi / lo split, so the three
+  // products accumulate straight into acc and are un-scaled once at the end
+  static_assert(OA_CHUNK <= 64 * 32, "a chunk's tile maxima fit one wave");
+  int ea = 0, eb = 0;
+  {
+    const int t0 = r0 >> 5, ntl = (r1 - r0 + 31) >> 5;
+    const float ma = lane < ntl ? D.tmaxA[(size_t)(t0 + lane) * TMX_W] : 0.f;
+    const float mb = lane < ntl ? D.tmaxB[(size_t)(t0 + lane) * TMX_W] : 0.f;
+    ea = pow2_exp(wave_max(ma));
+    eb = pow2_exp(wave_max(mb));
+  }
+  const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb);
   auto compute = [&](int buf) {
     if (live) {
       // operands of both k-steps: A[a][ks] (DY columns), B[b][ks] (X columns)
       f32x4 av[2][2][2], bv[2][2][2];   // [tile][ks][half]
-      float ma = 0.f, mb = 0.f;
 #pragma unroll
       for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
           for (int h2 = 0; h2 < 2; ++h2) {
-            const float* pa = &sd[buf][mh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2];
-            const float* pb = &sx[buf][nh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2];
-            av[a][ks][h2] = *reinterpret_cast<const f32x4*>(pa);
-            bv[a][ks][h2] = *reinterpret_cast<const f32x4*>(pb);
-            // the scales see only the tiles that are multiplied: a recomputed stage
-            // writes rows < H only, the rest of the LDS image is stale
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              if (a == 0 || use_m1) ma = fmaxf(ma, fabsf(av[a][ks][h2][u]));
-              if (a == 0 || use_n1) mb = fmaxf(mb, fabsf(bv[a][ks][h2][u]));
-            }
+            av[a][ks][h2] = *reinterpret_cast<const f32x4*>(&sd[buf][mh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2]);
+            bv[a][ks][h2] = *reinterpret_cast<const f32x4*>(&sx[buf][nh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2]);
           }
-      ma = wave_max(ma);
-      mb = wave_max(mb);
-      const int ea = pow2_exp(ma), eb = pow2_exp(mb);
-      const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb), un = ldexpf(1.f, -(ea + eb));
       f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
       // scaled hi / lo split: hi = f16(x s) by v_cvt_pk_f16_f32, lo = f16(x s - hi) by
       // v_fma_mix (split_f16; x s - hi is exact in fp32, so bitwise the plain form)
@@ -1843,14 +1881,12 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           if ((a == 1 && !use_m1) || (b == 1 && !use_n1)) continue;
-          f32x16 t = (f32x16)0.f;
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
-            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bh[b][ks], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bl[b][ks], t, 0, 0, 0);
-            t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a][ks], bh[b][ks], t, 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bh[b][ks], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bl[b][ks], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a][ks], bh[b][ks], acc[a][b], 0, 0, 0);
           }
-          acc[a][b] += t * un;
         }
     }
     if (do_bias) {
@@ -1877,6 +1913,7 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
     }
   }
   float* out = D.part + (size_t)chunk * M * NB;
+  const float ua = ldexpf(1.f, -ea), ub = ldexpf(1.f, -eb);   // exact inverse scales
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1884,7 +1921,8 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int mm = mh * 64 + a * 32 + rho(r, hh), nn = n0 + nh * 64 + b * 32 + j;
-        if (mm < M && nn < N) out[(size_t)mm * NB + nn] = xf_dy ? acc[a][b][r] * D.colv[mm] : acc[a][b][r];
+        const float v = acc[a][b][r] * ua * ub;
+        if (mm < M && nn < N) out[(size_t)mm * NB + nn] = xf_dy ? v * D.colv[mm] : v;
       }
   if (do_bias) out[(size_t)tid * NB + N] = xf_dy ? bsum * D.colv[tid] : bsum;
   if (fold && rcm == RECOMP_PC) {   // fixed-order sum over the 32 rows of each half-wave
@@ -2280,7 +2318,7 @@ static_assert(BWD_NBUF >= 2, "at least double buffered");
 struct BwdWs {
   size_t offs, buf0, span;   // shared offsets section; first buffer; buffer stride
   // offsets within a buffer (floats)
-  size_t xin, p0, pe, pc, dp0, dpe, aphi, patt, dlogit, su, au, sn, an, aq, agr, anet, part, total;
+  size_t xin, p0, pe, pc, dp0, dpe, aphi, patt, dlogit, tmax, su, au, sn, an, aq, agr, anet, part, total;
   int nbuf;                  // buffers rotated by the layer chain (BWD_NBUF or 2)
   size_t part_floats;
 };
@@ -2299,6 +2337,7 @@ static BwdWs bwd_ws(int num_mols, int num_atoms, int nf, int H, int n_layers, lo
   W.aphi = o; o += al64(P);
   W.patt = o; o += al64(P);
   W.dlogit = o; o += al64(P);
+  W.tmax = o; o += al64((P / 32 + 1) * TMX_W);
   W.su = o; o += al64(A * H);
   W.au = o; o += al64(A * H);
   W.sn = o; o += al64(A * H);
@@ -2395,6 +2434,7 @@ static void add_desc(OuterBatch& ob, int& wg, const float* DY, int ldd, int M, c
   D.nf = 0;
   D.actp = nullptr;
   D.f32r = 0;
+  D.tmaxA = D.tmaxB = nullptr;
   D.chunk = tiled ? OA_CHUNK : OA_CHUNK_ATOM;
   D.DY = DY; D.ldd = ldd; D.M = M; D.X = X; D.ldx = ldx; D.N = N;
   D.rows_dev = rows_dev; D.rows_static = rows_static;
@@ -2493,6 +2533,8 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     const int XW = xin_width(nf);
     add_desc(ob, wg, wb + Wl.dp0, H, H, wb + Wl.xin, XW, 2 * nf + 1, prow, 0, prb, part, G + R.We1, G + R.be1,
              PAIR_OUTER);
+    ob.d[ob.nd - 1].tmaxA = wb + Wl.tmax + TMX_DP0;
+    ob.d[ob.nd - 1].tmaxB = wb + Wl.tmax + TMX_XIN;
     // edge_nn.2: X = silu(pre0), pre0 recomputed from the xin rows
     // the layer's act_fn (variant layers; packed layer + vfl + 1): the recomputed
     // activations and their derivatives follow it (NULL: SiLU instances)
@@ -2500,6 +2542,8 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     const float* actp = (variants || f32b) ? Lp + egcl_layout(H, nf).vfl + 1 : nullptr;
     add_desc(ob, wg, wb + Wl.dpe, H, H, wb + Wl.xin, XW, H, prow, 0, prb, part, G + R.We2, G + R.be2, PAIR_OUTER);
     ob.d[ob.nd - 1].recomp = RECOMP_X0;
+    ob.d[ob.nd - 1].tmaxA = wb + Wl.tmax + TMX_DPE;
+    ob.d[ob.nd - 1].tmaxB = wb + Wl.tmax + TMX_X1;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
     ob.d[ob.nd - 1].actp = actp;
@@ -2513,6 +2557,8 @@ static int layer_weight_grads(hipStream_t st2, const BwdWs& Wl, float* wb, const
     if (variants) ob.d[ob.nd - 1].xrow = wb + Wl.patt;          // the message is e * att
     ob.d[ob.nd - 1].colv = Rp + R.wc2;
     ob.d[ob.nd - 1].recomp = RECOMP_PC;
+    ob.d[ob.nd - 1].tmaxA = wb + Wl.tmax + TMX_DPC;
+    ob.d[ob.nd - 1].tmaxB = wb + Wl.tmax + TMX_MSG;
     ob.d[ob.nd - 1].Lp = Lp;
     ob.d[ob.nd - 1].nf = nf;
     ob.d[ob.nd - 1].actp = actp;
@@ -2703,7 +2749,7 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     A.pair_off = offs + (size_t)l * (num_mols + 1);
     A.xin = wb + Wl.xin; A.p0 = nullptr; A.pe = wb + Wl.pe; A.pc = nullptr;
     A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
-    A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
+    A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit; A.tmax = wb + Wl.tmax;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
     A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
     A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
@@ -2874,7 +2920,7 @@ static int lf_backward_large_impl(int num_mols, int num_atoms, int max_mol_atoms
     A.ah = adj_h; A.ag = adj_g; A.apos = adj_pos; A.avel = adj_vel;
     A.xin = wb + Wl.xin; A.p0 = nullptr; A.pe = wb + Wl.pe; A.pc = nullptr;
     A.dp0 = wb + Wl.dp0; A.dpe = wb + Wl.dpe; A.aphi = wb + Wl.aphi;
-    A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit;
+    A.patt = wb + Wl.patt; A.dlogit = wb + Wl.dlogit; A.tmax = wb + Wl.tmax;
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
     A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
     A.blk_start = G.blk_start; A.rbl = G.rbl; A.max_n = max_mol_atoms;
