@@ -2,7 +2,8 @@
 # Round-end evidence for one library build (run on the GPU box via gpurun):
 # GPU tests, smoke, every bench mode, rocprofv3 kernel stats of the forward and
 # training benches, PMC traffic of the flow kernel, then the forward bench again
-# so its line carries the traffic of this exact build.
+# so its line carries the traffic of this exact build; the strong-scaling probe
+# and PMC of the training kernels.
 # Usage: bash tools/gpu_final.sh <tag>
 set -euo pipefail
 TAG=${1:-r02f}
@@ -28,4 +29,6 @@ timeout -k 10 900 python -u profiles/collect_pmc.py "$TAG" > "$OUT/pmc.log" 2>&1
 mkdir -p profiles/_box && cp "gpurun_out/${TAG}_pmc_traffic.json" profiles/_box/
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/bench_forward_traffic.json" 2> "$OUT/forward_traffic.err"
 rm -rf profiles/_box
+timeout -k 10 300 python -u tools/strong_scaling_probe.py > "$OUT/strong_probe.json" 2> "$OUT/strong.err"
+timeout -k 10 900 python -u profiles/collect_pmc.py "${TAG}_train" train lf_layer_bwd_kernel,outer_x3_kernel > "$OUT/pmc_train.log" 2>&1
 echo done
