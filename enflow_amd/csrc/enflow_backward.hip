@@ -195,12 +195,10 @@ struct BwdArgs {
   long long prb;              // pair rows allocated
 };
 // weight-fragment ring depth of the layer backward's F16X3 chains (prefetch distance
-// + 1 k-steps; each slot is 8 VGPRs of hi / lo fragments)
+// + 1 k-steps; each slot is 8 VGPRs of hi / lo fragments).  Depth 3 / 4 / 6 measured
+// within 1 % of 2 (profiles/r04/r04l_ab_train_split_once_and_ring_depth.txt)
 #ifndef ENFLOW_BWD_X3_DEPTH
 #define ENFLOW_BWD_X3_DEPTH 2
-#endif
-#ifndef ENFLOW_BWD_ACT_FILL
-#define ENFLOW_BWD_ACT_FILL 1   // activations of GEMM1 / GEMM2's operands as chain fillers (A/B knob)
 #endif
 // per-tile operand maxima (BwdArgs::tmax): X / DY of edge_nn.0, edge_nn.2, coord_nn.0
 enum { TMX_XIN = 0, TMX_DP0 = 1, TMX_X1 = 2, TMX_DPE = 3, TMX_MSG = 4, TMX_DPC = 5, TMX_W = 8 };
@@ -890,54 +888,37 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       f32x16 x0[NT];
       gemm0(x0);
       STAMP(4);
-      // x1 = silu(pre0) (kept: B operand of GEMM1).  ENFLOW_BWD_ACT_FILL (the SiLU
-      // instance): tile 0 here, tiles 1.. as fillers of GEMM1's steps on the tile
-      // before (the forward's fill1), and likewise pre_e -> store -> e for GEMM2,
-      // so the activations' VALU runs in the MFMA shadow of the next chain
-      constexpr bool actfill = ENFLOW_BWD_ACT_FILL && PREC == PREC_F16X3 && !VAR;
-      float mx1 = 0.f, mmsg = 0.f;
-      auto act_x1 = [&](int t, int g4) {
-        const int f0 = 32 * t + 8 * g4 + 4 * hh;
-        const f32x4 b = ld4(sm.bias + f0);
+      // x1 = silu(pre0) (kept: B operand of GEMM1)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float v = act_v<VAR>(act, x0[t][4 * g4 + u] + b[u]);
-          x0[t][4 * g4 + u] = v;
-          mx1 = fmaxf(mx1, fabsf(v));
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(sm.bias + f0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) x0[t][4 * g4 + u] = act_v<VAR>(act, x0[t][4 * g4 + u] + b[u]);
         }
-      };
-#pragma unroll
-      for (int t = 0; t < (actfill ? 1 : NT); ++t)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) act_x1(t, g4);
+      put_max(TMX_X1, lane_absmax(x0));
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(5);
       // GEMM1 (recompute): e = silu(edge_nn.2 x1 + be2); pre_e stored
       f32x16 ev[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) ev[t] = (f32x16)0.f;
-      auto fill1 = [&](int step) {
-        if constexpr (actfill) {
-          const int t = (step >> 2) + 1, g4 = step & 3;
-          if (t < NT) act_x1(t, g4);
+      chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(W, L.we2f, L.we2x, L.we2b, x0, ev, lane, nofill);
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int f0 = 32 * t + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(sm.bias + H + f0);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const float z = fmaf(ev[t][4 * g4 + u], inv1, b[u]);
+            ST_PARK(rpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
+            ev[t][4 * g4 + u] = act_v<VAR>(act, z);
+          }
         }
-      };
-      chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(W, L.we2f, L.we2x, L.we2b, x0, ev, lane, fill1);
-      put_max(TMX_X1, mx1);
-      auto act_e = [&](int t, int g4) {   // pre_e parked, e = act(pre_e)
-        const int f0 = 32 * t + 8 * g4 + 4 * hh;
-        const f32x4 b = ld4(sm.bias + H + f0);
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float z = fmaf(ev[t][4 * g4 + u], inv1, b[u]);
-          ST_PARK(rpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7), z);
-          ev[t][4 * g4 + u] = act_v<VAR>(act, z);
-        }
-      };
-#pragma unroll
-      for (int t = 0; t < (actfill ? 1 : NT); ++t)
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) act_e(t, g4);
       float att = 1.f;
       if (v_att) {   // egcl.py:60-62: message = e * sigmoid(att_nn(e))
         float d = 0.f;
@@ -953,30 +934,14 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
         for (int t = 0; t < NT; ++t) ev[t] *= att;
       }
-      if constexpr (!actfill) {
-        mmsg = lane_absmax(ev);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) mmsg = fmaxf(mmsg, fabsf(ev[0][r]));
-      }
+      put_max(TMX_MSG, lane_absmax(ev));
       __builtin_amdgcn_sched_barrier(0);   // keep the stage's stores ahead of the next chain
       STAMP(6);
       // GEMM2 (recompute): phi = coord_nn.2 silu(coord_nn.0 e + bc1)
       f32x16 cv[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) cv[t] = (f32x16)0.f;
-      auto fill2 = [&](int step) {
-        if constexpr (actfill) {
-          const int t = (step >> 2) + 1, g4 = step & 3;
-          if (t < NT) {
-            act_e(t, g4);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) mmsg = fmaxf(mmsg, fabsf(ev[t][4 * g4 + u]));
-          }
-        }
-      };
-      chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(W, L.wc1f, L.wc1x, L.wc1b, ev, cv, lane, fill2);
-      put_max(TMX_MSG, mmsg);
+      chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(W, L.wc1f, L.wc1x, L.wc1b, ev, cv, lane, nofill);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pre_e rows landed
       float part = 0.f;
       float mdz = 0.f;   // max |silu'(c)| (DY of coord_nn.0 = d phi * silu'(c))
@@ -1489,49 +1454,32 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
   if (do_bias) out[(size_t)tid * NB + N] = colf ? bsum * D.colv[tid] : bsum;
 }
 
-// F16X3 form of outer_acc_kernel for the tile-blocked pair rows (M > 1).
-// Each operand gets one power-of-two scale per chunk (max |x| of the chunk ->
-// [2^12, 2^13), as the layer backward's adjoint tiles): the chunk maximum is the
-// max over the per-tile maxima the layer backward stored (BwdArgs::tmax), so no
-// stage computes a maximum and the three products accumulate straight into acc;
-// the exact inverse scales are applied once to the finished sums.  (Per element
-// the split keeps ~22 bits relative to the chunk maximum; rows far below it lose
-// low bits that the sum could not hold anyway.)
-//
-// The stage goes to LDS ALREADY SPLIT: the thread that stages an element scales
-// it and writes its fp16 hi and lo halves to two planes, [column][row] (rows
-// contiguous, OX_LDH halves per column), so an MFMA operand (8 consecutive rows
-// of one column) is two ds_read_b64 per plane and the four waves that read each
-// element share one split instead of two each.  Bias sums come from the staging
-// registers (fixed-order lane sums at the end), not from the LDS image.
+// F16X3 form of outer_acc_kernel for the tile-blocked pair rows (M > 1): the
+// stage's DY / X tiles go to LDS column-major ([column][row], rows contiguous),
+// so an MFMA operand (8 consecutive rows of one column) is one ds_read_b128
+// pair.  Each operand gets one power-of-two scale per chunk (max |x| of the
+// chunk -> [2^12, 2^13), as the layer backward's adjoint tiles) before the
+// hi / lo split: the chunk maximum is the max over the per-tile maxima the
+// layer backward stored (BwdArgs::tmax), so no stage computes a maximum, the
+// three products accumulate straight into acc, and the exact inverse scales
+// are applied once to the finished sums.  (Per element the split keeps ~22
+// bits relative to the chunk maximum; rows far below it lose low bits that
+// the sum could not hold anyway.)
 //
 // Recomputed operands (OuterDesc::recomp) trade HBM bytes for MFMAs: the layer
 // backward stores neither pre(edge_nn.0) nor pre(coord_nn.0) (2 x H floats per
 // pair row written and read back), wave w rebuilds output tile w (features
 // 32 w .. 32 w + 31) of the stage's 32 rows in the forward's "weights = A"
 // orientation (lane = row, registers = features) from the packed forward
-// fragments and writes its split halves to the LDS stage.  RECOMP_PC reads the
-// stage's (scaled, split) messages back with ds_read_b64_tr_b16 as its chain's
-// B operand: lane = row, 4 consecutive features per read.
-#define OX_LDH 36   // LDS column stride (halves): 8-byte aligned, conflict-free b64 / tr reads
+// fragments, and writes it to the LDS stage.
+#define OX_LD 36   // LDS column stride (floats): 16-byte aligned operand reads
+#ifndef ENFLOW_OX_VEC
+#define ENFLOW_OX_VEC 1   // 16-B row staging (A/B knob: 0 = one dword per row)
+#endif
 #ifndef ENFLOW_OUTER_WPS
 #define ENFLOW_OUTER_WPS 2   // outer_x3_kernel occupancy hint (A/B knob)
 #endif
 static_assert(ENFLOW_OUTER_X3 == 1, "pair-row weight gradients run on outer_x3_kernel (recomputed operands)");
-typedef uint16_t OxPlane[128][OX_LDH];   // one plane (hi or lo) of one stage buffer
-
-// 8 values times the power of two s -> packed fp16 hi / lo words, x s = hi + lo
-__device__ __forceinline__ void split8s(const float (&v)[8], float s, uint32_t (&h)[4], uint32_t (&l)[4]) {
-  float x[8];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    x[2 * k] = v[2 * k] * s;
-    x[2 * k + 1] = v[2 * k + 1] * s;
-    const f16x2 hp = {(_Float16)x[2 * k], (_Float16)x[2 * k + 1]};   // v_cvt_pk_f16_f32 (RNE)
-    h[k] = __builtin_bit_cast(uint32_t, hp);
-  }
-  split_lo8(x, h, l);
-}
 
 // F32R (the ENFLOW_BWD_F32 backward): the recomputed operands come from the
 // fp32 MFMA on the forward's fp32 fragments (we1f / wc1f), as that backward's
@@ -1539,7 +1487,7 @@ __device__ __forceinline__ void split8s(const float (&v)[8], float s, uint32_t (
 // lose the accuracy the fp32 re-run was made for.
 template <int H, int RCM, bool GEN = false, bool F32R = false>
 __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int nbi, int r0, int r1,
-                                              OxPlane (*sd)[2], OxPlane (*sx)[2]) {
+                                              float (*sd)[128][OX_LD], float (*sx)[128][OX_LD]) {
   constexpr int NT = H / 32;
   const int NB = D.N + (D.outB ? 1 : 0);
   const int n0 = nbi * 128;
@@ -1548,32 +1496,21 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   const int j = lane & 31, hh = lane >> 5;
   const int mh = w & 1, nh = w >> 1;
   constexpr int rcm = RCM;
-  const bool do_bias = D.outB != nullptr && nbi == 0;   // wave-uniform
-  const bool fold = rcm == RECOMP_PC && D.part2 != nullptr && nbi == 0;   // coord_nn.2's gradient rides along
+  const bool do_bias = D.outB != nullptr && nbi == 0 && tid < M;
+  const bool xf_dy = D.xf_dy != 0, xf_x = D.xf_x != 0;
+  const bool fold = xf_dy && D.part2 != nullptr && nbi == 0;   // coord_nn.2's gradient rides along
   const Act act = GEN && D.actp ? act_of(D.actp) : act_silu();
   // recompute: the layer's packed forward weights
   const int nf = rcm ? D.nf : 1;
   const EgclLayout L = egcl_layout(H, nf);
   const rsrc_t W = weights_rsrc(rcm ? D.Lp : nullptr, rcm ? L.total : 0);
-  // the chunk's scales (one per operand, from the producer's per-tile maxima)
-  static_assert(OA_CHUNK <= 64 * 32, "a chunk's tile maxima fit one wave");
-  int ea = 0, eb = 0;
-  {
-    const int t0 = r0 >> 5, ntl = (r1 - r0 + 31) >> 5;
-    const float ma = lane < ntl ? D.tmaxA[(size_t)(t0 + lane) * TMX_W] : 0.f;
-    const float mb = lane < ntl ? D.tmaxB[(size_t)(t0 + lane) * TMX_W] : 0.f;
-    ea = pow2_exp(wave_max(ma));
-    eb = pow2_exp(wave_max(mb));
-  }
-  const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb);
-  const float ua = ldexpf(1.f, -ea), ub = ldexpf(1.f, -eb);   // exact inverse scales
-  // RECOMP_PC: lane = row sums of d wc2 (wacc2) and of the bias (bacc2), registers = features;
-  // otherwise bacc2[0..3]: the bias partials of the thread's 4 staged columns
-  float wacc2[16], bacc2[16];
+  float wacc[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) wacc2[q] = bacc2[q] = 0.f;
+  for (int q = 0; q < 16; ++q) wacc[q] = 0.f;
+  float bsum = 0.f;
   // edge_nn.0's fragments of output tile w (hi / lo per k-step): loop invariant,
   // loaded once per workgroup and kept in registers (RECOMP_X0)
+  // (the first k-step's; nf = 8's second k-step is read when used)
   f32x4 wfh = (f32x4)0.f, wfl = (f32x4)0.f;
   if constexpr (rcm == RECOMP_X0 && !F32R) {
     if (w < NT) {
@@ -1586,28 +1523,35 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = (f32x16)0.f;
-  // staged rows in registers, one stage ahead: a thread stages 4 consecutive rows
-  // of a column per 16-B load (float4 e4 = q * 256 + tid: column e4 / 8, rows
-  // 4 (e4 % 8) ..); xa4 the 4 rows' X factors, raj row j's aphi (the recompute's
-  // lane row), xb the stage's xin block (the fp32 recompute's operand source)
-  struct Stage { float rd[16], rx[16]; bool pv; f32x4 xa4; float raj; const float* xb; float rad; };
-  Stage S0, S1;
+  // staged rows in registers, one stage ahead
+  // ENFLOW_OX_VEC: a thread stages 4 consecutive rows of a column per 16-B load /
+  // ds_write_b128 (float4 e4 = q * 256 + tid: column e4 / 8, rows 4 (e4 % 8) ..),
+  // 4x fewer memory instructions than one dword per row; ra4 / xa4 the 4 rows'
+  // factors, raj row j's (the recompute's lane row)
+  struct Stage { float rd[16], rx[16], ra, xa; bool pv; f32x4 ra4, xa4; float raj; const float* xb; float rad; };
+  Stage S0;
   const int nst = (r1 - r0 + OB_ROWS - 1) / OB_ROWS;
-  const int r4 = (tid & 7) * 4;
+  // thread element q: column c = 8 q + tid / 32, row r = tid % 32 of the stage
   auto gload = [&](int st, Stage& G) {
     const int rb = r0 + st * OB_ROWS;
     const size_t rt = (size_t)(rb >> 5);
     const float* const dblk = D.DY + ((rt * D.ldd) << 5);
     const float* const xblk = D.X + ((rt * D.ldx + n0) << 5);
-    const bool pv = rb + j < r1;
+    const bool pv = rb + (tid & 31) < r1;
     G.pv = pv;
+    G.ra = 0.f;
+    G.xa = 1.f;
     G.xb = xblk;
+#if ENFLOW_OX_VEC
     if (rcm == RECOMP_PC) G.raj = pv ? D.rowv[rb + j] : 0.f;
-    // stage rows are whole 32-row tiles (pair rows are 32-aligned), so a float4
-    // of rows is valid or not as a whole
-    const bool pv4 = rb + r4 + 3 < r1;
     if constexpr (rcm != RECOMP_X0) {
+      // stage rows are whole 32-row tiles (pair rows are 32-aligned), so a float4
+      // of rows is valid or not as a whole
+      const int r4 = (tid & 7) * 4;
+      const bool pv4 = rb + r4 + 3 < r1;
+      G.ra4 = (f32x4)0.f;
       G.xa4 = (f32x4)1.f;
+      if (xf_dy) G.ra4 = pv4 ? ld4(D.rowv + rb + r4) : (f32x4)0.f;
       if (D.xrow) G.xa4 = pv4 ? ld4(D.xrow + rb + r4) : (f32x4)0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -1623,12 +1567,24 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
       }
       return;
     } else {   // RECOMP_X0: DY as float4 rows here, the X operand (xin) below
+      const int r4 = (tid & 7) * 4;
+      const bool pv4 = rb + r4 + 3 < r1;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int e4 = q * 256 + tid, c = e4 >> 3;
         const f32x4 d = (pv4 && c < M) ? ld4(dblk + 4 * e4) : (f32x4)0.f;
 #pragma unroll
         for (int u = 0; u < 4; ++u) G.rd[4 * q + u] = d[u];
+      }
+    }
+#endif
+    if (xf_dy) G.ra = pv ? D.rowv[rb + (tid & 31)] : 0.f;
+    if (D.xrow) G.xa = pv ? D.xrow[rb + (tid & 31)] : 0.f;
+    if constexpr (rcm != RECOMP_PC && !ENFLOW_OX_VEC) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = 8 * q + (tid >> 5);
+        G.rd[q] = (pv && c < M) ? dblk[(unsigned)(q * 256 + tid)] : 0.f;
       }
     }
     if constexpr (rcm == RECOMP_X0 && F32R) {
@@ -1656,59 +1612,47 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         const float rad = pv ? xblk[(2 * nf) * 32 + j] : 0.f;
         G.rad = 0.f;
         if (gemm0_radial_slot7(nf)) {
-          if (hh) G.rx[8 * nch - 1] = rad;
+          if (hh) {   // slot 8 nch - 1 (nch 1 / 2), by compile-time index: a runtime one puts Stage in scratch
+#pragma unroll
+            for (int u = 7; u < 16; u += 8)
+              if (u == 8 * nch - 1) G.rx[u] = rad;
+          }
         } else if (hh == 0) {
           if (nch == 1) G.rx[8] = rad;   // nf == 8: the radial's own (second) slice
           else G.rad = rad;              // nf == 16: the third slice
         }
       }
-    }
-  };
-  // 16 consecutive staged elements (4 columns x 4 rows) -> scaled split into the planes
-  auto put_cols = [&](OxPlane* P, const float (&v)[16], float s) {
+    } else {
 #pragma unroll
-    for (int qq = 0; qq < 2; ++qq) {
-      float x8[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x8[e] = v[8 * qq + e];
-      uint32_t h[4], l[4];
-      split8s(x8, s, h, l);
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        const int c = ((2 * qq + half) * 256 + tid) >> 3;
-        *reinterpret_cast<u32x2v*>(&P[0][c][r4]) = (u32x2v){h[2 * half], h[2 * half + 1]};
-        *reinterpret_cast<u32x2v*>(&P[1][c][r4]) = (u32x2v){l[2 * half], l[2 * half + 1]};
-      }
-    }
-  };
-  // a recompute wave's 16 values (lane = row j, features 32 w + rho(r, hh)) -> planes
-  auto put_rows = [&](OxPlane* P, const float (&v)[16], float s) {
-#pragma unroll
-    for (int gg = 0; gg < 2; ++gg) {
-      float x8[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) x8[e] = v[8 * gg + e];
-      uint32_t h[4], l[4];
-      split8s(x8, s, h, l);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int f = 32 * w + rho(8 * gg + e, hh);
-        const int sh = 16 * (e & 1);
-        P[0][f][j] = (uint16_t)(h[e >> 1] >> sh);
-        P[1][f][j] = (uint16_t)(l[e >> 1] >> sh);
+      for (int q = 0; q < 16; ++q) {
+        const int c = 8 * q + (tid >> 5);
+        G.rx[q] = (pv && n0 + c < N) ? xblk[(unsigned)(q * 256 + tid)] : 0.f;
       }
     }
   };
   auto lstore = [&](int buf, Stage& G) {
-    if constexpr (rcm != RECOMP_PC) {   // DY rows from HBM (no transform)
-      put_cols(sd[buf], G.rd, sa);
-      if (do_bias) {
+#if ENFLOW_OX_VEC
+    if constexpr (rcm != RECOMP_X0) {
+      const int r4 = (tid & 7) * 4;
+      if constexpr (rcm != RECOMP_PC) {
+        if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) bacc2[q] += (G.rd[4 * q] + G.rd[4 * q + 1]) + (G.rd[4 * q + 2] + G.rd[4 * q + 3]);
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const float z = G.rd[4 * q + u];
+              float fz, dz;
+              act_fd<GEN>(act, z, fz, dz);
+              if (fold) wacc[q] = fmaf(G.ra4[u], fz, wacc[q]);
+              G.rd[4 * q + u] = G.ra4[u] * dz;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          st4(&sd[buf][(q * 256 + tid) >> 3][r4],
+              (f32x4){G.rd[4 * q], G.rd[4 * q + 1], G.rd[4 * q + 2], G.rd[4 * q + 3]});
       }
-    }
-    if constexpr (rcm != RECOMP_X0) {   // X rows from HBM: act (xf_x), times the row factor (xrow)
-      if (D.xf_x) {
+      if (xf_x) {
 #pragma unroll
         for (int q = 0; q < 16; ++q) G.rx[q] = act_v<GEN>(act, G.rx[q]);
       }
@@ -1716,8 +1660,33 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
 #pragma unroll
         for (int q = 0; q < 16; ++q) G.rx[q] *= G.xa4[q & 3];
       }
-      put_cols(sx[buf], G.rx, sbs);
-    } else if constexpr (F32R) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(&sx[buf][(q * 256 + tid) >> 3][r4], (f32x4){G.rx[4 * q], G.rx[4 * q + 1], G.rx[4 * q + 2], G.rx[4 * q + 3]});
+      return;
+    } else {   // RECOMP_X0: DY rows as float4 (no transform on edge_nn.2's DY)
+      const int r4 = (tid & 7) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        st4(&sd[buf][(q * 256 + tid) >> 3][r4],
+            (f32x4){G.rd[4 * q], G.rd[4 * q + 1], G.rd[4 * q + 2], G.rd[4 * q + 3]});
+    }
+#endif
+    if constexpr (rcm != RECOMP_PC && !(ENFLOW_OX_VEC && rcm == RECOMP_X0)) {
+      if (xf_dy) {   // DY = aphi * silu'(pc) (wc2 applied at the end); d wc2 += aphi * silu(pc)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float z = G.rd[q];
+          float fz, dz;
+          act_fd<GEN>(act, z, fz, dz);
+          if (fold) wacc[q] = fmaf(G.ra, fz, wacc[q]);
+          G.rd[q] = G.ra * dz;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sd[buf][8 * q + (tid >> 5)][tid & 31] = G.rd[q];
+    }
+    if constexpr (rcm == RECOMP_X0 && F32R) {
       if (w < NT) {   // output tile w of pre0 -> act -> X, fp32 MFMA (the forward's f32 GEMM0 k order)
         f32x16 x = (f32x16)0.f;
 #pragma unroll
@@ -1735,16 +1704,15 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
           const float b = (G.pv && col >= 0) ? G.xb[col * 32 + j] : 0.f;
           x = mfma32(bload(W, lane * 4, (L.we1f + (w * (NFMAX + 1) + s) * 64) * 4), b, x);
         }
-        float v[16];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 b = ld4(D.Lp + L.be1 + 32 * w + 8 * g4 + 4 * hh);
+          const int f0 = 32 * w + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(D.Lp + L.be1 + f0);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[4 * g4 + u] = G.pv ? act_v<GEN>(act, x[4 * g4 + u] + b[u]) : 0.f;
+          for (int u = 0; u < 4; ++u) sx[buf][f0 + u][j] = G.pv ? act_v<GEN>(act, x[4 * g4 + u] + b[u]) : 0.f;
         }
-        put_rows(sx[buf], v, sbs);
       }
-    } else {
+    } else if constexpr (rcm == RECOMP_X0) {
       if (w < NT) {   // output tile w of pre0 -> silu -> X
         const int ks_n = gemm0_ksteps(nf);
         f32x16 x = (f32x16)0.f;
@@ -1771,44 +1739,38 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
           x = mfma_f16(al, bh, x);
         }
         x *= D.Lp[L.scl + 5];
-        float v[16];
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const f32x4 b = ld4(D.Lp + L.be1 + 32 * w + 8 * g4 + 4 * hh);
+          const int f0 = 32 * w + 8 * g4 + 4 * hh;
+          const f32x4 b = ld4(D.Lp + L.be1 + f0);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) v[4 * g4 + u] = G.pv ? act_v<GEN>(act, x[4 * g4 + u] + b[u]) : 0.f;
+          for (int u = 0; u < 4; ++u) sx[buf][f0 + u][j] = G.pv ? act_v<GEN>(act, x[4 * g4 + u] + b[u]) : 0.f;
         }
-        put_rows(sx[buf], v, sbs);
       }
+    } else {
+      if (xf_x) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) G.rx[q] = act_v<GEN>(act, G.rx[q]);
+      }
+      if (D.xrow) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) G.rx[q] *= G.xa;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sx[buf][8 * q + (tid >> 5)][tid & 31] = G.rx[q];
     }
   };
   // RECOMP_PC, after the stage's X is in LDS: pc = coord_nn.0 . X + bc1 (output
   // tile w), DY = aphi * silu'(pc) into LDS, d wc2 partial += aphi * silu(pc)
-  // ds_read_b64_tr_b16 addressing: lane 4 q + p of a 16-lane group reads feature
-  // f0 + q, rows (16 (lane & 16)) + 4 p ..; lane i of the group gets row i's 4 features
-  const int tq = (lane & 15) >> 2, tjb = (lane & 16) + 4 * (lane & 3);
-  auto trd = [&](const OxPlane& P, int f0) -> s16x4 {
-    return lds_tr16(reinterpret_cast<const uint32_t*>(&P[f0 + tq][tjb]));
-  };
+  float (&wacc2)[16] = wacc;   // RECOMP_PC's d wc2 partials (lane = row, registers = features)
   auto recomp_pc = [&](int buf, const Stage& G) {
-    if (w >= NT) return;
-    f32x16 cacc = (f32x16)0.f;
-    float cs;   // pc = cacc * cs + bc1
-    if constexpr (F32R) {   // fp32 chain of output tile w on wc1f (the forward's f32 k order)
+    if (F32R && w < NT) {   // fp32 chain of output tile w on wc1f (the forward's f32 k order)
+      f32x16 cacc = (f32x16)0.f;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         f32x16 X;
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            const int f0 = 32 * t + 16 * s2 + 8 * hf + 4 * hh;
-            typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
-            const f16x4v xh = __builtin_bit_cast(f16x4v, trd(sx[buf][0], f0));
-            const f16x4v xl = __builtin_bit_cast(f16x4v, trd(sx[buf][1], f0));
-#pragma unroll
-            for (int u = 0; u < 4; ++u) X[8 * s2 + 4 * hf + u] = ((float)xh[u] + (float)xl[u]) * ub;
-          }
+        for (int r = 0; r < 16; ++r) X[r] = sx[buf][32 * t + rho(r, hh)][j];
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) {
           const f32x4 a4 = bload4(W, lane * 16, (L.wc1f + ((w * NT + t) * 4 + rg) * 256) * 4);
@@ -1816,12 +1778,26 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
           for (int u = 0; u < 4; ++u) cacc = mfma32(a4[u], X[4 * rg + u], cacc);
         }
       }
-      cs = 1.f;
-    } else {
+      const float ra = ENFLOW_OX_VEC ? G.raj : G.ra;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int f0 = 32 * w + 8 * g4 + 4 * hh;
+        const f32x4 b = ld4(D.Lp + L.bc1 + f0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float z = cacc[4 * g4 + u] + b[u];
+          float fz, dz;
+          act_fd<GEN>(act, z, fz, dz);
+          wacc2[4 * g4 + u] = fmaf(ra, fz, wacc2[4 * g4 + u]);
+          sd[buf][f0 + u][j] = ra * dz;
+        }
+      }
+    } else if (w < NT) {
       // coord_nn.0's fragments of output tile w, requested half a chain at a time
       // (two L2 round trips per stage; resident they would cost 64 VGPRs across
-      // the stage); the B operand straight from the split planes (scaled by sbs)
+      // the stage)
       constexpr int HALF = NT > 1 ? NT : 2;   // k-steps per request group
+      f32x16 cacc = (f32x16)0.f;
 #pragma unroll
       for (int g = 0; g < 2 * NT; g += HALF) {
         f32x4 ch[HALF], cl[HALF];
@@ -1834,73 +1810,100 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
         }
         // chain_x3_fill's per-tile order: k-steps ascending, hi.hi, hi.lo, lo.hi
 #pragma unroll
-        for (int q = 0; q < HALF; ++q) {
-          const int ts = g + q, t = ts >> 1, s2 = ts & 1;
-          // fragment element e = feature 32 t + rho(8 s2 + e, hh) = 32 t + 16 s2 + 8 (e >> 2) + 4 hh + (e & 3)
-          const int f0 = 32 * t + 16 * s2 + 4 * hh;
-          const f16x8 bh = cat_f16x8(trd(sx[buf][0], f0), trd(sx[buf][0], f0 + 8));
-          const f16x8 bl = cat_f16x8(trd(sx[buf][1], f0), trd(sx[buf][1], f0 + 8));
-          cacc = mfma_f16(ch[q], bh, cacc);
-          cacc = mfma_f16(ch[q], bl, cacc);
-          cacc = mfma_f16(cl[q], bh, cacc);
+        for (int q = 0; q < HALF; q += 2) {
+          const int t = (g + q) >> 1;
+          f32x16 X;   // input tile t in the accumulator layout (lane = row, registers = features)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) X[r] = sx[buf][32 * t + rho(r, hh)][j];
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+            f16x8 bh, bl;
+            split_f16(X, s2, bh, bl);
+            cacc = mfma_f16(ch[q + s2], bh, cacc);
+            cacc = mfma_f16(ch[q + s2], bl, cacc);
+            cacc = mfma_f16(cl[q + s2], bh, cacc);
+          }
         }
       }
-      cs = D.Lp[L.scl + 3] * ub;
-    }
-    const float ra = G.raj;   // row j's aphi
-    float v[16];
+      const float inv2 = D.Lp[L.scl + 3];
+      const float ra = ENFLOW_OX_VEC ? G.raj : G.ra;   // row j's aphi
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 b = ld4(D.Lp + L.bc1 + 32 * w + 8 * g4 + 4 * hh);
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int f0 = 32 * w + 8 * g4 + 4 * hh;
+        const f32x4 b = ld4(D.Lp + L.bc1 + f0);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float z = fmaf(cacc[4 * g4 + u], cs, b[u]);
-        float fz, dz;
-        act_fd<GEN>(act, z, fz, dz);
-        wacc2[4 * g4 + u] = fmaf(ra, fz, wacc2[4 * g4 + u]);
-        v[4 * g4 + u] = ra * dz;
-        bacc2[4 * g4 + u] += v[4 * g4 + u];
+        for (int u = 0; u < 4; ++u) {
+          const float z = fmaf(cacc[4 * g4 + u], inv2, b[u]);
+          float fz, dz;
+          act_fd<GEN>(act, z, fz, dz);
+          wacc2[4 * g4 + u] = fmaf(ra, fz, wacc2[4 * g4 + u]);
+          sd[buf][f0 + u][j] = ra * dz;
+        }
       }
     }
-    put_rows(sd[buf], v, sa);
   };
   const bool use_m1 = mh * 64 + 32 < M, use_n0 = n0 + nh * 64 < N, use_n1 = n0 + nh * 64 + 32 < N;
   const bool live = mh * 64 < M && use_n0;
+  // the chunk's scales (one per operand, from the producer's per-tile maxima):
+  // max |x| of the chunk -> [2^12, 2^13) before the hi / lo split, so the three
+  // products accumulate straight into acc and are un-scaled once at the end
+  static_assert(OA_CHUNK <= 64 * 32, "a chunk's tile maxima fit one wave");
+  int ea = 0, eb = 0;
+  {
+    const int t0 = r0 >> 5, ntl = (r1 - r0 + 31) >> 5;
+    const float ma = lane < ntl ? D.tmaxA[(size_t)(t0 + lane) * TMX_W] : 0.f;
+    const float mb = lane < ntl ? D.tmaxB[(size_t)(t0 + lane) * TMX_W] : 0.f;
+    ea = pow2_exp(wave_max(ma));
+    eb = pow2_exp(wave_max(mb));
+  }
+  const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb);
   auto compute = [&](int buf) {
-    if (!live) return;
-    // operands of both k-steps: A[a][ks] (DY columns), B[b][ks] (X columns), rows
-    // 16 ks + 8 hh .. + 7 of the column, hi / lo planes
-    f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
-    auto rd8 = [&](const OxPlane& P, int c, int ks) -> f16x8 {
-      const uint16_t* p = &P[c][16 * ks + 8 * hh];
-      const u32x2v x0 = *reinterpret_cast<const u32x2v*>(p), x1 = *reinterpret_cast<const u32x2v*>(p + 4);
-      return __builtin_bit_cast(f16x8, (u32x4v){x0[0], x0[1], x1[0], x1[1]});
-    };
+    if (live) {
+      // operands of both k-steps: A[a][ks] (DY columns), B[b][ks] (X columns)
+      f32x4 av[2][2][2], bv[2][2][2];   // [tile][ks][half]
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        ah[a][ks] = rd8(sd[buf][0], mh * 64 + a * 32 + j, ks);
-        al[a][ks] = rd8(sd[buf][1], mh * 64 + a * 32 + j, ks);
-        bh[a][ks] = rd8(sx[buf][0], nh * 64 + a * 32 + j, ks);
-        bl[a][ks] = rd8(sx[buf][1], nh * 64 + a * 32 + j, ks);
-      }
+        for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+          for (int h2 = 0; h2 < 2; ++h2) {
+            av[a][ks][h2] = *reinterpret_cast<const f32x4*>(&sd[buf][mh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2]);
+            bv[a][ks][h2] = *reinterpret_cast<const f32x4*>(&sx[buf][nh * 64 + a * 32 + j][16 * ks + 8 * hh + 4 * h2]);
+          }
+      f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
+      // scaled hi / lo split: hi = f16(x s) by v_cvt_pk_f16_f32, lo = f16(x s - hi) by
+      // v_fma_mix (split_f16; x s - hi is exact in fp32, so bitwise the plain form)
 #pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if ((a == 1 && !use_m1) || (b == 1 && !use_n1)) continue;
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bh[b][ks], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bl[b][ks], acc[a][b], 0, 0, 0);
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a][ks], bh[b][ks], acc[a][b], 0, 0, 0);
+          f32x16 xa, xb;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            xa[jj] = av[a][ks][jj >> 2][jj & 3] * sa;
+            xb[jj] = bv[a][ks][jj >> 2][jj & 3] * sbs;
+          }
+          split_f16(xa, 0, ah[a][ks], al[a][ks]);
+          split_f16(xb, 0, bh[a][ks], bl[a][ks]);
         }
-      }
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          if ((a == 1 && !use_m1) || (b == 1 && !use_n1)) continue;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bh[b][ks], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bl[b][ks], acc[a][b], 0, 0, 0);
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a][ks], bh[b][ks], acc[a][b], 0, 0, 0);
+          }
+        }
+    }
+    if (do_bias) {
+#pragma unroll 8
+      for (int r = 0; r < OB_ROWS; ++r) bsum += sd[buf][tid][r];
+    }
   };
-  // rows two stages ahead in registers (S0 / S1 alternate; the loop is unrolled
-  // by two so each keeps its registers): a stage's loads have a whole stage of
-  // compute to land before its lstore
   gload(0, S0);
   lstore(0, S0);
   __syncthreads();
@@ -1908,24 +1911,19 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
     recomp_pc(0, S0);
     __syncthreads();
   }
-  if (nst > 1) gload(1, S1);
-  auto iter = [&](int st, Stage& Snext, Stage& Sfree) {
+  for (int st = 0; st < nst; ++st) {
     const int buf = st & 1;
-    if (st + 2 < nst) gload(st + 2, Sfree);
+    if (st + 1 < nst) gload(st + 1, S0);
     compute(buf);
-    if (st + 1 < nst) lstore(buf ^ 1, Snext);
+    if (st + 1 < nst) lstore(buf ^ 1, S0);
     __syncthreads();
     if (rcm == RECOMP_PC && st + 1 < nst) {
-      recomp_pc(buf ^ 1, Snext);
+      recomp_pc(buf ^ 1, S0);
       __syncthreads();
     }
-  };
-  for (int st = 0; st < nst; st += 2) {
-    iter(st, S1, S0);
-    if (st + 1 < nst) iter(st + 1, S0, S1);
   }
   float* out = D.part + (size_t)chunk * M * NB;
-  const bool colf = rcm == RECOMP_PC;   // DY = aphi * wc2 * silu'(pc): wc2[m] applied to the sums
+  const float ua = ldexpf(1.f, -ea), ub = ldexpf(1.f, -eb);   // exact inverse scales
 #pragma unroll
   for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1934,31 +1932,35 @@ __device__ __forceinline__ void outer_x3_body(const OuterDesc& D, int chunk, int
       for (int r = 0; r < 16; ++r) {
         const int mm = mh * 64 + a * 32 + rho(r, hh), nn = n0 + nh * 64 + b * 32 + j;
         const float v = acc[a][b][r] * ua * ub;
-        if (mm < M && nn < N) out[(size_t)mm * NB + nn] = colf ? v * D.colv[mm] : v;
+        if (mm < M && nn < N) out[(size_t)mm * NB + nn] = xf_dy ? v * D.colv[mm] : v;
       }
-  if constexpr (rcm == RECOMP_PC) {   // fixed-order sums over the 32 rows of each half-wave
+  if (do_bias) out[(size_t)tid * NB + N] = xf_dy ? bsum * D.colv[tid] : bsum;
+  if (fold && rcm == RECOMP_PC) {   // fixed-order sum over the 32 rows of each half-wave
     if (w < NT) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float v = wacc2[r], bs = bacc2[r];
+        float v = wacc2[r];
 #pragma unroll
-        for (int off = 16; off > 0; off >>= 1) {
-          v += __shfl_xor(v, off, 64);
-          bs += __shfl_xor(bs, off, 64);
-        }
-        const int m = 32 * w + rho(r, hh);
-        if (j == 0 && fold) D.part2[(size_t)chunk * M + m] = v;
-        if (j == 0 && do_bias) out[(size_t)m * NB + N] = bs * D.colv[m];
+        for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (j == 0) D.part2[(size_t)chunk * M + 32 * w + rho(r, hh)] = v;
       }
     }
-  } else if (do_bias) {   // fixed-order sum over the 8 row groups of each column
+  } else if (fold && ENFLOW_OX_VEC) {   // fixed-order sum over the 8 row groups of each column
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      float v = bacc2[q];
+      float v = wacc[q];
 #pragma unroll
       for (int off = 1; off < 8; off <<= 1) v += __shfl_xor(v, off, 64);
       const int c = (q * 256 + tid) >> 3;
-      if ((tid & 7) == 0 && c < M) out[(size_t)c * NB + N] = v;
+      if ((tid & 7) == 0 && c < M) D.part2[(size_t)chunk * M + c] = v;
+    }
+  } else if (fold) {   // fixed-order sum over the 32 rows a half-wave holds
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      float v = wacc[q];
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if ((tid & 31) == 0 && 8 * q + (tid >> 5) < M) D.part2[(size_t)chunk * M + 8 * q + (tid >> 5)] = v;
     }
   }
 }
@@ -1974,8 +1976,8 @@ __global__ void __launch_bounds__(256, ENFLOW_OUTER_WPS) outer_x3_kernel(OuterBa
   const int r0 = chunk * D.chunk;
   if (r0 >= rows) return;
   const int r1 = min(rows, r0 + D.chunk);
-  __shared__ __attribute__((aligned(16))) OxPlane sd[2][2];   // [buffer][hi / lo]
-  __shared__ __attribute__((aligned(16))) OxPlane sx[2][2];
+  __shared__ float sd[2][128][OX_LD];
+  __shared__ float sx[2][128][OX_LD];
   // recomputed operands need the layer's hidden width at compile time
   // (one register allocation per branch: the modes' staged operands differ)
   if (D.recomp == RECOMP_X0) {
