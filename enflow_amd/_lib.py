@@ -23,7 +23,6 @@ ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2
 ERR_TOO_MANY_FEATURES = 4
 ERR_RANGE = 8
-ERR_INTERNAL = 16
 DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
 PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
@@ -39,8 +38,6 @@ SIGNATURES = {
     "enflow_abi_version": (_i, []),
     "enflow_set_latency_threshold": (_i, [_i]),
     "enflow_latency_threshold": (_i, []),
-    "enflow_set_coop_max": (_i, [_i]),
-    "enflow_coop_max": (_i, []),
     "enflow_max_atoms": (_i, []),
     "enflow_max_node_nf": (_i, []),
     "enflow_supports_hidden": (_i, [_i]),
@@ -144,28 +141,11 @@ def lib(nf=None):
             fn.argtypes = args
         if _lat_threshold[0] is not None and hasattr(handle, "enflow_set_latency_threshold"):
             handle.enflow_set_latency_threshold(_lat_threshold[0])
-        if _coop_max[0] is not None and hasattr(handle, "enflow_set_coop_max"):
-            handle.enflow_set_coop_max(_coop_max[0])
         _libs[path] = handle
     return handle
 
 
 _lat_threshold = [None]
-_coop_max = [None]
-
-
-def set_coop_max(max_mols):
-    """Route fused <= 32-atom inference launches of at most `max_mols`
-    molecules (and within the latency threshold) to the cooperative instance,
-    two workgroups per molecule (-1: half the device's CU count, the default;
-    0: never).  Per library like set_latency_threshold; returns the previous
-    setting (None: never set from Python)."""
-    prev = _coop_max[0]
-    _coop_max[0] = int(max_mols)
-    for h in _libs.values():
-        if hasattr(h, "enflow_set_coop_max"):
-            h.enflow_set_coop_max(int(max_mols))
-    return prev
 
 
 def set_latency_threshold(max_mols):
@@ -343,9 +323,6 @@ def _raise_code(e):
         raise HipPathError(f"molecule larger than {lib().enflow_max_atoms()} atoms")
     if e & ERR_TOO_MANY_FEATURES:
         raise HipPathError(f"node_nf larger than the kernels' feature width (at most {MAX_NODE_NF})")
-    if e & ERR_INTERNAL:
-        raise HipPathError("the cooperative flow instance's two workgroups of a molecule did not meet "
-                           "within the wait bound (no result); enflow_amd._lib.set_coop_max(0) disables it")
     if e & ERR_RANGE:
         raise RangeError("a split-precision (f16x3 / bf16) GEMM operand left the range its split "
                          "represents at fp32 accuracy (an fp16 / bf16 overflow, or a layer whose "

@@ -14,7 +14,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SRCS = [os.path.join(CSRC, f) for f in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip", "enflow_timing.hip",
-                                              "enflow_latency.hip", "enflow_coop.hip")
+                                              "enflow_latency.hip")
         if os.path.exists(os.path.join(CSRC, f))]
 HDRS = [os.path.join(CSRC, h) for h in ("flow_device.h", "flow_kernel.h", "enflow_timing.h", "enflow_large.h",
                                          "enflow_latency.h")] + [os.path.join(ROOT, "include", "enflow_hip.h")]

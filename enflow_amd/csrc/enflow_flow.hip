@@ -487,10 +487,6 @@ static int lat_threshold_now() {
 
 template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
-  if (NN == 32 && num_mols <= enflow_coop_max_now() && num_mols <= lat_threshold_now()) {
-    FlowArgs Ac = A;   // + the stream's exchange buffer and epoch
-    if (enflow_coop_launch(HH, REV, prec, num_mols, st, &Ac)) return;
-  }
   if (NN == 32 && num_mols <= lat_threshold_now() && enflow_lat_launch(HH, REV, prec, num_mols, st, &A)) return;
   if (prec & ENFLOW_EGCL_VARIANTS) launch_flow_v<HH, NN, RBB, REV, true>(prec & 0xff, num_mols, st, A);
   else launch_flow_v<HH, NN, RBB, REV, false>(prec, num_mols, st, A);
@@ -517,8 +513,6 @@ int enflow_set_latency_threshold(int max_mols) {
   return prev;
 }
 int enflow_latency_threshold(void) { return lat_threshold_now(); }
-int enflow_set_coop_max(int max_mols) { return enflow_coop_set_max(max_mols); }
-int enflow_coop_max(void) { return enflow_coop_max_now(); }
 int enflow_max_atoms(void) { return MAX_ATOMS; }
 int enflow_max_node_nf(void) { return NFMAX; }
 int enflow_supports_hidden(int hidden_nf) { return hid_ok(hidden_nf); }

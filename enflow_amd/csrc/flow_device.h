@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 12
+#define ENFLOW_ABI 11
 #ifndef WAVES
 #define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
 #endif
@@ -1518,19 +1518,14 @@ template <int H, int NMAX, int RB, int PREC = PREC_F32, bool VAR = false, bool B
 __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* __restrict__ Lp, const EgclLayout& L,
                                            const MolRef& M, int nf, int tid, int r0, int rb,
                                            bool zero_agg STAMP_ARGS, const float* __restrict__ cpos = nullptr,
-                                           const float* __restrict__ ch = nullptr, Pre&& pre = NoMid{},
-                                           int part = 0, int nparts = 1) {
+                                           const float* __restrict__ ch = nullptr, Pre&& pre = NoMid{}) {
   constexpr int NT = H / 32;
   constexpr int AST = Smem<H, NMAX, RB>::AST;
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave index: SGPR
   const int j = lane & 31, hh = lane >> 5;
   const int P = sm.npairs;
-  // this workgroup's tiles [TB0, TB1): all of them, or its part of the
-  // molecule's when `nparts` workgroups share it (enflow_coop.hip)
-  const int TALL = (P + 31) >> 5;
-  const int TPP = (TALL + nparts - 1) / nparts;
-  const int TB0 = min(TALL, part * TPP), T = min(TALL, TB0 + TPP);
-  const int tpw = (T - TB0 + WAVES - 1) / WAVES;
+  const int T = (P + 31) >> 5;
+  const int tpw = (T + WAVES - 1) / WAVES;
 
   // zero aggregates / heads, stage biases, find each wave's head row
   if (zero_agg)   // first compaction pass of the block (later passes accumulate)
@@ -1558,7 +1553,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
     }
   }
   if (tid < WAVES) {
-    const int t0 = TB0 + tid * tpw;
+    const int t0 = tid * tpw;
     int hr = -1, ih = 0;
     if (t0 < T) {
       const int p0 = t0 * 32;
@@ -1570,7 +1565,7 @@ __device__ __forceinline__ void edge_tiles(Smem<H, NMAX, RB>& sm, const float* _
   }
   __syncthreads();
 
-  const int t0 = TB0 + w * tpw, t1 = min(T, t0 + tpw);
+  const int t0 = w * tpw, t1 = min(T, t0 + tpw);
   const int headrow = sm.headrow[w];
   const bool ishead = sm.ishead[w] != 0;
   const int nh = (nf + 1) >> 1;
@@ -2461,22 +2456,14 @@ struct FlowArgs {
   uint32_t* ticket = nullptr;
   float* ldj_total = nullptr;
   double ldj_cst = 0.0;
-  // cooperative instance (enflow_coop.hip, two workgroups per molecule): the
-  // pair's exchange rows [num_mols][2][coop_stride] and flags [num_mols][2],
-  // epoch = this launch's base (flag value of layer it: epoch + it + 1)
-  float* xchg = nullptr;
-  uint32_t* xflag = nullptr;
-  uint32_t epoch = 0;
-  int coop_stride = 0;
   __device__ __forceinline__ NoiseSrc noise_src() const { return NoiseSrc{noise, seed, offset}; }
 };
 
 enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
 
 template <int H, int NMAX, int RB>
-__device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowArgs& A, MolRef& M, int what,
-                                              int mol = -1) {
-  const int m = mol < 0 ? (int)blockIdx.x : mol;
+__device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowArgs& A, MolRef& M, int what) {
+  const int m = blockIdx.x;
   const int tid = threadIdx.x;
   M.a0 = A.mol_ptr[m];
   M.n = A.mol_ptr[m + 1] - M.a0;

@@ -11,70 +11,6 @@
 #ifndef ENFLOW_BLOCKED_WPS
 #define ENFLOW_BLOCKED_WPS ENFLOW_WAVES_PER_SIMD   // row-blocked (> 64-atom) instances
 #endif
-// ENFLOW_COOP (enflow_coop.hip): two workgroups per molecule on two CUs (a
-// cooperative launch, both resident).  Workgroup 2 m + p runs molecule m's
-// pair build, node phase and update in full -- the same instructions on the
-// same data as its partner, so both hold bitwise the same state -- but only
-// its half p of each layer's edge tiles; after the tiles the pair swaps its
-// aggregate rows (message sums, force sums) through global memory and each
-// adds the partner's (a + b == b + a in IEEE arithmetic: both get the same
-// sums).  Workgroup 2 m writes the molecule's outputs.
-#ifndef ENFLOW_COOP
-#define ENFLOW_COOP 0
-#endif
-#if ENFLOW_COOP
-// wait bound of the exchange (s_sleep rounds of ~64 cycles: ~0.1 s); a pair
-// that never meets raises ENFLOW_ERR_INTERNAL instead of hanging the launch
-#define ENFLOW_COOP_SPINS (1 << 22)
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ void coop_exchange(Smem<H, NMAX, RB>& sm, const FlowArgs& A, int mol, int part, int n,
-                                              uint32_t flag_value) {
-  constexpr int AST = Smem<H, NMAX, RB>::AST;
-  const int tid = threadIdx.x;
-#if defined(ENFLOW_COOP_DIAG) && ENFLOW_COOP_DIAG == 1
-  return;   // A/B diagnostic (wrong results): the tile split without any exchange
-#endif
-  uint32_t* const mine = reinterpret_cast<uint32_t*>(A.xchg + ((size_t)mol * 2 + part) * A.coop_stride);
-  const uint32_t* const theirs = reinterpret_cast<const uint32_t*>(A.xchg + ((size_t)mol * 2 + (part ^ 1)) * A.coop_stride);
-  const int cnt = n * AST;
-  // device-scope relaxed atomics: coherent across the XCDs' L2s without a
-  // whole-cache release / acquire; the flag is stored once every data store of
-  // the workgroup has completed (vmcnt(0), then the barrier)
-  for (int e = tid; e < cnt; e += BLOCK)
-    __hip_atomic_store(&mine[e], __float_as_uint(sm.agg[e]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid == 0) {
-    __hip_atomic_store(&mine[cnt], (uint32_t)sm.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&mine[cnt + 1], sm.big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    __hip_atomic_store(&A.xflag[(size_t)mol * 2 + part], flag_value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-#if defined(ENFLOW_COOP_DIAG) && ENFLOW_COOP_DIAG == 2
-    spins = ENFLOW_COOP_SPINS;   // A/B diagnostic (wrong results): the exchange's traffic without the wait
-#endif
-    while (spins < ENFLOW_COOP_SPINS && (int)(__hip_atomic_load(&A.xflag[(size_t)mol * 2 + (part ^ 1)], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT) - flag_value) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins >= ENFLOW_COOP_SPINS) {
-        sm.err |= ENFLOW_ERR_INTERNAL;
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  for (int e = tid; e < cnt; e += BLOCK) {
-    const float t = __uint_as_float(__hip_atomic_load(&theirs[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    sm.agg[e] = sm.agg[e] + t;   // commutative: the partner computes t' + a' = the same sum
-  }
-  if (tid == 0) {
-    sm.err |= (int)__hip_atomic_load(&theirs[cnt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.big |= __hip_atomic_load(&theirs[cnt + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-}
-#endif
 // batch log|detJ| in the same launch: every workgroup publishes its ldj_mol
 // entry and takes a ticket; the last one sums ldj_mol in reduce_ldj_kernel's
 // fixed order (per-thread strided double sums, then a tree over the block) --
@@ -84,8 +20,7 @@ __device__ __forceinline__ void ticket_reduce_ldj(const FlowArgs& A, double* red
   const int tid = threadIdx.x;
   __threadfence();                       // this block's ldj_mol entry visible device-wide
   __syncthreads();
-  // one ticket per molecule (the cooperative instance: its first workgroup's)
-  if (tid == 0) *last = atomicAdd(A.ticket, 1u) == (unsigned)A.num_mols - 1u;
+  if (tid == 0) *last = atomicAdd(A.ticket, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!*last) return;
   __threadfence();                       // acquire: every block's entry
@@ -127,11 +62,9 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       for (int i = 0; i < ENFLOW_SKEW; ++i) __builtin_amdgcn_s_sleep(127);
     }
 #endif
-  const int mol = ENFLOW_COOP ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
-  const int part = ENFLOW_COOP ? (int)(blockIdx.x & 1) : 0;   // the cooperative pair's half
-  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG, mol)) {   // error raised; keep the ticket count
-    if (!REV && A.ticket && part == 0) {
-      if (threadIdx.x == 0) A.ldj_mol[mol] = 0.f;
+  if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) {   // error raised; keep the ticket count
+    if (!REV && A.ticket) {
+      if (threadIdx.x == 0) A.ldj_mol[blockIdx.x] = 0.f;
       ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
     }
     return;
@@ -193,7 +126,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       }
       STAMP(2);
       npairs_layer += tot;
-      if (A.stats != nullptr && tid == 0 && part == 0) {
+      if (A.stats != nullptr && tid == 0) {
         unsigned long long edges = 0;
         for (int a = 0; a < rb; ++a) edges += (unsigned long long)sm.cntrow[r0 + a];
         atomicAdd(&A.stats[0], (unsigned long long)tot);
@@ -209,12 +142,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
           if (wv < (H / 32) * (RB / 32)) nfr.issue(weights_rsrc(Lp, L.total), L, tid_l & 63, wv);
         }
       };
-      edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS, nullptr, nullptr, pre,
-                                         part, ENFLOW_COOP ? 2 : 1);
-#if ENFLOW_COOP
-      static_assert(!BLOCKED, "the cooperative instance runs whole-molecule images");
-      coop_exchange(sm, A, mol, part, n, A.epoch + (uint32_t)it + 1u);
-#endif
+      edge_tiles<H, NMAX, RB, PREC, VAR>(sm, Lp, L, Ml, nf, tid_l, r0, rb, true STAMP_PASS, nullptr, nullptr, pre);
       if constexpr (BLOCKED) {   // blocks with more pairs than the buffer: further passes
         constexpr int PC = Smem<H, NMAX, RB>::PC;
         for (int p0 = PC; p0 < tot; p0 += PC) {
@@ -269,7 +197,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       block_pass(0, n);   // the whole molecule in one pass
     }
     if (!REV && A.tape != nullptr && tid == 0 && A.pair_counts != nullptr)
-      A.pair_counts[(size_t)l * A.num_mols + mol] = npairs_layer;
+      A.pair_counts[(size_t)l * A.num_mols + blockIdx.x] = npairs_layer;
     for (int a = tid; a < n; a += BLOCK) {
       const float q = sm.Q[a];
       const float eq = expf(q);
@@ -323,7 +251,6 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   // (ENFLOW_ERR_RANGE) instead of returned silently; the f32 path returns
   // whatever the arithmetic gives, as the reference does.
   bool bad = false;
-  if (part == 0) {
   for (int e = tid; e < n * 3; e += BLOCK) {
     const float p = sm.pos[e], v = sm.vel[e];
     A.pos[(size_t)M.a0 * 3 + e] = p;
@@ -339,15 +266,14 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   }
   if (!REV) {
     const float s = block_sum(sm, ldj);
-    if (tid == 0) A.ldj_mol[mol] = s;
+    if (tid == 0) A.ldj_mol[blockIdx.x] = s;
     bad |= tid == 0 && !__builtin_isfinite(s);
   }
   if constexpr (PREC != PREC_F32) {
     if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
   }
-  }
   if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
-  if (!REV && A.ticket && part == 0) ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
+  if (!REV && A.ticket) ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
   STAMP(7);
   STAMP_FLUSH
 }

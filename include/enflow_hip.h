@@ -41,8 +41,6 @@ extern "C" {
                                           f16x3) a GEMM operand of a molecule / row block was
                                           entirely below 2^-7 in magnitude (its fp16 lo parts
                                           subnormal): rerun with ENFLOW_PREC_F32 */
-#define ENFLOW_ERR_INTERNAL         16 /* (ABI 12) the cooperative instance's two workgroups of a
-                                          molecule did not meet within the wait bound: no result */
 
 /* Precision of the flow's two H x H edge GEMMs (edge_nn.2, coord_nn.0); all
  * other arithmetic is fp32 in every mode.  See DESIGN.md for the error model. */
@@ -65,8 +63,7 @@ extern "C" {
  * kinds (enflow_pack_egcl_act_f32, the ArgMax activation trailer), node_nf up to 16 in
  * libenflow_hip_nf16.so; 11: ENFLOW_ERR_RANGE also flags an f16x3 GEMM operand that is entirely
  * small, ENFLOW_BWD_F32 -- the fp32-GEMM backward for a tape recorded by an ENFLOW_PREC_F32
- * forward); 12: the cooperative instance of the fused flow kernel (two workgroups per molecule
- * for batches of at most half the CU count), enflow_set_coop_max, ENFLOW_ERR_INTERNAL). */
+ * forward). */
 int enflow_abi_version(void);
 
 /* Batches of <= 32-atom molecules with at most this many molecules run the
@@ -79,18 +76,6 @@ int enflow_abi_version(void);
  * one in effect on the current device. */
 int enflow_set_latency_threshold(int max_mols);
 int enflow_latency_threshold(void);
-
-/* Batches of <= 32-atom molecules with at most this many molecules (and at most
- * the latency threshold) run the cooperative instance: two 8-wave workgroups
- * per molecule on two CUs, each taking half of every layer's edge tiles, the
- * pair's aggregate rows swapped once per layer through device memory.  Default
- * (-1): half the current device's CU count (0 without cooperative launch
- * support); 0: never.  Layers with constructor variants / non-SiLU act_fn and
- * training forwards (tape) use the other instances.  Replaces no reference
- * interface (the strong-scaling knob, as above).  Returns the previous setting;
- * enflow_coop_max() the value in effect. */
-int enflow_set_coop_max(int max_mols);
-int enflow_coop_max(void);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept.  The ABI
  * ships as two builds of the same sources: libenflow_hip.so (node_nf <= 8) and

@@ -415,9 +415,6 @@ def test_kernel_instance_selected(mols, kernel_instance):
         model(Data.from_arrays(b, device=DEV))
     names = set(t.stats)
     want = "lf_flow_kernel<fwd,lat>" if kernel_instance == "8-wave" else "lf_flow_kernel<fwd>"
-    if kernel_instance == "coop":   # two workgroups per molecule while the pairs can all be resident
-        cus = torch.cuda.get_device_properties(DEV).multi_processor_count
-        want = "lf_flow_kernel<fwd,coop>" if 2 * mols <= cus else "lf_flow_kernel<fwd,lat>"
     print(f"[{kernel_instance}] {mols} molecules ran {sorted(names)}")
     assert want in names, names
 

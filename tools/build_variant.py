@@ -28,7 +28,7 @@ def main():
     from enflow_amd.build import obj_dir
     odir = obj_dir(LIB)   # the product build's objects (enflow_amd/build/libenflow_hip_so)
     others = [os.path.join(odir, s + ".o") for s in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip",
-                                                     "enflow_timing.hip", "enflow_latency.hip", "enflow_coop.hip") if s != tu]
+                                                     "enflow_timing.hip", "enflow_latency.hip") if s != tu]
     so = os.path.join(out_dir, f"libenflow_{name}.so")
     subprocess.run(["hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", so, obj] + others, check=True)
     print(so)

@@ -28,11 +28,8 @@ def main():
     t1 = None
     for n in (1, 2, 4, 8):
         m1 = 1024 // n
-        for mode, thr, coop in (("auto", -1, -1), ("no cooperative", -1, 0), ("4-wave only", 0, 0)):
-            if coop == 0 and m1 > 2 * 128 and mode == "no cooperative":
-                continue
+        for mode, thr in (("auto", -1), ("4-wave only", 0)):
             L.enflow_set_latency_threshold(thr)
-            L.enflow_set_coop_max(coop)
             run = bench.FlowRunner(model, bench.batch_tensors(bench.sub_batch(g, 0, m1), dev), bench.ATOMS, False,
                                    dev, torch.Generator(dev).manual_seed(0))
             el = bench.timed(run.step, 40, 30, None, dev)
@@ -41,14 +38,11 @@ def main():
             if n == 1 and mode == "auto":
                 t1 = ms
             out["rows"].append({"ranks": n, "kernel": mode, "molecules_per_rank": m1,
-                                "latency_instance": m1 <= L.enflow_latency_threshold(),
-                                "cooperative_instance": m1 <= min(L.enflow_coop_max(), L.enflow_latency_threshold()),
-                                "ms_per_step": ms,
+                                "latency_instance": m1 <= L.enflow_latency_threshold(), "ms_per_step": ms,
                                 "global_molecule_transforms_per_s": 1024 / (ms * 1e-3),
                                 "strong_scaling_efficiency": t1 / (n * ms)})
             print(json.dumps(out["rows"][-1]), file=sys.stderr, flush=True)
     L.enflow_set_latency_threshold(-1)
-    L.enflow_set_coop_max(-1)
     print(json.dumps(out, indent=1))
 
 
