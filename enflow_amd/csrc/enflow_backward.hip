@@ -177,6 +177,11 @@ struct BwdArgs {
   // standalone EGCL.forward backward (enflow_egcl_backward_f32): adjoints of the
   // network outputs Q [A], F [A][3], G [A][nf] given directly (NULL: the flow's
   // leapfrog adjoint); the layer-input adjoints then start at zero
+  // fused path: the forward taped the layer's pair words / row counts (TapeLayout::pairs,
+  // cnt) and its pair counts ([num_mols], this layer's): loaded, not rebuilt (0: rebuild,
+  // the standalone EGCL backward's tape)
+  const int32_t* pair_counts_l;
+  int tape_pairs;
   const float* eg_dQ;
   const float* eg_dF;
   const float* eg_dG;
@@ -199,6 +204,9 @@ struct BwdArgs {
 // within 1 % of 2 (profiles/r04/r04l_ab_train_split_once_and_ring_depth.txt)
 #ifndef ENFLOW_BWD_X3_DEPTH
 #define ENFLOW_BWD_X3_DEPTH 2
+#endif
+#ifndef ENFLOW_BWD_RL
+#define ENFLOW_BWD_RL 2   // when GEMM3 re-reads the parked pre_e rows (A/B knob, see the tile; r04u: 2 -0.8 %)
 #endif
 // per-tile operand maxima (BwdArgs::tmax): X / DY of edge_nn.0, edge_nn.2, coord_nn.0
 enum { TMX_XIN = 0, TMX_DP0 = 1, TMX_X1 = 2, TMX_DPE = 3, TMX_MSG = 4, TMX_DPC = 5, TMX_W = 8 };
@@ -687,7 +695,18 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       if (2 * nf + 1 > 32) sb.wrad[k] = Rp[R.We1 + k * (2 * nf + 1) + 2 * nf];
     }
   }
-  if constexpr (!BIG) build_pairs(sm, M, tid);   // same positions as the forward -> same pairs (reuses sm.u)
+  if constexpr (!BIG) {
+    if (B.tape_pairs) {   // the forward's list of this layer (same positions -> the same pairs)
+      const int np = B.pair_counts_l[m];
+      const float* tp = B.tape + T.pairs + la * TAPE_PAIR_CAP;
+      for (int e = tid; e < np; e += BLOCK) sm.pairs[e] = __float_as_uint(tp[e]);
+      for (int a = tid; a < n; a += BLOCK) sm.cntrow[a] = __float_as_int(B.tape[T.cnt + la + a]);
+      if (tid == 0) sm.npairs = np;
+      __syncthreads();
+    } else {
+      build_pairs(sm, M, tid);   // same positions as the forward -> same pairs (reuses sm.u)
+    }
+  }
 
   STAMP(3);
   // ---- edge chain backward, one 32-pair tile per wave step (egcl.py:57-74, 76-89)
@@ -906,6 +925,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) ev[t] = (f32x16)0.f;
       chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(W, L.we2f, L.we2x, L.we2b, x0, ev, lane, nofill);
+      STAMP(18);
 #pragma unroll
       for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -942,6 +962,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) cv[t] = (f32x16)0.f;
       chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(W, L.wc1f, L.wc1x, L.wc1b, ev, cv, lane, nofill);
+      STAMP(19);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // pre_e rows landed
       float part = 0.f;
       float mdz = 0.f;   // max |silu'(c)| (DY of coord_nn.0 = d phi * silu'(c))
@@ -995,13 +1016,27 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       for (int t = 0; t < NT; ++t) ae[t] = (f32x16)0.f;
       float sc3 = 1.f;
       if constexpr (PREC == PREC_F16X3) sc3 = tile_pow2_scale(cv);   // cv already stored unscaled
-      // pre_e rows re-read during the chain, a quad per step, as the B operand tiles retire
+      STAMP(16);
+      // pre_e rows re-read (ENFLOW_BWD_RL 0: during the chain, a quad per step;
+      // 1: all before the chain; 2: all after it)
       f32x16 rl[NT];
-      chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(WB, LB.wc1T, LB.wc1Tx, 0, cv, ae, lane, [&](int i) {
+      auto rl_load = [&](int i) {
         const int t = i >> 2, g4 = i & 3;
 #pragma unroll
         for (int u = 0; u < 4; ++u) rl[t][4 * g4 + u] = bload(rpe, lob, tsb + ((32 * t + 8 * g4 + u) << 7));
+      };
+      if constexpr (ENFLOW_BWD_RL == 1) {
+#pragma unroll
+        for (int i = 0; i < 4 * NT; ++i) rl_load(i);
+      }
+      chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(WB, LB.wc1T, LB.wc1Tx, 0, cv, ae, lane, [&](int i) {
+        if constexpr (ENFLOW_BWD_RL == 0) rl_load(i);
       });
+      if constexpr (ENFLOW_BWD_RL == 2) {
+#pragma unroll
+        for (int i = 0; i < 4 * NT; ++i) rl_load(i);
+      }
+      STAMP(17);
       const float u3 = inv2 * sc3;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
@@ -2763,6 +2798,8 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     A.su = wb + Wl.su; A.au = wb + Wl.au; A.sn = wb + Wl.sn; A.an = wb + Wl.an;
     A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
     A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
+    A.pair_counts_l = pair_counts + (size_t)l * num_mols;
+    A.tape_pairs = eg_dQ == nullptr && !getenv("ENFLOW_BWD_REBUILD_PAIRS");
     if (f32b) {   // generic (VAR) instance: any flags / act_fn
 #define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true, PREC_F32>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);

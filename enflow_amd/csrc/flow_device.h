@@ -194,7 +194,12 @@ __host__ __device__ inline EgclBwdLayout egcl_bwd_layout(int H) {
 
 // Training tape written by the forward (one block per quantity, layer-major):
 // per layer l and atom a the layer INPUT state and what the backward re-reads.
-struct TapeLayout { size_t hx, g, pos, vel, q, total; int ldhx; };
+struct TapeLayout { size_t hx, g, pos, vel, q, pairs, cnt, total; int ldhx; };
+// the fused forward's pair words of a layer, per molecule a slab of TAPE_PAIR_CAP
+// words per atom from its first atom's (a molecule of n <= 64 atoms has at most
+// n (n - 1) unique pairs), and the per-row edge counts: the layer backward reads
+// them instead of rebuilding the neighbour list from the same positions
+constexpr int TAPE_PAIR_CAP = 63;
 __host__ __device__ inline TapeLayout tape_layout(int num_atoms, int nf, int H, int n_layers) {
   TapeLayout T;
   const size_t LA = (size_t)num_atoms * n_layers;
@@ -205,6 +210,8 @@ __host__ __device__ inline TapeLayout tape_layout(int num_atoms, int nf, int H, 
   T.pos = o; o += LA * 3;
   T.vel = o; o += LA * 3;
   T.q = o; o += LA;               // Q = vel_scaling_nn(h)
+  T.pairs = o; o += LA * TAPE_PAIR_CAP;   // [l][a0 .. a0 + n)'s slab: pair words (uint32 bits)
+  T.cnt = o; o += LA;             // [l][a]: edges of row a (int32 bits)
   T.total = o;
   return T;
 }
@@ -1147,7 +1154,7 @@ __device__ __forceinline__ void bias_silu(f32x16 (&X)[NT], const float* __restri
 // product library): per phase, the summed shader-clock cycles of wave 0 of
 // every workgroup, measured between the phase's enclosing barriers.
 #if defined(ENFLOW_STAMPS) || (defined(ENFLOW_STAMPS_BWD) && defined(ENFLOW_BACKWARD_TU))
-#define NSTAMP 16
+#define NSTAMP 20
 __device__ unsigned long long enflow_stamp_acc[NSTAMP];
 #define STAMP_DECL unsigned long long st_prev = __builtin_amdgcn_s_memtime(), st_acc[NSTAMP] = {0};
 #define STAMP_ARGS , unsigned long long& st_prev, unsigned long long (&st_acc)[NSTAMP]

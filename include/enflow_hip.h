@@ -180,7 +180,10 @@ int enflow_pack_argmax_f32(const float* raw, int hidden_nf, int node_nf,
  *                        += reference edge-list entries, summed over layers
  *   tape               : optional (NULL = inference); training tape of
  *                        enflow_lf_tape_size floats: per layer the layer-input
- *                        state, message sums and Q, read by enflow_lf_backward_f32
+ *                        state, message sums and Q, and (molecules of <= 64 atoms)
+ *                        the layer's neighbour list -- pair words and per-row edge
+ *                        counts, so the backward does not rebuild it -- read by
+ *                        enflow_lf_backward_f32 (the layout is the library's own)
  *   pair_counts        : [n_layers][num_mols] unique pairs per layer (required
  *                        with tape)
  *   gemm_precision     : ENFLOW_PREC_* (edge_nn.2 / coord_nn.0 GEMMs)

@@ -90,7 +90,8 @@ def test_argument_errors_launch_nothing():
 def test_backward_sizes_and_argument_errors():
     L = _lib.lib()
     A, M, nf, H, nl = 22 * 4, 4, 5, 128, 8
-    assert L.enflow_lf_tape_size(A, nf, H, nl) == nl * A * (nf + H + nf + 3 + 3 + 1)
+    # per layer and atom: h | message sums, g, pos, vel, Q, the pair-word slab (63) and the row's edge count
+    assert L.enflow_lf_tape_size(A, nf, H, nl) == nl * A * (nf + H + nf + 3 + 3 + 1 + 63 + 1)
     assert L.enflow_egcl_bwd_packed_size(H, nf) >= 2 * H * H
     assert L.enflow_egcl_bwd_packed_size(96, nf) == -1
     assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480) > 4 * 480 * 5 * H * 4

@@ -46,7 +46,7 @@ def main():
     ldj_mol = torch.empty(mols, device=dev)
     ldj = torch.empty(1, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 32)()
     for rep in range(3):
         for k in work:
             work[k].copy_(inp[k])

@@ -13,7 +13,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PHASES = ["load", "leapfrog", "node", "pairs", "tile:setup+xin+gemm0", "tile:epi0", "tile:gemm1+epi1",
           "tile:gemm2+epi2+phi", "tile:gemm3", "tile:wait+epi3", "tile:gemm4", "tile:epi4", "tile:gemm5",
-          "atomics+barrier", "writeback", "-"]
+          "atomics+barrier", "writeback", "-", "tile:gemm3 scale(cv)", "tile:gemm3 chain", "tile:gemm1 chain",
+          "tile:gemm2 chain"]
 
 
 def main():
@@ -39,7 +40,7 @@ def main():
     nll = Alchemical_NLL(kBT=default_kBT(), softening=0.1)
     base = Data.from_arrays(b, device=dev)
     noise = torch.randn_like(base.h)
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 32)()
     for rep in range(3):
         model.zero_grad(set_to_none=True)
         out, ldj = model(base._replace(), noise=noise)
