@@ -2799,7 +2799,8 @@ static int lf_backward_impl(int num_mols, int num_atoms, int max_mol_atoms, int 
     A.aq = wb + Wl.aq; A.agr = wb + Wl.agr; A.err = err_flag;
     A.eg_dQ = eg_dQ; A.eg_dF = eg_dF; A.eg_dG = eg_dG;
     A.pair_counts_l = pair_counts + (size_t)l * num_mols;
-    A.tape_pairs = eg_dQ == nullptr && !getenv("ENFLOW_BWD_REBUILD_PAIRS");
+    // the forward's 64-atom instance tapes the list (molecules of 33..64 atoms; see flow_kernel.h)
+    A.tape_pairs = eg_dQ == nullptr && max_mol_atoms > 32 && !getenv("ENFLOW_BWD_REBUILD_PAIRS");
     if (f32b) {   // generic (VAR) instance: any flags / act_fn
 #define CALL(HH, NN) ENFLOW_TIMED("lf_layer_bwd_kernel", st, hipLaunchKernelGGL((lf_layer_bwd_kernel<HH, NN, true, PREC_F32>), dim3(num_mols), dim3(BLOCK), 0, st, A))
       DISPATCH_HN_B(H, max_mol_atoms, CALL);

@@ -180,7 +180,10 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
           A.tape[T.vel + la * 3 + e] = sm.vel[r0 * 3 + e];
         }
         for (int a = tid; a < rb; a += BLOCK) A.tape[T.q + la + a] = sm.Q[r0 + a];
-        if constexpr (!BLOCKED && NMAX <= TAPE_PAIR_CAP + 1) {   // the layer's neighbour list for the backward
+        // the layer's neighbour list for the backward: the 64-atom image only (the
+        // training forward's instance for molecules of 33..64 atoms; the <= 32-atom
+        // instances keep their registers -- their backward rebuilds the list)
+        if constexpr (!BLOCKED && NMAX == TAPE_PAIR_CAP + 1) {
           float* const tp = A.tape + T.pairs + la * TAPE_PAIR_CAP;
           for (int e = tid; e < sm.npairs; e += BLOCK) tp[e] = __uint_as_float(sm.pairs[e]);
           for (int a = tid; a < rb; a += BLOCK) A.tape[T.cnt + la + a] = __int_as_float(sm.cntrow[r0 + a]);
