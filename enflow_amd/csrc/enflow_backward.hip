@@ -1337,6 +1337,9 @@ __device__ __forceinline__ int find_desc(const OuterBatch& ob, int bid) {
 // reduction and runs on VALU.  The bias column (sum of DY) is accumulated by
 // the n-block-0 workgroup from the same LDS image.
 #define OB_ROWS 32
+#ifndef ENFLOW_ATOM_X3
+#define ENFLOW_ATOM_X3 1   // atom-row weight gradients on the F16X3 MFMA (0: fp32 MFMA; A/B knob)
+#endif
 #ifndef ENFLOW_OUTER_X3
 #define ENFLOW_OUTER_X3 1    // pair-row weight gradients on F16X3 MFMA (0: fp32 MFMA)
 #endif
@@ -1436,7 +1439,60 @@ __global__ void __launch_bounds__(256, 2) outer_acc_kernel(OuterBatch ob) {
     const int buf = st & 1;
     if (st + 1 < nst) gload(st + 1);
     if (M > 1) {
-      if (live) {
+      if (live && !TILED && ENFLOW_ATOM_X3) {
+        // atom rows on the F16X3 MFMA (32x32x16, 3 products) instead of 32x32x2 fp32:
+        // each lane gathers its operands' 8 rows per k-step from the row-major stage
+        // (A: rows 16 ks + 8 hh + e of DY column m, B: the same rows of X column n),
+        // a power-of-two scale per stage, wave and operand (max |x| -> [2^12, 2^13))
+        // before the hi / lo split, the stage's sums added with the exact inverse scale
+        float av[2][2][8], bv[2][2][8];
+        float ma = 0.f, mb = 0.f;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const int r = 16 * ks + 8 * hh + e;
+              av[a][ks][e] = sd[buf][r][mh * 64 + a * 32 + j];
+              bv[a][ks][e] = sx[buf][r][nh * 64 + a * 32 + j];
+              if (a == 0 || use_m1) ma = fmaxf(ma, fabsf(av[a][ks][e]));
+              if (a == 0 || use_n1) mb = fmaxf(mb, fabsf(bv[a][ks][e]));
+            }
+        ma = wave_max(ma);
+        mb = wave_max(mb);
+        const int ea = pow2_exp(ma), eb = pow2_exp(mb);
+        const float sa = ldexpf(1.f, ea), sbs = ldexpf(1.f, eb);
+        const float un = ldexpf(ldexpf(1.f, -ea), -eb);
+        f16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            f32x16 xa, xb;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              xa[e] = av[a][ks][e] * sa;
+              xb[e] = bv[a][ks][e] * sbs;
+            }
+            split_f16(xa, 0, ah[a][ks], al[a][ks]);
+            split_f16(xb, 0, bh[a][ks], bl[a][ks]);
+          }
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            if ((a == 1 && !use_m1) || (b == 1 && !use_n1)) continue;
+            f32x16 t = (f32x16)0.f;
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+              t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bh[b][ks], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[a][ks], bl[b][ks], t, 0, 0, 0);
+              t = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[a][ks], bh[b][ks], t, 0, 0, 0);
+            }
+            acc[a][b] += t * un;
+          }
+      } else if (live) {
         if (use_m1 && use_n1) {
 #pragma unroll 4
           for (int s = 0; s < OB_ROWS / 2; ++s) {
