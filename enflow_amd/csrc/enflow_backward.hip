@@ -1317,7 +1317,7 @@ struct OuterBatch {
 #define OA_CHUNK 2048        // pair rows per partial
 #endif
 #ifndef OA_CHUNK_ATOM
-#define OA_CHUNK_ATOM 512    // atom rows per partial (a few hundred workgroups for 64k atoms)
+#define OA_CHUNK_ATOM 256    // atom rows per partial (r04z: 256 -1 % of backward vs 512 on the F16X3 atom-row kernel)
 #endif
 static_assert(OA_CHUNK % 64 == 0 && OA_CHUNK_ATOM % 64 == 0, "partial chunks are whole row stages");
 
