@@ -2126,6 +2126,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_pt
                                                           const float* adj_ldj, float* apre_rows, float* spre_rows,
                                                           float* anet_rows) {
   __shared__ float pre[NMAX][H + 1];
+  __shared__ float spv[NMAX][H + 1];   // act(pre), once per (atom, unit): network.2's input
   __shared__ float net[NMAX][2 * NFMAX];
   __shared__ float anet[NMAX][2 * NFMAX];
   __shared__ float hs[NMAX][NFMAX];
@@ -2142,16 +2143,15 @@ __global__ void __launch_bounds__(BLOCK) argmax_bwd_kernel(const int32_t* mol_pt
     float v = Draw[rb1 + k];
     for (int f = 0; f < nf; ++f) v = fmaf(Draw[rW1 + k * nf + f], hs[a][f], v);
     pre[a][k] = v;
-    spre_rows[(size_t)(a0 + a) * H + k] = am.k == ACT_SILU ? v * sigmoid_f(v) : act_f(am, v);
+    const float sv = am.k == ACT_SILU ? v * sigmoid_f(v) : act_f(am, v);
+    spv[a][k] = sv;
+    spre_rows[(size_t)(a0 + a) * H + k] = sv;
   }
   __syncthreads();
   for (int e = tid; e < n * 2 * nf; e += BLOCK) {
     const int a = e / (2 * nf), o = e - a * 2 * nf;
     float s = Draw[rb2 + o];
-    for (int kk = 0; kk < H; ++kk) {
-      const float p = pre[a][kk];
-      s = fmaf(Draw[rW2 + o * H + kk], am.k == ACT_SILU ? p * sigmoid_f(p) : act_f(am, p), s);
-    }
+    for (int kk = 0; kk < H; ++kk) s = fmaf(Draw[rW2 + o * H + kk], spv[a][kk], s);
     net[a][o] = s;
   }
   __syncthreads();
