@@ -185,8 +185,7 @@ class _FlowFunction(torch.autograd.Function):
             grads += layer_grads(net, grad_layers[li * rstride:(li + 1) * rstride])
         if kind == _lib.DEQUANT_ARGMAX:
             am = flow.dequantize
-            gd, _ = unpad_grads(grad_dq, list(am.named_parameters()), ARGMAX_HDIMS, am.pad_geom(hid))
-            grads += [gd[k].contiguous().to(p.dtype) for k, p in am.named_parameters()]
+            grads += argmax_grads(am, grad_dq, am.pad_geom(hid))
         # d h of the data only exists without a learned dequantiser (z = h + noise)
         gh_in = ah if kind != _lib.DEQUANT_ARGMAX else None
         return (None, None, gh_in, ag, apos, avel) + tuple(grads)
@@ -280,7 +279,17 @@ def layer_grads(net, flat):
     if att:
         ga, _ = unpad_grads(flat[off:], att, EGCL_HDIMS, geom)
         g.update(ga)
-    return [g[name].contiguous().to(p.dtype) for name, p in net.named_parameters()]
+    # act_fn's own parameters (a frozen PReLU slope) get no gradient
+    return [None if name.startswith("act_fn.") else g[name].contiguous().to(p.dtype)
+            for name, p in net.named_parameters()]
+
+
+def argmax_grads(am, flat, geom):
+    """ArgMax's flat gradient split into its parameters, named_parameters() order
+    (None for a frozen PReLU slope, network.1)."""
+    gd, _ = unpad_grads(flat, am.kernel_named(), ARGMAX_HDIMS, geom)
+    return [None if k.startswith("network.1.") else gd[k].contiguous().to(p.dtype)
+            for k, p in am.named_parameters()]
 
 
 class _EGCLFunction(torch.autograd.Function):
@@ -425,7 +434,6 @@ class _ArgMaxFunction(torch.autograd.Function):
             meta["mol_ptr"].numel() - 1, A, meta["max_n"], nf, hid, _lib.ptr(meta["mol_ptr"]), _lib.ptr(h),
             _lib.ptr(raw), _lib.ptr(noise), _lib.ptr(az), _lib.ptr(alq), _lib.ptr(grad), _lib.ptr(ws), wsb,
             _lib.stream_ptr(dev)), "enflow_argmax_backward_f32")
-        gd, _ = unpad_grads(grad, list(am.named_parameters()), ARGMAX_HDIMS, am.pad_geom())
-        grads = [gd[k].contiguous().to(p.dtype) for k, p in am.named_parameters()]
+        grads = argmax_grads(am, grad, am.pad_geom())
         # h is the categorical data (one-hot, argmax.py:13): no gradient is returned for it
         return (None, None, None, None) + tuple(grads)

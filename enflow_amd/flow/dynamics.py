@@ -19,6 +19,7 @@ import warnings
 import torch
 
 from .. import _lib
+from ..nn._act import check_trainable
 from ..nn.argmax import ArgMax
 from ..nn.egcl import EGCL
 from ..nn.floor import Floor
@@ -141,6 +142,10 @@ class LFIntegrator(BaseFlow):
         if nf is not None and nf > _lib.TRAIN_MAX_NODE_NF:
             raise NotImplementedError(f"enflow_amd trains node_nf <= {_lib.TRAIN_MAX_NODE_NF} (got {nf}); "
                                       "inference runs up to 16")
+        for n in self.networks:
+            check_trainable(n.act_fn, "LFIntegrator training")
+        if isinstance(self.dequantize, ArgMax):
+            check_trainable(self.dequantize.network[1], "LFIntegrator training (ArgMax)")
 
     def _needs_grad(self):
         return torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())

@@ -6,14 +6,47 @@ the same instance at every position of the block's MLPs.  The kernels know
 the elementwise torch activations below (ENFLOW_ACT_* in include/enflow_hip.h,
 forward and derivative in flow_device.h act_f / act_d); a layer whose act_fn
 is not SiLU is packed with its code and runs the variant-capable kernels.
+
+nn.PReLU (one learnable slope, the torch default num_parameters=1) runs as
+LeakyReLU with the module's current slope: max(0, x) + a * min(0, x) is
+LeakyReLU(a) for every a, and the slope is read when the layer is packed (the
+packed-weight caches key on every parameter's version, so an optimizer step on
+it re-packs).  The HIP backward has no slope gradient: training with the slope
+trainable is refused (check_trainable); a frozen slope trains.
 """
 from torch import nn
 
 SILU, RELU, LEAKY_RELU, ELU, CELU, SELU, GELU, GELU_TANH, TANH, SIGMOID, SOFTPLUS, MISH, HARDTANH, IDENTITY = range(14)
 
 
+def act_kind(m):
+    """The ENFLOW_ACT_* kind alone (no parameter read: no device sync for PReLU)."""
+    if isinstance(m, nn.PReLU):
+        _check_prelu(m)
+        return LEAKY_RELU
+    return act_code(m)[0]
+
+
+def _check_prelu(m):
+    if m.weight.numel() != 1:
+        raise NotImplementedError(f"enflow_amd kernels implement PReLU with one slope (num_parameters=1), "
+                                  f"got {m.weight.numel()}")
+
+
+def check_trainable(m, where):
+    """Refuse a differentiable call while act_fn has trainable parameters (the
+    HIP backward differentiates the Linear layers, not the activation)."""
+    if any(p.requires_grad for p in m.parameters()):
+        raise NotImplementedError(
+            f"{where}: the HIP backward has no gradient for the parameters of act_fn {type(m).__name__}; "
+            "freeze them (requires_grad_(False)) to train the rest, or run under torch.no_grad()")
+
+
 def act_code(m):
     """(kind, p0, p1) of an activation module; NotImplementedError otherwise."""
+    if isinstance(m, nn.PReLU):
+        _check_prelu(m)
+        return LEAKY_RELU, float(m.weight.detach().reshape(())), 0.0
     if isinstance(m, nn.SiLU):
         return SILU, 0.0, 0.0
     if isinstance(m, nn.ReLU):
@@ -47,7 +80,7 @@ def act_code(m):
 
 def supported(m):
     try:
-        act_code(m)
+        act_kind(m)
         return True
     except NotImplementedError:
         return False

@@ -10,7 +10,7 @@ from torch import nn
 
 from .. import _lib
 from ..utils.helpers import one_hot, mol_ptr_from_counts
-from ._act import SILU, act_code
+from ._act import SILU, act_code, act_kind, check_trainable
 from ._pad import ARGMAX_HDIMS, Geom, flat_padded, kernel_hidden
 
 
@@ -34,7 +34,7 @@ class ArgMax(nn.Module):
         width = width or self.kernel_hidden
         if width is None or width < self.hidden_nf:
             raise NotImplementedError(f"ArgMax hidden_nf {self.hidden_nf} past the kernel width {width}")
-        flat = flat_padded(list(self.named_parameters()), ARGMAX_HDIMS, self.pad_geom(width), device)
+        flat = flat_padded(self.kernel_named(), ARGMAX_HDIMS, self.pad_geom(width), device)
         # ABI 10: [act kind, p0, p1, 0] of network.1 after the parameters (argmax.py:7);
         # the device copy is cached (a host-to-device copy per call would stall the
         # stream once per training step)
@@ -46,13 +46,18 @@ class ArgMax(nn.Module):
             self._act_trailer = trailer = (key, t)
         return torch.cat([flat, trailer[1]])
 
+    def kernel_named(self):
+        """(name, parameter) of the two Linear layers (a PReLU slope, network.1,
+        travels in the act code)."""
+        return [(k, p) for k, p in self.named_parameters() if not k.startswith("network.1.")]
+
     def act(self):
         """(kind, p0, p1) of the network's activation (ENFLOW_ACT_*)."""
         return act_code(self.network[1])
 
     def generic_act(self):
         """True if the activation is not SiLU (the flow then runs its variant-capable kernels)."""
-        return self.act()[0] != SILU
+        return act_kind(self.network[1]) != SILU
 
     def pad_geom(self, width=None):
         nf = self.node_nf
@@ -112,6 +117,7 @@ class ArgMax(nn.Module):
                else noise.to(device=dev, dtype=torch.float32).contiguous())
         params = list(self.parameters())
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            check_trainable(self.network[1], "ArgMax.forward")
             from ..flow._train import _ArgMaxFunction
             meta = self._meta(h.shape[0], N, dev, _lib.TRAIN_MAX_ATOMS)
             z, lq = _ArgMaxFunction.apply(self, meta, h, eps, *params)

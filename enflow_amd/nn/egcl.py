@@ -12,7 +12,7 @@ from torch import nn
 
 from .. import _lib
 from ..data.base import Edges
-from ._act import SILU, act_code, supported as act_supported
+from ._act import SILU, act_code, act_kind, check_trainable, supported as act_supported
 from ._pad import EGCL_HDIMS, Geom, flat_padded, kernel_hidden
 
 
@@ -67,8 +67,8 @@ class EGCL(nn.Module):
     def hip_supported(self):
         """The HIP kernels implement every constructor flag of the reference
         (attention, norm_diff, tanh; ``clamp`` is stored and unused there too)
-        with the activations of nn/_act.py (SiLU, ReLU, LeakyReLU, ELU, CELU, SELU,
-        GELU, Tanh, Sigmoid, Softplus, Mish, Hardtanh / ReLU6, Identity),
+        with the activations of nn/_act.py (SiLU, ReLU, LeakyReLU, PReLU, ELU, CELU,
+        SELU, GELU, Tanh, Sigmoid, Softplus, Mish, Hardtanh / ReLU6, Identity),
         input_nf and output_nf <= 16 and any hidden_nf
         <= 128 (hidden 32 / 64 / 128 and one feature width compiled, other
         shapes zero-padded)."""
@@ -88,7 +88,7 @@ class EGCL(nn.Module):
     def variant_flags(self):
         """ENFLOW_EGCL_* flags of this layer's constructor variants (0 = defaults)."""
         return ((_lib.EGCL_ATTENTION if self.attention else 0) | (_lib.EGCL_NORM_DIFF if self.norm_diff else 0)
-                | (_lib.EGCL_TANH if self.tanh else 0) | (_lib.EGCL_ACT if self.act()[0] != SILU else 0))
+                | (_lib.EGCL_TANH if self.tanh else 0) | (_lib.EGCL_ACT if act_kind(self.act_fn) != SILU else 0))
 
     def act(self):
         """(kind, p0, p1) of act_fn (ENFLOW_ACT_*)."""
@@ -96,8 +96,9 @@ class EGCL(nn.Module):
 
     def raw_named(self):
         """(name, parameter) in the default-flag named_parameters() order the C
-        ABI expects (att_nn, present with attention=True, travels separately)."""
-        return [(k, p) for k, p in self.named_parameters() if not k.startswith("att_nn.")]
+        ABI expects (att_nn, present with attention=True, travels separately;
+        a PReLU slope, registered first as act_fn.weight, travels in the act code)."""
+        return [(k, p) for k, p in self.named_parameters() if not k.startswith(("att_nn.", "act_fn."))]
 
     def raw_parameters(self):
         return [p for _, p in self.raw_named()]
@@ -205,6 +206,7 @@ class EGCL(nn.Module):
             if self.kernel_nf > _lib.TRAIN_MAX_NODE_NF:
                 raise NotImplementedError(f"enflow_amd differentiates EGCL up to node_nf {_lib.TRAIN_MAX_NODE_NF} "
                                           "(inference runs up to 16); call it under torch.no_grad()")
+            check_trainable(self.act_fn, "EGCL.forward")
             from ..flow._train import _EGCLFunction
             q, f, g = _EGCLFunction.apply(self, meta, h, edges.pos, *params)
         else:

@@ -261,17 +261,56 @@ def test_activation_codes_and_variant_flags():
     assert act_code(nn.ReLU6()) == (12, 0.0, 6.0)
     assert act_code(nn.GELU(approximate="tanh"))[0] == 7
     assert act_code(nn.Softplus(2.0, 10.0)) == (10, 2.0, 10.0)
+    assert act_code(nn.PReLU(init=0.125)) == (2, 0.125, 0.0)   # LeakyReLU with the module's slope
     with pytest.raises(NotImplementedError):
-        act_code(nn.PReLU())
+        act_code(nn.PReLU(num_parameters=3))
+    with pytest.raises(NotImplementedError):
+        act_code(nn.Hardswish())
     assert EGCL(5, 5, 32).variant_flags() == 0
     assert EGCL(5, 5, 32, act_fn=nn.Tanh()).variant_flags() == _lib.EGCL_ACT
     assert EGCL(5, 5, 32, act_fn=nn.Tanh()).hip_supported() in (True, False)   # needs only the library
-    assert not EGCL(5, 5, 32, act_fn=nn.PReLU()).hip_supported()
+    assert not EGCL(5, 5, 32, act_fn=nn.Hardswish()).hip_supported()
+    assert not EGCL(5, 5, 32, act_fn=nn.PReLU(3)).hip_supported()
     am = ArgMax(5, 32, act_fn=nn.ELU(0.5))
     raw = am.kernel_raw("cpu")
     assert raw.numel() == sum(p.numel() for p in am.parameters()) + 4
     assert raw[-4:].tolist() == [3.0, 0.5, 0.0, 0.0]
     assert am.generic_act() and not ArgMax(5, 32).generic_act()
+
+
+def test_prelu_slope_travels_in_the_act_code():
+    """PReLU (one slope): the slope is not a kernel weight (raw vectors as the
+    SiLU layer's), it is the act code's p0; its gradient slot is None and a
+    trainable slope is refused on the differentiable paths."""
+    from torch import nn
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.nn._act import check_trainable
+    from enflow_amd.flow._train import layer_grads, argmax_grads
+    torch.manual_seed(0)
+    ref = EGCL(5, 5, 32)
+    torch.manual_seed(0)
+    act = nn.PReLU(init=0.2)
+    net = EGCL(5, 5, 32, act_fn=act)
+    names = [k for k, _ in net.named_parameters()]
+    assert names[0] == "act_fn.weight" and [k for k, _ in net.raw_named()] == [k for k, _ in ref.raw_named()]
+    assert torch.equal(net.kernel_raw("cpu"), ref.kernel_raw("cpu"))   # same init stream, slope excluded
+    assert net.act() == (2, pytest.approx(0.2), 0.0) and net.variant_flags() == _lib.EGCL_ACT
+    with torch.no_grad():
+        act.weight.fill_(-0.5)
+    assert net.act()[1] == -0.5
+    flat = torch.arange(ref.kernel_raw("cpu").numel() + 33, dtype=torch.float32)
+    gl = layer_grads(net, flat)
+    assert gl[0] is None and all(torch.equal(a, b) for a, b in zip(gl[1:], layer_grads(ref, flat)))
+    am = ArgMax(5, 32, act_fn=nn.PReLU(init=0.3))
+    raw = am.kernel_raw("cpu")
+    assert raw.numel() == sum(p.numel() for p in am.parameters()) - 1 + 4
+    assert raw[-4:].tolist() == [2.0, pytest.approx(0.3), 0.0, 0.0]
+    ga = argmax_grads(am, raw[:-4], am.pad_geom())
+    assert [g is None for g in ga] == [k.startswith("network.1.") for k, _ in am.named_parameters()]
+    with pytest.raises(NotImplementedError, match="freeze"):
+        check_trainable(act, "test")
+    act.weight.requires_grad_(False)
+    check_trainable(act, "test")
 
 
 def test_asm_hazard_scan_gate_on_synthetic_assembly(tmp_path):
