@@ -139,3 +139,31 @@ def test_trainable_prelu_is_refused():
     with torch.no_grad():   # inference runs with the slope trainable
         net(d.h, d.edges)
         am(d.h)
+
+
+@pytest.mark.parametrize("case", ["large_256_atoms", "nf12_library"])
+def test_prelu_equals_leaky_on_the_other_paths(case):
+    """The large-system kernels (> the fused kernels' 64-atom image) and the
+    16-feature library take the same act code: EGCL forward and a 2-layer flow
+    bitwise equal to the LeakyReLU-built modules."""
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules
+    sizes, nf, chain = ([256, 40], 5, True) if case == "large_256_atoms" else ([22, 17, 30], 12, False)
+    b = make_molecules(len(sizes), sizes, nf=nf, seed=7, chain=chain)
+    res = []
+    for act in (lambda: nn.PReLU(init=0.15), lambda: nn.LeakyReLU(0.15)):
+        torch.manual_seed(8)
+        nets = [EGCL(nf, nf, 64, act_fn=act()) for _ in range(2)]
+        am = ArgMax(nf, 64, act_fn=act())
+        model = LFIntegrator(nets, am, dt=0.05).to(DEV)
+        d = Data.from_arrays(b, device=DEV)
+        with torch.no_grad():
+            q, f, g = model.networks[0](d.h, d.edges)
+            eps = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(9))
+            o, ldj = model(d, noise=eps)
+        res.append([t.cpu().numpy().copy() for t in (q, f, g, o.h, o.g, o.pos, o.vel)] + [np.array([float(ldj)])])
+    for i, (x, y) in enumerate(zip(*res)):
+        np.testing.assert_array_equal(x, y, err_msg=str(i))
+    print(f"{case}: PReLU == LeakyReLU (EGCL forward, flow forward, log|detJ|)")
