@@ -768,6 +768,18 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
     const int TT = (P + 31) >> 5;
     const int tpw = (TT + WAVES - 1) / WAVES;
     const int t0 = w * tpw, t1 = min(TT, t0 + tpw);
+    // GEMM0's first-k-step weight fragments (the same for every tile): loaded
+    // here, re-requested by each tile's second GEMM0 and carried into the next
+    // tile's first, which then waits on no load
+    f32x4 cfh[NT], cfl[NT];
+    if constexpr (PREC == PREC_F16X3) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int so = (L.we1x + (t * KS0MAX) * 512) * 4;
+        cfh[t] = bload4(W, lane * 32, so);
+        cfl[t] = bload4(W, lane * 32 + 16, so);
+      }
+    }
     for (int tile = t0; tile < t1; ++tile) {
       const int p = tile * 32 + j;
       const bool valid = p < P;
@@ -841,19 +853,22 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       // tile (here, and again for silu'(pre0) after GEMM4) instead of parking pre0
       // in HBM: the same instruction sequence on the same operands, so both are
       // bitwise the forward's pre0 (outer_x3_kernel recomputes it from xin, too)
-      auto gemm0 = [&](f32x16 (&x0)[NT]) {
+      auto gemm0 = [&](f32x16 (&x0)[NT], bool fresh) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) x0[t] = (f32x16)0.f;
       if constexpr (PREC == PREC_F16X3) {
         const int ks_n = gemm0_ksteps(nf), nch = gemm0_nch(nf);
-        // the first k-step's fragments requested before the operand build, so
-        // their L2 round trip overlaps it (they are the only loads the chain waits on)
-        f32x4 fh0[NT], fl0[NT];
+        // the first k-step's fragments: carried (cfh / cfl), or requested before
+        // the operand build so their L2 round trip overlaps it
+        auto& fh0 = cfh;
+        auto& fl0 = cfl;
+        if (fresh) {
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-          const int so = (L.we1x + (t * KS0MAX) * 512) * 4;
-          fh0[t] = bload4(W, lane * 32, so);
-          fl0[t] = bload4(W, lane * 32 + 16, so);
+          for (int t = 0; t < NT; ++t) {
+            const int so = (L.we1x + (t * KS0MAX) * 512) * 4;
+            fh0[t] = bload4(W, lane * 32, so);
+            fl0[t] = bload4(W, lane * 32 + 16, so);
+          }
         }
         for (int ks = 0; ks < ks_n; ++ks) {   // k order gemm0_col (as the forward)
           f32x16 in;
@@ -905,7 +920,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       }
       };
       f32x16 x0[NT];
-      gemm0(x0);
+      gemm0(x0, false);
       STAMP(4);
       // x1 = silu(pre0) (kept: B operand of GEMM1)
 #pragma unroll
@@ -1086,7 +1101,7 @@ __global__ void __launch_bounds__(BLOCK, 2) lf_layer_bwd_kernel(BwdArgs B) {
       if constexpr (PREC == PREC_F16X3) sc4 = tile_pow2_scale(ae, mdpe);   // ae already stored unscaled
       chain_prec_fill<PREC, NT, 1, ENFLOW_BWD_X3_DEPTH>(WB, LB.we2T, LB.we2Tx, 0, ae, ax, lane, nofill);
       STAMP(10);
-      gemm0(rl);   // pre0 again (bitwise the first pass's)
+      gemm0(rl, true);   // pre0 again (bitwise the first pass's)
       const float u4 = inv1 * sc4;
 #pragma unroll
       for (int t = 0; t < NT; ++t)
