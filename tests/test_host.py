@@ -342,3 +342,17 @@ def test_product_build_refuses_diagnostic_switches():
     from enflow_amd import build
     with pytest.raises(ValueError):
         build.build(out=build.OUT, defines=("ENFLOW_STAMPS",))
+
+
+def test_committed_pmc_traffic_matches_the_built_library():
+    """bench.py reports roofline.traffic only from a PMC summary collected on
+    this exact library build (hash match); the committed evidence must cover
+    the library the sources build (builds are reproducible)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    traffic, src = bench.load_traffic(bench.workload_name("forward"), bench.lib_sha())
+    assert traffic is not None and traffic > 0, f"no profiles/**/*pmc_traffic.json for lib {bench.lib_sha()}"
+    print("traffic", traffic, "from", src)
