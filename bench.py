@@ -24,6 +24,7 @@ and the CPU oracle timed on a bounded sample over the host's cores
 """
 import argparse
 import hashlib
+import struct
 import json
 import os
 import subprocess
@@ -150,7 +151,51 @@ def lib_sha():
     return h.hexdigest()[:16]
 
 
-def load_traffic(workload, sha):
+def _elf_sections(d, base=0):
+    """{name: (offset, size)} of an ELF64 image at d[base:]."""
+    shoff = struct.unpack_from("<Q", d, base + 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", d, base + 0x3A)
+    raw = []
+    for i in range(shnum):
+        name, _typ, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", d, base + shoff + i * shentsize)
+        raw.append((name, off, size))
+    stroff = base + raw[shstrndx][1]
+    out = {}
+    for name, off, size in raw:
+        e = d.index(b"\0", stroff + name)
+        out[d[stroff + name:e].decode()] = (base + off, size)
+    return out
+
+
+def code_sha(path=None):
+    """Hash of the device code the library runs: the .text of every gfx950 code
+    object in its .hip_fatbin (offload bundles in order).  Unlike a hash of the
+    whole .so it does not move with the build directory (hipcc's path-derived
+    __hip_cuid_* symbols live outside .text), so a rebuild of the same sources
+    anywhere keeps roofline.traffic's PMC summary."""
+    from enflow_amd import _lib
+    with open(path or _lib.LIB_PATH, "rb") as fh:
+        d = fh.read()
+    off, size = _elf_sections(d)[".hip_fatbin"]
+    fat = d[off:off + size]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    h = hashlib.sha256()
+    pos = fat.find(magic)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", fat, pos + len(magic))[0]
+        q = pos + len(magic) + 8
+        for _ in range(n):
+            eoff, esize, tlen = struct.unpack_from("<QQQ", fat, q)
+            triple = fat[q + 24:q + 24 + tlen].decode()
+            q += 24 + tlen
+            if "gfx950" in triple and esize > 0:
+                t_off, t_size = _elf_sections(fat, pos + eoff)[".text"]
+                h.update(fat[t_off:t_off + t_size])
+        pos = fat.find(magic, q)
+    return h.hexdigest()[:16]
+
+
+def load_traffic(workload, sha, code=None):
     """HBM bytes per flow-kernel launch from a committed rocprofv3 PMC summary
     (profiles/*pmc_traffic.json, written by profiles/collect_pmc.py) -- only if
     it was collected for this workload AND this exact library build."""
@@ -162,7 +207,9 @@ def load_traffic(workload, sha):
                 d = json.load(fh)
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("lib_sha") == sha:
+        if d.get("workload") != workload:
+            continue
+        if (code is not None and d.get("code_sha") == code) or d.get("lib_sha") == sha:
             return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
 
@@ -458,8 +505,8 @@ def run_flow(args, world, rank, device, dist, cpu):
         alg, issued = flop_counts(pairs, n_atoms, layers, HID, NF, c["prec"], argmax=not c["reverse"])
         kern_ms = kt[kname]["ms_per_launch"]
         nmax = 32 if atoms <= 32 else (64 if atoms <= 64 else 256)
-        sha = lib_sha()
-        traffic, tsrc = load_traffic(workload_name(args.mode), sha)
+        sha, code = lib_sha(), code_sha()
+        traffic, tsrc = load_traffic(workload_name(args.mode), sha, code)
         line = {
             "metric": c["metric"], "value": mols * world * args.steps / elapsed, "unit": c["unit"],
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -476,7 +523,7 @@ def run_flow(args, world, rank, device, dist, cpu):
             "roofline": roofline_mfma(alg, issued, kern_ms, c["prec"],
                                       f"lf_flow_kernel<{HID},{nmax},{str(c['reverse']).lower()},"
                                       f"{c['prec']}>", traffic,
-                                      {"traffic_source": tsrc, "lib_sha": sha}),
+                                      {"traffic_source": tsrc, "lib_sha": sha, "code_sha": code}),
             "kernels": kt,
             "cpu_baseline": cpu,
         }

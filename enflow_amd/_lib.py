@@ -38,6 +38,8 @@ SIGNATURES = {
     "enflow_abi_version": (_i, []),
     "enflow_set_latency_threshold": (_i, [_i]),
     "enflow_latency_threshold": (_i, []),
+    "enflow_set_split_threshold": (_i, [_i]),
+    "enflow_set_fs_threshold": (_i, [_i]),
     "enflow_max_atoms": (_i, []),
     "enflow_max_node_nf": (_i, []),
     "enflow_supports_hidden": (_i, [_i]),
@@ -141,6 +143,10 @@ def lib(nf=None):
             fn.argtypes = args
         if _lat_threshold[0] is not None and hasattr(handle, "enflow_set_latency_threshold"):
             handle.enflow_set_latency_threshold(_lat_threshold[0])
+        if _split_threshold[0] is not None and hasattr(handle, "enflow_set_split_threshold"):
+            handle.enflow_set_split_threshold(_split_threshold[0])
+        if _fs_threshold[0] is not None and hasattr(handle, "enflow_set_fs_threshold"):
+            handle.enflow_set_fs_threshold(_fs_threshold[0])
         _libs[path] = handle
     return handle
 
@@ -159,6 +165,36 @@ def set_latency_threshold(max_mols):
     for h in _libs.values():
         if hasattr(h, "enflow_set_latency_threshold"):
             h.enflow_set_latency_threshold(int(max_mols))
+    return prev
+
+
+_split_threshold = [None]
+_fs_threshold = [None]
+
+
+def set_split_threshold(max_mols):
+    """Route fused <= 32-atom H = 128 f16x3 inference launches of at most
+    `max_mols` molecules (and at most half the device's CUs) to the
+    feature-split instance with two workgroups per molecule
+    (enflow_split.hip; -1: CUs / 2, the default; 0: never).  Per library, like
+    set_latency_threshold.  Returns the previous setting (None: never set)."""
+    prev = _split_threshold[0]
+    _split_threshold[0] = int(max_mols)
+    for h in _libs.values():
+        if hasattr(h, "enflow_set_split_threshold"):
+            h.enflow_set_split_threshold(int(max_mols))
+    return prev
+
+
+def set_fs_threshold(max_mols):
+    """Route such launches of at most `max_mols` molecules that do not take
+    the two-workgroup split to the feature-split instance with one workgroup
+    per molecule (-1: never, the default).  Returns the previous setting."""
+    prev = _fs_threshold[0]
+    _fs_threshold[0] = int(max_mols)
+    for h in _libs.values():
+        if hasattr(h, "enflow_set_fs_threshold"):
+            h.enflow_set_fs_threshold(int(max_mols))
     return prev
 
 

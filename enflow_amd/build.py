@@ -14,10 +14,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 SRCS = [os.path.join(CSRC, f) for f in ("enflow_flow.hip", "enflow_backward.hip", "enflow_large.hip", "enflow_timing.hip",
-                                              "enflow_latency.hip")
+                                              "enflow_latency.hip", "enflow_split.hip")
         if os.path.exists(os.path.join(CSRC, f))]
 HDRS = [os.path.join(CSRC, h) for h in ("flow_device.h", "flow_kernel.h", "enflow_timing.h", "enflow_large.h",
-                                         "enflow_latency.h")] + [os.path.join(ROOT, "include", "enflow_hip.h")]
+                                         "enflow_latency.h", "enflow_split.h")] + [os.path.join(ROOT, "include", "enflow_hip.h")]
 OUT = os.path.join(HERE, "libenflow_hip.so")
 ARCH = os.environ.get("ENFLOW_OFFLOAD_ARCH", "gfx950")
 SCANNER = os.path.join(ROOT, "tools", "asm_hazard_scan.py")

@@ -231,7 +231,7 @@ struct BwdSmem {
   float apos[NMAX * 3], avel[NMAX * 3], aF[NMAX * 3];
   float aQ[NMAX];
   uint32_t nmax[NMAX / 32];   // per atom tile: max |d pre(node_nn.0)| (float bits)
-  float wrad[NFMAX == 16 ? H : 1];   // nf 16: edge_nn.0.weight[:, 2 nf] (the radial column)
+  alignas(16) float wrad[NFMAX == 16 ? H : 1];   // nf 16: edge_nn.0.weight[:, 2 nf] (the radial column)
 };
 
 // Adjoint tiles span many decades (coord_nn.2 starts at gain 0.001), so before

@@ -27,6 +27,7 @@
 
 #include "enflow_large.h"
 #include "enflow_latency.h"
+#include "enflow_split.h"
 
 // ---------------------------------------------------------------------------
 // packing kernels
@@ -487,6 +488,7 @@ static int lat_threshold_now() {
 
 template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
+  if (NN == 32 && enflow_fs_launch(HH, REV, prec, num_mols, st, &A)) return;
   if (NN == 32 && num_mols <= lat_threshold_now() && enflow_lat_launch(HH, REV, prec, num_mols, st, &A)) return;
   if (prec & ENFLOW_EGCL_VARIANTS) launch_flow_v<HH, NN, RBB, REV, true>(prec & 0xff, num_mols, st, A);
   else launch_flow_v<HH, NN, RBB, REV, false>(prec, num_mols, st, A);

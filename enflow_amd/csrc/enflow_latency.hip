@@ -61,3 +61,17 @@ bool enflow_lat_launch(int H, bool rev, int prec, int num_mols, hipStream_t st, 
   }
 #endif
 }
+
+#ifdef ENFLOW_STAMPS
+// diagnostic build only: the latency TU's own stamp accumulators
+extern "C" int enflow_read_stamps_lat(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(enflow_lat::enflow_stamp_acc), sizeof(unsigned long long) * NSTAMP) !=
+      hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[NSTAMP] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enflow_lat::enflow_stamp_acc), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return NSTAMP;
+}
+#endif

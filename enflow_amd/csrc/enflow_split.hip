@@ -1,0 +1,872 @@
+// enflow_split.hip -- the feature-split latency instance of the fused flow
+// (LFIntegrator.forward / reverse, enflow/flow/dynamics.py:10-37, driving
+// EGCL.forward, enflow/nn/egcl.py:76-92) for batches that leave CUs idle: the
+// stated 1024-molecule batch split over 8 GPUs is 128 molecules per GPU
+// (enflow/main.py:141-143, DistributedSampler), a molecule per CU and half the
+// CUs idle, so the step time is one molecule's serial chain of layers.
+//
+// What sets that chain in the whole-tile instances (phase stamps, profiles/r05):
+// a wave owns a 32-pair edge tile and streams every H x H weight fragment of
+// its three GEMMs from L2 (64 KB per GEMM per tile), one chain step ahead, so
+// each F16X3 step waits on an L2 round trip; the tile loop is ~60 % of a layer.
+//
+// Here the four waves of a workgroup share every tile and split its OUTPUT
+// features: wave w owns features 32 w .. 32 w + 31 of edge_nn.0, edge_nn.2 and
+// coord_nn.0 (H = 128), so its weight fragments of the three GEMMs (hi / lo
+// fp16, 36 KB) are loaded into registers once per layer (one wave per SIMD:
+// 512 registers).  A GEMM's input (all 128 features of the 32 pairs) is
+// exchanged through LDS as the producers' own fp16 hi / lo split, in the MFMA
+// B-operand lane layout (one ds_write_b128 / ds_read_b128 per lane and k-slice,
+// conflict-free); two barriers per tile.  Each wave segment-sums the messages of
+// its own 32 features (selection-matrix MFMAs as in edge_tiles) and the four
+// coord_nn.2 partial dots are added in wave order (deterministic).
+//
+// SPLIT = 2 (at most half as many molecules as CUs): two workgroups per
+// molecule, on two CUs, each owning half of the molecule's rows.  Message and
+// force sums are per row, so each workgroup's aggregates, node phase and
+// leapfrog update of its own atoms are complete; the only exchange per layer is
+// the updated positions and features of its atoms (what the partner's next
+// neighbour list and edge_nn.0 inputs read: 3 + nf floats per atom), handed off
+// as 8-byte {value, tag} granules written with `sc1` stores and polled with
+// `sc1` loads (MI355X_MICROARCH.md: the data-tagged granule hand-off, ~1 us).
+// The pair sits on one XCD (blocks b and b ^ 8); a bounded wait flags
+// ENFLOW_ERR_HANDOFF and the host re-runs the launch on the whole-tile instance.
+//
+// Results are deterministic; they may differ from the whole-tile instances in
+// the last bits (the coord_nn.2 dot is summed per 32-feature block first).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include <mutex>
+#include "enflow_hip.h"
+#include "enflow_timing.h"
+#include "enflow_split.h"
+
+#define WAVES 4
+namespace enflow_fs {
+#include "flow_device.h"
+
+constexpr int NMX = 32;                // molecule capacity (<= 32-atom molecules)
+constexpr int HALF = NMX / 2;          // rows per workgroup of a SPLIT = 2 pair
+constexpr int XG = NFMAX + 3;          // granules per atom in a hand-off: pos (3) + h (nf)
+constexpr int XSLOT = HALF * XG;       // granules per (molecule, half, parity)
+
+template <int H>
+struct FsSmem {
+  static constexpr int NT = H / 32, KS = 2 * NT;
+  Smem<H, NMX, NMX> s;
+  // GEMM operand exchange: [x0 | e][k-slice][hi | lo][lane] x 16 B
+  alignas(16) uint32_t xb[2][KS][2][64][4];
+  float phip[2][NT][32];               // coord_nn.2 partial dots [tile parity][wave][pair]
+  uint32_t tb[NT][32];                 // per wave: the tile's selection words (f16 multiplicity << 16 | segment)
+  int rt[NT][96];                      // per wave: segment rows (slots 32.. absorb the non-start lanes)
+  int nseg[NT];
+  uint8_t vld[NT][2][64];              // per wave and tile parity: lane holds a pair
+  alignas(16) float dummy[NT][H];      // message rows of lanes without a segment
+  int timeout;
+};
+
+struct FsArgs {
+  uint64_t* xch;       // [mols][2 halves][2 parities][XSLOT] hand-off granules (SPLIT = 2)
+  uint32_t* ctl;       // [0] ticket, [1] epoch (+1 per launch, by the last workgroup)
+  float* part;         // [blocks] log|detJ| partial per workgroup
+  int split;           // 1 or 2
+  int blocks;
+};
+
+// wave w's output block of the three edge GEMMs (F16X3 fragments, registers)
+template <int H>
+struct FsW {
+  static constexpr int NT = H / 32, KS = 2 * NT;
+  f32x4 g0h[KS0MAX], g0l[KS0MAX], g1h[KS], g1l[KS], g2h[KS], g2l[KS];
+  __device__ __forceinline__ void load(rsrc_t W, const EgclLayout& L, int lane, int w, int ks0) {
+    const int vo = lane * 32;
+#pragma unroll
+    for (int ks = 0; ks < KS0MAX; ++ks) {
+      if (ks < ks0) {
+        g0h[ks] = bload4(W, vo, (L.we1x + (w * KS0MAX + ks) * 512) * 4);
+        g0l[ks] = bload4(W, vo + 16, (L.we1x + (w * KS0MAX + ks) * 512) * 4);
+      }
+    }
+#pragma unroll
+    for (int ts = 0; ts < KS; ++ts) {
+      g1h[ts] = bload4(W, vo, (L.we2x + (w * KS + ts) * 512) * 4);
+      g1l[ts] = bload4(W, vo + 16, (L.we2x + (w * KS + ts) * 512) * 4);
+    }
+#pragma unroll
+    for (int ts = 0; ts < KS; ++ts) {
+      g2h[ts] = bload4(W, vo, (L.wc1x + (w * KS + ts) * 512) * 4);
+      g2l[ts] = bload4(W, vo + 16, (L.wc1x + (w * KS + ts) * 512) * 4);
+    }
+  }
+};
+
+// accumulator of output block w from the LDS bias image (feature 32 w + 8 g4 + 4 hh + u)
+__device__ __forceinline__ f32x16 bias_block(const float* __restrict__ b, int w, int hh) {
+  f32x16 a;
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const f32x4 v = ld4(b + 32 * w + 8 * g4 + 4 * hh);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[4 * g4 + u] = v[u];
+  }
+  return a;
+}
+__device__ __forceinline__ void silu_block(f32x16& X, float c, float K) {
+#pragma unroll
+  for (int g4 = 0; g4 < 4; ++g4) {
+    const f32x4 y = silu4s((f32x4){X[4 * g4], X[4 * g4 + 1], X[4 * g4 + 2], X[4 * g4 + 3]}, c, K);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) X[4 * g4 + u] = y[u];
+  }
+}
+__device__ __forceinline__ void st_u4(uint32_t* p, const f16x8& v) {
+  *reinterpret_cast<u32x4v*>(p) = __builtin_bit_cast(u32x4v, v);
+}
+__device__ __forceinline__ f16x8 ld_u4(const uint32_t* p) {
+  return __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4v*>(p));
+}
+
+// The pair word decode shared by a tile's GEMM pass and its force pass.
+struct PairLane {
+  bool valid;
+  int il, jl, i, row;
+  float c, dx, dy, dz, radial;
+};
+template <int H>
+__device__ __forceinline__ PairLane decode_pair(FsSmem<H>& F, const MolRef& M, int r0, int P, int tile, int j) {
+  auto& sm = F.s;
+  PairLane q;
+  const int p = tile * 32 + j;
+  q.valid = p < P;
+  const uint32_t pr = q.valid ? sm.pairs[p] : 0u;
+  q.il = (int)(pr & 0xffu);
+  q.jl = (int)((pr >> 8) & 0xffu);
+  q.i = r0 + q.il;
+  q.c = (float)(pr >> 16);
+  q.row = q.valid ? q.il : -1 - j;
+  // Edges.coord_diff with the reference's half-box image (base.py:15-19)
+  q.dx = pbc1(sm.pos[q.i * 3 + 0] - sm.pos[q.jl * 3 + 0], M.bx * 0.5f);
+  q.dy = pbc1(sm.pos[q.i * 3 + 1] - sm.pos[q.jl * 3 + 1], M.by * 0.5f);
+  q.dz = pbc1(sm.pos[q.i * 3 + 2] - sm.pos[q.jl * 3 + 2], M.bz * 0.5f);
+  q.radial = q.dx * q.dx + q.dy * q.dy + q.dz * q.dz;   // egcl.py:79
+  return q;
+}
+
+// forces of one tile (egcl.py:68-74: trans = clamp(coord_diff * phi), segment
+// sums for the mean), phi = the four waves' partial dots in wave order; run by
+// one wave, tiles in order (rows continuing into the next tile accumulate)
+template <int H>
+__device__ __forceinline__ void tile_forces(FsSmem<H>& F, const MolRef& M, int r0, int P, int tile, int lane,
+                                           bool& range_bad) {
+  constexpr int NT = H / 32;
+  constexpr int AST = Smem<H, NMX, NMX>::AST;
+  auto& sm = F.s;
+  const int j = lane & 31, hh = lane >> 5;
+  const PairLane q = decode_pair(F, M, r0, P, tile, j);
+  float phi = 0.f;
+#pragma unroll
+  for (int w = 0; w < NT; ++w) phi += F.phip[tile & 1][w][j];
+  range_bad |= q.valid && !__builtin_isfinite(phi);
+  const SegExec SE = seg_exec(q.row);
+  const int row_next = __shfl_down(q.row, 1, 32);
+  const bool seg_end = q.valid && (j == 31 || row_next != q.row);
+  f32x4* const fslot = reinterpret_cast<f32x4*>(&sm.agg[(q.valid ? q.il : 0) * AST + H]);   // H + 3: padding
+  const f32x4 fold = *fslot;
+  float tx = q.c * clamp100(q.dx * phi);
+  float ty = q.c * clamp100(q.dy * phi);
+  float tz = q.c * clamp100(q.dz * phi);
+  float tw = 0.f;
+  seg_scan4x(tx, ty, tz, tw, SE);
+  if (seg_end && hh == 0) *fslot = fold + (f32x4){tx, ty, tz, tw};
+}
+
+// EGCL edge part of the workgroup's rows (edge_tiles' contract: agg[row][0..H)
+// message sums, agg[row][H..H+2] force sums, multiplicity-weighted), every tile
+// shared by the four waves, wave w on output block w.  Software-pipelined over
+// tiles, two barriers per tile:
+//   B1(t) | GEMM1(t), its MFMA shadow: act + coord_nn.2 dot of tile t - 1 ->
+//         phi partials | act(e) -> operands, message image | message MFMAs
+//   B2(t) | forces of tile t - 1 (one wave, rotating) | GEMM2(t), its shadow:
+//         pair decode, GEMM0, act and operand split of tile t + 1
+// KS0: edge_nn.0 k-slices compiled (gemm0_ksteps(nf) <= KS0; slices past it
+// multiply zero fragments by zero inputs: exact).
+template <int H, int KS0, class Pre>
+__device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restrict__ Lp, const EgclLayout& L,
+                                              const MolRef& M, int nf, int tid, int r0, int rb, const FsW<H>& Wt,
+                                              Pre&& pre STAMP_ARGS) {
+  constexpr int NT = H / 32, KS = 2 * NT;
+  static_assert(NT == WAVES, "one output block per wave");
+  constexpr int AST = Smem<H, NMX, NMX>::AST;
+  constexpr int MIS = Smem<H, NMX, NMX>::MIS;
+  auto& sm = F.s;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5;
+  const int P = sm.npairs;
+  const int T = (P + 31) >> 5;
+  for (int e = tid; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
+  const float K0 = Lp[L.scl + 4], K1 = Lp[L.scl + 0], K2 = Lp[L.scl + 2];
+  for (int k = tid; k < H; k += BLOCK) {
+    sm.bias[k] = Lp[L.be1 + k] * K0;
+    sm.bias[H + k] = Lp[L.be2 + k] * K1;
+    sm.bias[2 * H + k] = Lp[L.bc1 + k] * K2;
+    sm.bias[3 * H + k] = Lp[L.wc2 + k];
+  }
+  __syncthreads();
+  constexpr float NLOG2E = -1.4426950408889634f;
+  const float c0 = NLOG2E * Lp[L.scl + 5], c1 = NLOG2E * Lp[L.scl + 1], c2 = NLOG2E * Lp[L.scl + 3];
+  const int nch = gemm0_nch(nf);
+  const bool rad7 = gemm0_radial_slot7(nf);
+  uint32_t* const img = &sm.u.mm.img[w][0];
+  const int ibase = (8 * hh + ((lane >> 2) & 3)) * MIS + 2 * (4 * ((lane >> 4) & 1) + (lane & 3));
+  bool range_bad = false;
+  uint32_t bigw = 0u;
+  STAMP(9);
+
+  // front(t): decode, segment tables, GEMM0, act, operand split -> xb[0]
+  // (branch-free: a tile past the last one decodes to invalid lanes, writes
+  // nothing anybody reads)
+  auto front = [&](int tile) {
+    const int p = tile * 32 + j;
+    const bool valid = p < P;
+    uint32_t pr = sm.pairs[valid ? p : 0];
+    pr = valid ? pr : 0u;
+    const int il = (int)(pr & 0xffu), jl = (int)((pr >> 8) & 0xffu), i = r0 + il;
+    const float c = (float)(pr >> 16);
+    const int row = valid ? il : -1 - j;
+    const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], M.bx * 0.5f);
+    const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], M.by * 0.5f);
+    const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], M.bz * 0.5f);
+    const float radial = dx * dx + dy * dy + dz * dz;   // egcl.py:79
+    // segment tables of the tile (the message MFMAs' selection matrix)
+    const int row_prev = __shfl_up(row, 1, 32);
+    const bool start = j == 0 || row_prev != row;
+    const uint32_t Sb = (uint32_t)__ballot(start);
+    const int seg = __builtin_popcount(Sb & (uint32_t)((2ull << j) - 1ull)) - 1;
+    F.tb[w][j] = ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)c) << 16) | (uint32_t)seg;
+    F.rt[w][(start && hh == 0) ? seg : 32 + lane] = valid ? il : -1;
+    F.nseg[w] = __builtin_popcount(Sb);
+    const uint32_t vmask = valid ? ENFLOW_BIG_BITS : 0u;
+    // GEMM0: edge_nn.0 . [h_i, h_j, radial] (egcl.py:57-58), output block w
+    f32x16 x0 = bias_block(sm.bias, w, hh);
+    uint32_t o0 = 0u;
+#pragma unroll
+    for (int ks = 0; ks < KS0; ++ks) {
+      f32x16 in;
+      const float* hrow = &sm.h[(hh ? jl : i) * NFP + 8 * (ks < nch ? ks : 0)];   // rows zero-padded past nf
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) in[jj] = ks < nch ? hrow[jj] : 0.f;
+      in[7] = (hh && ks == nch - 1 && rad7) ? radial : in[7];
+      in[0] = (hh == 0 && ks == nch && !rad7) ? radial : in[0];
+      f16x8 bh, bl;
+      split_f16(in, 0, bh, bl);
+      o0 = or_hi(o0, bh);
+      x0 = mfma_f16(Wt.g0h[ks], bh, x0);
+      x0 = mfma_f16(Wt.g0h[ks], bl, x0);
+      x0 = mfma_f16(Wt.g0l[ks], bh, x0);
+    }
+    bigw |= __ballot((o0 & vmask) != 0u) ? (uint32_t)BIGK_X0 : 0u;
+    silu_block(x0, c0, K0);
+    uint32_t o1 = 0u;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      f16x8 bh, bl;
+      split_f16(x0, s, bh, bl);
+      o1 = or_hi(o1, bh);
+      st_u4(&F.xb[0][2 * w + s][0][lane][0], bh);
+      st_u4(&F.xb[0][2 * w + s][1][lane][0], bl);
+    }
+    bigw |= __ballot((o1 & vmask) != 0u) ? (uint32_t)BIGK_Y0 : 0u;
+    F.vld[w][tile & 1][lane] = valid;
+  };
+  // coord_nn.2 partial dot of a tile's coord_nn.0 accumulators (block w) -> phi partials
+  auto dot2 = [&](const f32x16& hc, int tile) {
+    float part = 0.f;
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 w2 = ld4(sm.bias + 3 * H + 32 * w + 8 * g4 + 4 * hh);
+      const f32x4 y = silu4s((f32x4){hc[4 * g4], hc[4 * g4 + 1], hc[4 * g4 + 2], hc[4 * g4 + 3]}, c2, K2);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
+    }
+    part += __shfl_xor(part, 32, 64);
+    F.phip[tile & 1][w][j] = part;   // both lane halves: the same value to the same word
+  };
+
+  f32x16 hc = bias_block(sm.bias + 2 * H, w, hh);   // tile t - 1's coord_nn.0 accumulators
+  if (T > 0) front(0);
+  STAMP(10);
+  for (int tile = 0; tile < T; ++tile) {
+    __syncthreads();   // B1: x0 of every block in LDS
+    STAMP(11);
+    // ---- GEMM1: edge_nn.2 (egcl.py:20-24), output block w; shadow: tile - 1's coord_nn.2
+    f32x16 e = bias_block(sm.bias + H, w, hh);
+    {
+      f16x8 bh[KS], bl[KS];
+#pragma unroll
+      for (int ts = 0; ts < KS; ++ts) {
+        bh[ts] = ld_u4(&F.xb[0][ts][0][lane][0]);
+        bl[ts] = ld_u4(&F.xb[0][ts][1][lane][0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ts = 0; ts < KS; ++ts) {
+        e = mfma_f16(Wt.g1h[ts], bh[ts], e);
+        e = mfma_f16(Wt.g1h[ts], bl[ts], e);
+        e = mfma_f16(Wt.g1l[ts], bh[ts], e);
+      }
+      dot2(hc, tile - 1);   // (tile 0: a dummy write to phi partials nobody reads)
+#pragma unroll
+      for (int k = 0; k < 3 * KS; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, 5, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    STAMP(12);
+    silu_block(e, c1, K1);
+    {
+      uint32_t o2 = 0u;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        f16x8 bh, bl;
+        split_f16(e, s, bh, bl);
+        o2 = or_hi(o2, bh);
+        st_u4(&F.xb[1][2 * w + s][0][lane][0], bh);
+        st_u4(&F.xb[1][2 * w + s][1][lane][0], bl);
+        // the message image of this block: [pair][hi 16 dwords | lo 16 dwords]
+        const u32x4v hv = __builtin_bit_cast(u32x4v, bh), lv = __builtin_bit_cast(u32x4v, bl);
+        uint32_t* const r = img + j * MIS + 2 * hh + 8 * s;
+        *reinterpret_cast<u32x2v*>(r) = (u32x2v){hv[0], hv[1]};
+        *reinterpret_cast<u32x2v*>(r + 4) = (u32x2v){hv[2], hv[3]};
+        *reinterpret_cast<u32x2v*>(r + 16) = (u32x2v){lv[0], lv[1]};
+        *reinterpret_cast<u32x2v*>(r + 20) = (u32x2v){lv[2], lv[3]};
+      }
+      const uint32_t vmask = F.vld[w][tile & 1][lane] ? ENFLOW_BIG_BITS : 0u;
+      bigw |= __ballot((o2 & vmask) != 0u) ? (uint32_t)BIGK_M : 0u;
+    }
+    STAMP(13);
+    {   // message segment sums of block w on the matrix cores (edge_tiles' MMA path):
+        // agg[row(n)][32 w + f] += sum_p E[p][f] S[p][n], S[p][n] = multiplicity of p in segment n
+      u32x4v tq[4];
+#pragma unroll
+      for (int qq = 0; qq < 4; ++qq)
+        tq[qq] = *reinterpret_cast<const u32x4v*>(&F.tb[w][16 * (qq >> 1) + 8 * hh + 4 * (qq & 1)]);
+      const int rn = F.rt[w][j];
+      const int nseg = F.nseg[w];
+      f16x8 sel[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const u32x4v q0 = tq[2 * ks], q1 = tq[2 * ks + 1];
+        const uint32_t wv[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+        u32x4v pk;
+#pragma unroll
+        for (int i2 = 0; i2 < 4; ++i2) {
+          const uint32_t a0 = (wv[2 * i2] & 0xffffu) == (uint32_t)j ? wv[2 * i2] >> 16 : 0u;
+          const uint32_t a1 = (wv[2 * i2 + 1] & 0xffffu) == (uint32_t)j ? wv[2 * i2 + 1] & 0xffff0000u : 0u;
+          pk[i2] = a0 | a1;
+        }
+        sel[ks] = __builtin_bit_cast(f16x8, pk);
+      }
+      const bool vn = j < nseg && rn >= 0;
+      float* const dstn = vn ? &sm.agg[rn * AST + 32 * w] : &F.dummy[w][0];
+      s16x4 ar[4][2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int rd = 0; rd < 2; ++rd) ar[k][rd] = lds_tr16(img + ibase + (16 * (k >> 1) + 4 * rd) * MIS + 16 * (k & 1));
+      f32x16 Y;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 v = ld4(dstn + 8 * g4 + 4 * hh);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) Y[4 * g4 + u] = v[u];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(cat_f16x8(ar[k][0], ar[k][1]), sel[k >> 1], Y, 0, 0, 0);
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4)
+        st4(dstn + 8 * g4 + 4 * hh, (f32x4){Y[4 * g4], Y[4 * g4 + 1], Y[4 * g4 + 2], Y[4 * g4 + 3]});
+    }
+    STAMP(14);
+    __syncthreads();   // B2: e of every block in LDS; phi partials of tile - 1 complete
+    STAMP(15);
+    if (tile > 0 && w == (tile - 1) % WAVES) tile_forces(F, M, r0, P, tile - 1, lane, range_bad);
+    STAMP(16);
+    // ---- GEMM2: coord_nn.0 (egcl.py:35-42), output block w; shadow: tile + 1's front
+    hc = bias_block(sm.bias + 2 * H, w, hh);
+    {
+      f16x8 bh[KS], bl[KS];
+#pragma unroll
+      for (int ts = 0; ts < KS; ++ts) {
+        bh[ts] = ld_u4(&F.xb[1][ts][0][lane][0]);
+        bl[ts] = ld_u4(&F.xb[1][ts][1][lane][0]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ts = 0; ts < KS; ++ts) {
+        hc = mfma_f16(Wt.g2h[ts], bh[ts], hc);
+        hc = mfma_f16(Wt.g2h[ts], bl[ts], hc);
+        hc = mfma_f16(Wt.g2l[ts], bh[ts], hc);
+      }
+      front(tile + 1);
+#pragma unroll
+      for (int k = 0; k < 3 * KS + 3 * KS0; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, 6, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    STAMP(17);
+  }
+  if (T > 0) dot2(hc, T - 1);
+  pre();
+  __syncthreads();
+  if (T > 0 && w == (T - 1) % WAVES) tile_forces(F, M, r0, P, T - 1, lane, range_bad);
+  if (__ballot(range_bad))
+    if (lane == 0) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
+  if (lane == 0 && T > 0) atomicOr(&sm.big, bigw | (uint32_t)BIGK_EDGE);
+  __syncthreads();
+  STAMP(18);
+}
+
+// ArgMax.forward (argmax.py:13-25) on the molecule: argmax_dequant's
+// arithmetic, every atom (both workgroups of a pair draw the same noise
+// elements, so their h agree bitwise); returns log_q of this thread's atoms.
+// (argmax_dequant itself is reused as is.)
+
+// the hand-off (SPLIT = 2): tag of (launch epoch, layer); never 0 (a zeroed slot never matches)
+__device__ __forceinline__ uint32_t xtag(uint32_t epoch, int l) {
+  return ((epoch & 0xffffffu) << 8) | 0x80u | (uint32_t)(l & 0x7f);
+}
+// publish the workgroup's atoms [r0, r0 + rb): pos (3) and h (nf), sc1 stores
+template <int H>
+__device__ __forceinline__ void fs_publish(FsSmem<H>& F, uint64_t* slot, int r0, int rb, int nf, uint32_t tag) {
+  auto& sm = F.s;
+  const int per = 3 + nf;
+  for (int e = threadIdx.x; e < rb * per; e += BLOCK) {
+    const int a = e / per, k = e - a * per;
+    const float v = k < 3 ? sm.pos[(r0 + a) * 3 + k] : sm.h[(r0 + a) * NFP + (k - 3)];
+    const uint64_t g = ((uint64_t)tag << 32) | (uint64_t)__float_as_uint(v);
+    __hip_atomic_store(slot + a * XG + k, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// wait for the partner's atoms [r0, r0 + rb) of this tag (bounded: ~0.1 s, then ENFLOW_ERR_HANDOFF)
+template <int H>
+__device__ __forceinline__ void fs_consume(FsSmem<H>& F, const uint64_t* slot, int r0, int rb, int nf, uint32_t tag) {
+  auto& sm = F.s;
+  const int per = 3 + nf;
+  for (int e = threadIdx.x; e < rb * per; e += BLOCK) {
+    const int a = e / per, k = e - a * per;
+    uint64_t g = 0;
+    int spins = 0;
+    for (;;) {
+      g = __hip_atomic_load(slot + a * XG + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((uint32_t)(g >> 32) == tag) break;
+      if (++spins > (1 << 20)) {
+        F.timeout = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const float v = __uint_as_float((uint32_t)g);
+    if (k < 3) sm.pos[(r0 + a) * 3 + k] = v;
+    else sm.h[(r0 + a) * NFP + (k - 3)] = v;
+  }
+  __syncthreads();
+}
+
+template <int H, bool REV, int SPLIT, int KS0>
+__global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
+  __shared__ FsSmem<H> F;
+  auto& sm = F.s;
+  const int tid = threadIdx.x;
+  STAMP_DECL
+  const int b = blockIdx.x;
+  // SPLIT = 2: blocks b and b ^ 8 (one XCD under round-robin placement) are the
+  // two halves of molecule (b >> 4) * 8 + (b & 7)
+  const int m = SPLIT == 2 ? (b >> 4) * 8 + (b & 7) : b;
+  const int half = SPLIT == 2 ? (b >> 3) & 1 : 0;
+  float ldj = 0.f;
+  bool active = m < A.num_mols;
+  MolRef M{0, 0, 0.f, 0.f, 0.f, 0.f};
+  if (active) {
+    M.a0 = A.mol_ptr[m];
+    M.n = A.mol_ptr[m + 1] - M.a0;
+    if (M.n > NMX || A.nf > NFMAX) {
+      if (tid == 0) atomicOr(A.err, M.n > NMX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
+      active = false;
+    }
+  }
+  if (active) {
+    const int n = M.n, nf = A.nf;
+    M.rc = A.r_cut[m];
+    for (int e = tid; e < n * 3; e += BLOCK) {
+      sm.pos[e] = (A.pos_in ? A.pos_in : A.pos)[(size_t)M.a0 * 3 + e];
+      sm.vel[e] = (A.vel_in ? A.vel_in : A.vel)[(size_t)M.a0 * 3 + e];
+      sm.boxa[e] = A.box[(size_t)M.a0 * 3 + e];
+    }
+    const float* const hin = A.h_in ? A.h_in : A.h;
+    const float* const gin = A.g_in ? A.g_in : A.g;
+    for (int e = tid; e < n * NFP; e += BLOCK) {   // rows zero-padded past nf
+      const int a = e / NFP, q = e - a * NFP;
+      const size_t src = (size_t)(M.a0 + a) * nf + q;
+      sm.h[e] = q < nf ? hin[src] : 0.f;
+      sm.g[e] = q < nf ? gin[src] : 0.f;
+    }
+    if (tid == 0) {
+      sm.err = 0;
+      sm.big = 0u;
+      F.timeout = 0;
+    }
+    __syncthreads();
+    if (n > 0) {
+      M.bx = sm.boxa[0];
+      M.by = sm.boxa[1];
+      M.bz = sm.boxa[2];
+    }
+    // the workgroup's rows
+    const int n0 = SPLIT == 2 ? (n + 1) >> 1 : n;
+    const int r0 = half ? n0 : 0, rb = half ? n - n0 : n0;
+    const int pr0 = half ? 0 : n0, prb = half ? n0 : n - n0;   // the partner's rows
+    const uint32_t epoch = SPLIT == 2 ? __hip_atomic_load(&X.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    uint64_t* const xmine = SPLIT == 2 ? X.xch + ((size_t)(m * 2 + half) * 2) * XSLOT : nullptr;
+    const uint64_t* const xpart = SPLIT == 2 ? X.xch + ((size_t)(m * 2 + (half ^ 1)) * 2) * XSLOT : nullptr;
+    auto pbox = [&](int a, int d) { return sm.boxa[a * 3 + d]; };
+
+    STAMP(0);
+    if (!REV) {
+      if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
+        // every atom in both halves (the same draws); half 0 counts log_q
+        const float lq = argmax_dequant<H, NMX, NMX, false>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+        if (half == 0) ldj += lq;
+      } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+        for (int e = tid; e < n * nf; e += BLOCK) {
+          const int a = e / nf, q = e - a * nf;
+          sm.h[a * NFP + q] += A.dequant_scale * A.noise_src().uniform((size_t)M.a0 * nf + e);
+        }
+        __syncthreads();
+      }
+    }
+
+    STAMP(1);
+    for (int it = 0; it < A.n_layers; ++it) {
+      int nfl = __builtin_amdgcn_readfirstlane(A.nf), nl = __builtin_amdgcn_readfirstlane(M.n), tid_l = tid;
+      asm volatile("" : "+s"(nfl), "+s"(nl), "+v"(tid_l));
+      MolRef Ml = M;
+      Ml.n = nl;
+      const EgclLayout L = egcl_layout(H, nfl);
+      const int l = REV ? A.n_layers - 1 - it : it;
+      const float* Lp = A.layers + (size_t)l * L.total;
+      const rsrc_t W = weights_rsrc(Lp, L.total);
+      const int lane = tid_l & 63, w = __builtin_amdgcn_readfirstlane(tid_l >> 6);
+      // this wave's weight block, requested before the neighbour list (its L2
+      // round trips overlap the pair build)
+      FsW<H> Wt;
+      Wt.load(W, L, lane, w, KS0);
+      if (REV) {   // dynamics.py:28-30 on the workgroup's atoms
+        for (int a = r0 + tid; a < r0 + rb; a += BLOCK) {
+          for (int q = 0; q < nfl; ++q) sm.h[a * NFP + q] -= sm.g[a * NFP + q] * A.dt;
+          for (int d = 0; d < 3; ++d)
+            sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, pbox(a, d));
+        }
+        __syncthreads();
+        if constexpr (SPLIT == 2) {
+          const uint32_t tag = xtag(epoch, it);
+          fs_publish(F, xmine + (it & 1) * XSLOT, r0, rb, nfl, tag);
+          fs_consume(F, xpart + (it & 1) * XSLOT, pr0, prb, nfl, tag);
+        }
+      }
+      STAMP(2);
+      build_images(sm, Ml, tid_l);
+      STAMP(3);
+      block_counts(sm, Ml, tid_l, r0, rb, true);   // build_images zeroed the whole count matrix
+      block_compact(sm, nl, tid_l, rb, 0);
+      STAMP(4);
+      if (A.stats != nullptr && tid == 0) {
+        unsigned long long edges = 0;
+        for (int a = 0; a < rb; ++a) edges += (unsigned long long)sm.cntrow[r0 + a];
+        atomicAdd(&A.stats[0], (unsigned long long)sm.npairs);
+        atomicAdd(&A.stats[1], edges);
+      }
+      NodeFrags<H> nfr;
+      fs_edge_tiles<H, KS0>(F, Lp, L, Ml, nfl, tid_l, r0, rb, Wt, [&] {
+        if (w < H / 32) nfr.issue(W, L, lane, w);
+      } STAMP_PASS);
+      STAMP(5);
+      node_phase_x3_f<H, NMX, NMX, false>(sm, Lp, L, nl, nfl, tid_l, r0, rb, nfr, true);
+      STAMP(6);
+      if (tid == 0) {
+        if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_RANGE;
+        sm.big = 0u;
+      }
+      constexpr int AST = Smem<H, NMX, NMX>::AST;
+      for (int a = r0 + tid; a < r0 + rb; a += BLOCK) {
+        const float q = sm.Q[a];
+        const float eq = expf(q);
+        const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);   // helpers.py:63-70
+        auto force = [&](int d) { return sm.agg[(a - r0) * AST + H + d] * inv * A.cw; };
+        if (!REV) {   // dynamics.py:15-22
+          for (int d = 0; d < 3; ++d) {
+            const float Fd = force(d);
+            const float v = eq * sm.vel[a * 3 + d] + Fd * A.dt;
+            sm.vel[a * 3 + d] = v;
+            sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, pbox(a, d));
+          }
+          for (int qf = 0; qf < nfl; ++qf) {
+            const float gn = sm.g[a * NFP + qf] + sm.G[a * NFP + qf] * A.dt;
+            sm.g[a * NFP + qf] = gn;
+            sm.h[a * NFP + qf] += gn * A.dt;
+          }
+          ldj += q;
+        } else {      // dynamics.py:32-35
+          for (int qf = 0; qf < nfl; ++qf) sm.g[a * NFP + qf] -= sm.G[a * NFP + qf] * A.dt;
+          for (int d = 0; d < 3; ++d) {
+            const float Fd = force(d);
+            sm.vel[a * 3 + d] = (sm.vel[a * 3 + d] - Fd * A.dt) / eq;
+          }
+        }
+      }
+      __syncthreads();
+      STAMP(7);
+      if constexpr (SPLIT == 2) {
+        if (!REV && it + 1 < A.n_layers) {
+          const uint32_t tag = xtag(epoch, it);
+          fs_publish(F, xmine + (it & 1) * XSLOT, r0, rb, nfl, tag);
+          fs_consume(F, xpart + (it & 1) * XSLOT, pr0, prb, nfl, tag);
+        }
+      }
+      STAMP(8);
+    }
+
+    if (REV) {   // dequantize.reverse (argmax.py:27-28 / floor.py:13), the workgroup's atoms
+      for (int a = r0 + tid; a < r0 + rb; a += BLOCK) {
+        if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
+          int best = 0;
+          float bv = sm.h[a * NFP];
+          for (int q = 1; q < nf; ++q)
+            if (sm.h[a * NFP + q] > bv) { bv = sm.h[a * NFP + q]; best = q; }
+          A.argmax_idx[M.a0 + a] = best;
+          atomicMax(A.max_idx, best);
+        } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+          for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] = floorf(sm.h[a * NFP + q]);
+        }
+      }
+      __syncthreads();
+    }
+    bool bad = false;
+    for (int e = tid; e < rb * 3; e += BLOCK) {
+      const int ee = r0 * 3 + e;
+      const float p = sm.pos[ee], v = sm.vel[ee];
+      A.pos[(size_t)M.a0 * 3 + ee] = p;
+      A.vel[(size_t)M.a0 * 3 + ee] = v;
+      bad |= !__builtin_isfinite(p) || !__builtin_isfinite(v);
+    }
+    for (int e = tid; e < rb * nf; e += BLOCK) {
+      const int a = r0 + e / nf, q = e % nf;
+      const float hv = sm.h[a * NFP + q], gv = sm.g[a * NFP + q];
+      A.h[(size_t)(M.a0 + a) * nf + q] = hv;
+      A.g[(size_t)(M.a0 + a) * nf + q] = gv;
+      bad |= (!REV && !__builtin_isfinite(hv)) || !__builtin_isfinite(gv);
+    }
+    if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
+    __syncthreads();
+    if (tid == 0) {
+      int err = sm.err;
+      if (F.timeout) err |= ENFLOW_ERR_HANDOFF;
+      if (err) atomicOr(A.err, err);
+    }
+  }
+  STAMP(19);
+  STAMP_FLUSH
+  if (REV) return;
+  // log|detJ|: this workgroup's partial, then the last workgroup to finish sums
+  // them in a fixed order (per molecule half 0 + half 1, then
+  // reduce_ldj_kernel's strided double sums and tree) and resets the ticket.
+  // The partials are sc1 stores drained before the ticket add, and read with sc1
+  // loads by the workgroup whose add came last (MI355X_MICROARCH.md, hand-off
+  // table row 1): no cache-wide fence.
+  const float s = block_sum(sm, ldj);
+  __shared__ int last;
+  if (tid == 0) {
+    if (s != s || !__builtin_isfinite(s)) {
+      if (active) atomicOr(A.err, ENFLOW_ERR_RANGE);
+    }
+    __hip_atomic_store(&X.part[b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(&X.ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)X.blocks - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  constexpr int RT = 256;
+  double* red = reinterpret_cast<double*>(sm.agg);
+  double acc = 0.0;
+  if (tid < RT)
+    for (int mm = tid; mm < A.num_mols; mm += RT) {
+      float v;
+      if (SPLIT == 2) {
+        const int b0 = (mm >> 3) * 16 + (mm & 7);
+        v = __hip_atomic_load(&X.part[b0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+            __hip_atomic_load(&X.part[b0 + 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        v = __hip_atomic_load(&X.part[mm], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      A.ldj_mol[mm] = v;
+      acc += (double)v;
+    }
+  if (tid < RT) red[tid] = acc;
+  __syncthreads();
+  for (int off = RT / 2; off > 0; off >>= 1) {
+    if (tid < off) red[tid] += red[tid + off];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    A.ldj_total[0] = (float)(red[0] + A.ldj_cst);
+    __hip_atomic_store(&X.ctl[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&X.ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// reverse launches have no ticket: the epoch advances in a one-thread kernel
+// after them (stream order) so the next launch's tags differ
+__global__ void fs_epoch_kernel(uint32_t* ctl) {
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace enflow_fs
+
+// ---------------------------------------------------------------------------
+// host side: per-(device, stream) hand-off buffers (allocated on first use,
+// deliberately never freed: a static destructor running after the HIP runtime
+// has torn down must not call into it), the instance choice
+// ---------------------------------------------------------------------------
+namespace {
+struct XBuf {
+  int dev;
+  hipStream_t st;
+  int cap;            // molecules
+  uint64_t* xch;
+  uint32_t* ctl;
+  float* part;
+};
+std::mutex g_mu;
+XBuf g_buf[64];
+int g_nbuf = 0;
+int g_split_threshold = -1;   // SPLIT = 2 for batches of at most this many molecules (-1: CUs / 2)
+int g_fs_threshold = -1;      // SPLIT = 1 for batches of at most this many molecules (-1: off)
+int g_cus[64];
+
+int cus_of(int dev) {
+  if (dev < 0 || dev >= 64) return 0;
+  if (g_cus[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return 0;
+    g_cus[dev] = c;
+  }
+  return g_cus[dev];
+}
+
+XBuf* buffers(int dev, hipStream_t st, int mols) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  XBuf* hit = nullptr;
+  for (int i = 0; i < g_nbuf; ++i)
+    if (g_buf[i].dev == dev && g_buf[i].st == st) hit = &g_buf[i];
+  if (hit && hit->cap >= mols) return hit;
+  if (!hit) {
+    if (g_nbuf >= 64) return nullptr;
+    hit = &g_buf[g_nbuf++];
+    hit->dev = dev;
+    hit->st = st;
+    hit->cap = 0;
+    hit->ctl = nullptr;
+  }
+  // (re)size: the old buffers may still be read by queued launches -- leaked
+  const int cap = mols < 128 ? 128 : mols;
+  const size_t blocks = (size_t)2 * cap + 16;
+  uint64_t* x = nullptr;
+  float* p = nullptr;
+  if (hipMalloc(&x, sizeof(uint64_t) * (size_t)cap * 4 * enflow_fs::XSLOT) != hipSuccess) return nullptr;
+  if (hipMalloc(&p, sizeof(float) * blocks) != hipSuccess) return nullptr;
+  if (hipMemsetAsync(x, 0, sizeof(uint64_t) * (size_t)cap * 4 * enflow_fs::XSLOT, st) != hipSuccess) return nullptr;
+  if (!hit->ctl) {
+    uint32_t* c = nullptr;
+    if (hipMalloc(&c, sizeof(uint32_t) * 4) != hipSuccess) return nullptr;
+    if (hipMemsetAsync(c, 0, sizeof(uint32_t) * 4, st) != hipSuccess) return nullptr;
+    hit->ctl = c;
+  }
+  hit->xch = x;
+  hit->part = p;
+  hit->cap = cap;
+  return hit;
+}
+}  // namespace
+
+int enflow_fs_split_for(int num_mols) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  const int cus = cus_of(dev);
+  const int t2 = g_split_threshold >= 0 ? g_split_threshold : cus / 2;
+  if (num_mols > 0 && num_mols <= t2 && 2 * num_mols <= cus) return 2;
+  if (num_mols > 0 && g_fs_threshold >= 0 && num_mols <= g_fs_threshold) return 1;
+  return 0;
+}
+
+bool enflow_fs_launch(int H, bool rev, int prec, int num_mols, hipStream_t st, const void* flow_args) {
+  const auto& A = *static_cast<const enflow_fs::FlowArgs*>(flow_args);
+  if (H != 128 || prec != ENFLOW_PREC_F16X3 || A.tape != nullptr || A.nf > NFMAX) return false;
+  const int split = enflow_fs_split_for(num_mols);
+  if (split == 0) return false;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  XBuf* B = buffers(dev, st, num_mols);
+  if (!B) return false;
+  enflow_fs::FsArgs X;
+  X.xch = B->xch;
+  X.ctl = B->ctl;
+  X.part = B->part;
+  X.split = split;
+  X.blocks = split == 2 ? ((2 * num_mols + 15) / 16) * 16 : num_mols;
+  enflow_fs::FlowArgs Ak = A;
+  Ak.ticket = nullptr;   // the instance reduces through its own ticket (FsArgs::ctl)
+  Ak.num_mols = num_mols;   // (the reverse entry leaves it unset: whole-tile kernels index by block)
+  const char* name = rev ? "lf_fs_kernel<rev>" : "lf_fs_kernel<fwd>";
+  const dim3 grid(X.blocks), blk(256);
+#define FS_GO(RV, SP, K0) ENFLOW_TIMED(name, st, hipLaunchKernelGGL((enflow_fs::lf_fs_kernel<128, RV, SP, K0>), grid, blk, 0, st, Ak, X))
+  const bool k1 = enflow_fs::gemm0_ksteps(A.nf) == 1;   // nf <= 7 (radial in slot 7): one edge_nn.0 k-slice
+  if (split == 2) {
+    if (rev) { if (k1) FS_GO(true, 2, 1); else FS_GO(true, 2, KS0MAX); }
+    else { if (k1) FS_GO(false, 2, 1); else FS_GO(false, 2, KS0MAX); }
+  } else {
+    if (rev) { if (k1) FS_GO(true, 1, 1); else FS_GO(true, 1, KS0MAX); }
+    else { if (k1) FS_GO(false, 1, 1); else FS_GO(false, 1, KS0MAX); }
+  }
+#undef FS_GO
+  if (rev && split == 2) hipLaunchKernelGGL(enflow_fs::fs_epoch_kernel, dim3(1), dim3(64), 0, st, B->ctl);
+  return true;
+}
+
+extern "C" {
+#ifdef ENFLOW_STAMPS
+// diagnostic build only: this TU's stamp accumulators
+int enflow_read_stamps_fs(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(enflow_fs::enflow_stamp_acc), sizeof(unsigned long long) * NSTAMP) !=
+      hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[NSTAMP] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enflow_fs::enflow_stamp_acc), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return NSTAMP;
+}
+#endif
+int enflow_set_split_threshold(int max_mols) {
+  const int prev = g_split_threshold;
+  g_split_threshold = max_mols < 0 ? -1 : max_mols;
+  return prev;
+}
+int enflow_set_fs_threshold(int max_mols) {
+  const int prev = g_fs_threshold;
+  g_fs_threshold = max_mols < 0 ? -1 : max_mols;
+  return prev;
+}
+}  // extern "C"

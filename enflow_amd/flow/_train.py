@@ -280,7 +280,8 @@ def layer_grads(net, flat):
         ga, _ = unpad_grads(flat[off:], att, EGCL_HDIMS, geom)
         g.update(ga)
     # act_fn's own parameters (a frozen PReLU slope) get no gradient
-    return [None if name.startswith("act_fn.") else g[name].contiguous().to(p.dtype)
+    own = net.act_param_ids()
+    return [None if id(p) in own else g[name].contiguous().to(p.dtype)
             for name, p in net.named_parameters()]
 
 

@@ -26,7 +26,11 @@ class EGCL(nn.Module):
         self.attention = attention
         self.norm_diff = norm_diff
         self.tanh = tanh
-        self.act_fn = act_fn
+        # the reference never registers act_fn as a child of its own (egcl.py:11-55):
+        # a parameterised activation's weights appear only inside the Sequentials
+        # (PReLU: edge_nn.1.weight, after edge_nn.0.bias), so state_dict keys and
+        # parameter order stay the reference's
+        object.__setattr__(self, "act_fn", act_fn)
         edge_coords_nf = 1
         # construction order = reference order (egcl.py:12-55): same RNG stream
         self.edge_nn = nn.Sequential(nn.Linear(input_edge + edge_coords_nf, hidden_nf), act_fn,
@@ -97,8 +101,14 @@ class EGCL(nn.Module):
     def raw_named(self):
         """(name, parameter) in the default-flag named_parameters() order the C
         ABI expects (att_nn, present with attention=True, travels separately;
-        a PReLU slope, registered first as act_fn.weight, travels in the act code)."""
-        return [(k, p) for k, p in self.named_parameters() if not k.startswith(("att_nn.", "act_fn."))]
+        act_fn's own parameters -- a PReLU slope, named edge_nn.1.weight as in the
+        reference -- travel in the act code)."""
+        own = self.act_param_ids()
+        return [(k, p) for k, p in self.named_parameters() if not k.startswith("att_nn.") and id(p) not in own]
+
+    def act_param_ids(self):
+        """ids of act_fn's parameters (shared by every position of the block)."""
+        return {id(p) for p in self.act_fn.parameters()}
 
     def raw_parameters(self):
         return [p for _, p in self.raw_named()]

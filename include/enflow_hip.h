@@ -41,6 +41,9 @@ extern "C" {
                                           f16x3) a GEMM operand of a molecule / row block was
                                           entirely below 2^-7 in magnitude (its fp16 lo parts
                                           subnormal): rerun with ENFLOW_PREC_F32 */
+#define ENFLOW_ERR_HANDOFF         32  /* ABI 12: a two-workgroup latency launch (enflow_set_split_threshold)
+                                          timed out waiting for its partner workgroup (not co-resident):
+                                          outputs invalid, rerun with the split instance off */
 
 /* Precision of the flow's two H x H edge GEMMs (edge_nn.2, coord_nn.0); all
  * other arithmetic is fp32 in every mode.  See DESIGN.md for the error model. */
@@ -76,6 +79,19 @@ int enflow_abi_version(void);
  * one in effect on the current device. */
 int enflow_set_latency_threshold(int max_mols);
 int enflow_latency_threshold(void);
+
+/* ABI 12: the feature-split latency instance (H = 128, f16x3, inference): the
+ * four waves of a workgroup share every 32-pair edge tile, each owning 32 of
+ * its output features with those weights in registers.  Batches of at most
+ * `max_mols` molecules that fit two workgroups per molecule on the device's
+ * CUs run it with each molecule's rows split over two workgroups (one position
+ * / feature hand-off per layer; -1 (default): CUs / 2; 0: never).
+ * enflow_set_fs_threshold: batches of at most `max_mols` molecules that do not
+ * take that split run it with one workgroup per molecule (-1 (default): never).
+ * Same strong-scaling role as enflow_set_latency_threshold (enflow/main.py:
+ * 141-145); both return the previous setting. */
+int enflow_set_split_threshold(int max_mols);
+int enflow_set_fs_threshold(int max_mols);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept.  The ABI
  * ships as two builds of the same sources: libenflow_hip.so (node_nf <= 8) and

@@ -99,7 +99,7 @@ def main():
         # the 2x-corrected one kept beside it as an upper bound.
         raw = (allc["FETCH_SIZE"] + allc["WRITE_SIZE"]) * 1024.0
         hi = (2 * allc["FETCH_SIZE"] + allc["WRITE_SIZE"]) * 1024.0
-        tr = {"workload": bench.workload_name(), "kernel": KERNEL, "lib_sha": bench.lib_sha(),
+        tr = {"workload": bench.workload_name(), "kernel": KERNEL, "lib_sha": bench.lib_sha(), "code_sha": bench.code_sha(),
               "hbm_bytes_per_launch": raw,
               "hbm_bytes_per_launch_fetch_x2": hi, "fetch_kib": allc["FETCH_SIZE"],
               "write_kib": allc["WRITE_SIZE"]}

@@ -13,6 +13,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "enflow_amd", "libenflow_hip_stamps.so")
+FS_PHASES = ["load", "dequant", "layer:weights+rev", "pairs:images+idmap", "pairs:counts+compact", "(after tiles)",
+             "node", "update", "exchange", "  tiles:setup", "  decode+gemm0+act+xw", "  B1 wait", "  forces",
+             "  gemm1", "  act1+split+ew", "  msg mma", "  B2 wait", "  gemm2+dot", "  tail", "writeback"]
 PHASES = ["load", "dequant", "pairs:counts+compact", "pairs:images+idmap", "edge_tiles(all)", "node", "update", "writeback",
           "  tiles:setup", "  gemm0", "  silu0", "  gemm1", "  silu1", "  segsum", "  gemm2+phi+force", "  tail-barrier"]
 
@@ -24,19 +27,26 @@ def main():
     if not os.path.exists(SO):          # build here (CPU container) and ship: the box only runs it
         sys.path.insert(0, ROOT)
         from enflow_amd.build import build
-        build(force=True, out=SO, defines=["ENFLOW_STAMPS"])
+        build(force=False, out=SO, defines=["ENFLOW_STAMPS"])
     if len(sys.argv) > 1 and sys.argv[1] == "build":
         return
     mols = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1024
+    lat = "lat" in sys.argv[1:]         # the 8-wave latency instance instead of the 4-wave one
+    fs = 2 if "fs2" in sys.argv[1:] else (1 if "fs1" in sys.argv[1:] else 0)   # the feature-split instance
     os.environ["ENFLOW_LIB"] = SO
     sys.path.insert(0, ROOT)
     import torch
     import bench
     from enflow_amd import _lib
     L = _lib.lib()
-    L.enflow_read_stamps.restype = ctypes.c_int
-    L.enflow_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
-    L.enflow_set_latency_threshold(0)      # the stamped instance is the 4-wave one
+    rd = L.enflow_read_stamps_fs if fs else (L.enflow_read_stamps_lat if lat else L.enflow_read_stamps)
+    rd.restype = ctypes.c_int
+    rd.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.enflow_set_latency_threshold(100000 if lat else 0)   # which instance is stamped
+    L.enflow_set_split_threshold(100000 if fs == 2 else 0)
+    L.enflow_set_fs_threshold(100000 if fs == 1 else -1)
+    phases = FS_PHASES if fs else PHASES
+    wgs = mols * (2 if fs == 2 else 1)
     dev = torch.device("cuda", 0)
     from enflow_amd.data.synthetic import make_molecules
     model = bench.build_model(dev, bench.LAYERS)
@@ -51,15 +61,15 @@ def main():
         for k in work:
             work[k].copy_(inp[k])
         torch.cuda.synchronize()
-        L.enflow_read_stamps(buf, 1)
+        rd(buf, 1)
         model.forward_buffers(work["h"], work["g"], work["pos"], work["vel"], inp["box"], inp["r_cut"],
                               inp["mol_ptr"], bench.ATOMS, noise, ldj_mol, ldj, err)
         torch.cuda.synchronize()
-        L.enflow_read_stamps(buf, 1)
+        rd(buf, 1)
     tot = sum(buf)       # every stamp closes the interval since the previous one: disjoint
-    for name, v in zip(PHASES, buf):
-        print(f"{name:24s} {100.0 * v / tot:6.2f} %   {v / mols:12.0f} cycles/WG  "
-              f"{v / mols / bench.LAYERS:10.0f} cycles/WG/layer")
+    for name, v in zip(phases, buf):
+        print(f"{name:24s} {100.0 * v / tot:6.2f} %   {v / wgs:12.0f} cycles/WG  "
+              f"{v / wgs / bench.LAYERS:10.0f} cycles/WG/layer")
 
 
 if __name__ == "__main__":
