@@ -23,6 +23,9 @@ ERR_TOO_MANY_ATOMS = 1
 ERR_FEW_IMAGES = 2
 ERR_TOO_MANY_FEATURES = 4
 ERR_RANGE = 8
+ERR_SMALL = 16      # ABI 12: f16x3 operand entirely small (precision, not overflow)
+ERR_HANDOFF = 32    # ABI 12: a two-workgroup latency launch lost its partner (re-run without the split)
+ERR_RERUN = ERR_RANGE | ERR_SMALL   # bits an fp32-GEMM re-run of the flagged molecules resolves
 DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
 PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
@@ -57,6 +60,11 @@ SIGNATURES = {
                                       _i, _p, _p, _u64, _u64, _f, _f, _f, _p, _p, _p, _p, _p, _p, _p, _i, _p]),
     "enflow_lf_reverse_io_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                       _i, _f, _f, _p, _p, _p, _i, _p]),
+    "enflow_lf_forward_io2_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                       _i, _p, _p, _u64, _u64, _f, _f, _f, _p, _p, _p, _p, _p, _p, _p, _i,
+                                       _p, _p, _i, _p]),
+    "enflow_lf_reverse_io2_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _p, _i,
+                                       _i, _f, _f, _p, _p, _p, _i, _p, _p, _i, _p]),
     "enflow_lf_large_workspace_size": (_i64, [_i, _i, _i, _i]),
     "enflow_lf_forward_large_f32": (_i, [_i, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p, _p, _i,
                                          _i, _p, _p, _f, _f, _f, _p, _p, _p, _i, _p, _p, _p, _i64, _p]),
@@ -283,11 +291,13 @@ class KernelTimer:
 
 
 _pending = []
-# launches re-run with fp32 GEMMs after an ENFLOW_ERR_RANGE (inference and training; tests read it)
+# launches re-run with fp32 GEMMs after an ENFLOW_ERR_RANGE / _SMALL (inference and training; tests read
+# it); FP32_MOL_RERUNS: molecules of the inference re-runs that ran only the flagged molecules
 FP32_RERUNS = [0]
+FP32_MOL_RERUNS = [0]
 
 
-def defer_err(err_flag):
+def defer_err(err_flag, small_warns=False):
     """Queue a device error word for a later check instead of synchronising now:
     a non-blocking copy into pinned host memory plus an event.  The training
     backward uses this so the host-side tail of the step (gradient views, the
@@ -298,15 +308,23 @@ def defer_err(err_flag):
     host.copy_(err_flag, non_blocking=True)
     ev = torch.cuda.Event()
     ev.record(torch.cuda.current_stream(err_flag.device))
-    _pending.append((ev, host))
+    _pending.append((ev, host, small_warns))
 
 
 def check_pending():
     """Raise for any deferred error word (waits only for the queued events)."""
     while _pending:
-        ev, host = _pending.pop(0)
+        ev, host, small_warns = _pending.pop(0)
         ev.synchronize()
-        _raise_code(int(host.item()))
+        e = int(host.item())
+        if small_warns and e == ERR_SMALL:
+            import warnings
+            warnings.warn("enflow_amd: a deferred-check training step ran an f16x3 GEMM whose operand was "
+                          "entirely below 2^-7 (gradients ~1e-5 relative instead of fp32 accuracy); set "
+                          "gemm_precision='f32' or defer_error_check=False for the fp32 re-run",
+                          RuntimeWarning, stacklevel=2)
+            continue
+        _raise_code(e)
 
 
 def take_err(err_flag):
@@ -359,6 +377,12 @@ def _raise_code(e):
         raise HipPathError(f"molecule larger than {lib().enflow_max_atoms()} atoms")
     if e & ERR_TOO_MANY_FEATURES:
         raise HipPathError(f"node_nf larger than the kernels' feature width (at most {MAX_NODE_NF})")
+    if e & ERR_HANDOFF:
+        raise HipPathError("a two-workgroup latency launch timed out waiting for its partner workgroup "
+                           "(not co-resident on the device); run with enflow_amd._lib.set_split_threshold(0)")
+    if e & ERR_SMALL and not e & ERR_RANGE:
+        raise RangeError("an f16x3 GEMM operand of a molecule was entirely below 2^-7 in magnitude (its "
+                         "fp16 split loses fp32 accuracy there); run with gemm_precision='f32'")
     if e & ERR_RANGE:
         raise RangeError("a split-precision (f16x3 / bf16) GEMM operand left the range its split "
                          "represents at fp32 accuracy (an fp16 / bf16 overflow, or a layer whose "

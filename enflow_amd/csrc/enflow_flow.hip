@@ -566,6 +566,53 @@ static int check_common(int num_mols, int max_mol_atoms, int nf, int H) {
   return 0;
 }
 
+int enflow_lf_forward_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                             float* h, float* g, float* pos, float* vel,
+                             const float* layers, int n_layers,
+                             int dequant_kind, const float* dequant, const float* noise,
+                             uint64_t noise_seed, uint64_t noise_offset,
+                             float dequant_scale, float dt, float cw,
+                             float* ldj_mol, float* ldj_total, uint32_t* ticket, int32_t* err_flag,
+                             uint64_t* pair_stats, float* tape, int32_t* pair_counts, int gemm_precision,
+                             int32_t* mol_err, const int32_t* mol_list, int num_listed, void* stream) {
+  int rc = check_common(num_mols, max_mol_atoms, nf, H);
+  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
+      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
+  if (rc) return rc;
+  if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
+  if (!h || !g || !pos || !vel || !ldj_mol || !ldj_total || !err_flag) return -1;
+  // training tape: the backward handles molecules of <= 64 atoms (unblocked pair lists)
+  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr || max_mol_atoms > 64)) return -1;
+  // the tape feeds the fp32-accurate backward: it must come from an fp32-accurate forward
+  if (tape != nullptr && (gemm_precision & 0xff) == ENFLOW_PREC_BF16) return -1;
+  // a molecule list runs a subset (no in-launch ticket: the reduction below covers every molecule)
+  if (mol_list != nullptr && (ticket != nullptr || num_listed < 0 || num_listed > num_mols)) return -1;
+  if ((mol_list != nullptr || mol_err != nullptr) && max_mol_atoms > MAX_ATOMS) return -3;
+  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
+             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
+             reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
+  A.h_in = h_in; A.g_in = g_in; A.pos_in = pos_in; A.vel_in = vel_in;
+  A.seed = noise_seed; A.offset = noise_offset;
+  const double cst = dequant_kind == ENFLOW_DEQUANT_ARGMAX ? -0.5 * kLog2Pi : 0.0;
+  A.ticket = num_mols > 0 ? ticket : nullptr;
+  A.ldj_total = ldj_total;
+  A.ldj_cst = cst;
+  A.mol_err = mol_err;
+  A.mol_list = mol_list;
+  const int grid = mol_list != nullptr ? num_listed : num_mols;
+  if (grid > 0) {
+#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, false>(gemm_precision, grid, S(stream), A)
+    DISPATCH_HN(H, max_mol_atoms, CALL);
+#undef CALL
+  }
+  if (A.ticket == nullptr)
+    ENFLOW_TIMED("reduce_ldj_kernel", S(stream),
+                 hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total));
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
 int enflow_lf_forward_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
                              const int32_t* mol_ptr, const float* r_cut, const float* box,
                              const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
@@ -577,34 +624,10 @@ int enflow_lf_forward_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int
                              float* ldj_mol, float* ldj_total, uint32_t* ticket, int32_t* err_flag,
                              uint64_t* pair_stats, float* tape, int32_t* pair_counts, int gemm_precision,
                              void* stream) {
-  int rc = check_common(num_mols, max_mol_atoms, nf, H);
-  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
-      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
-  if (rc) return rc;
-  if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
-  if (!h || !g || !pos || !vel || !ldj_mol || !ldj_total || !err_flag) return -1;
-  // training tape: the backward handles molecules of <= 64 atoms (unblocked pair lists)
-  if (tape != nullptr && (num_atoms < 0 || pair_counts == nullptr || max_mol_atoms > 64)) return -1;
-  // the tape feeds the fp32-accurate backward: it must come from an fp32-accurate forward
-  if (tape != nullptr && (gemm_precision & 0xff) == ENFLOW_PREC_BF16) return -1;
-  FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, dequant, noise,
-             dequant_scale, dt, cw, ldj_mol, nullptr, nullptr, err_flag,
-             reinterpret_cast<unsigned long long*>(pair_stats), tape, pair_counts, num_mols, num_atoms};
-  A.h_in = h_in; A.g_in = g_in; A.pos_in = pos_in; A.vel_in = vel_in;
-  A.seed = noise_seed; A.offset = noise_offset;
-  const double cst = dequant_kind == ENFLOW_DEQUANT_ARGMAX ? -0.5 * kLog2Pi : 0.0;
-  A.ticket = num_mols > 0 ? ticket : nullptr;
-  A.ldj_total = ldj_total;
-  A.ldj_cst = cst;
-  if (num_mols > 0) {
-#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, false>(gemm_precision, num_mols, S(stream), A)
-    DISPATCH_HN(H, max_mol_atoms, CALL);
-#undef CALL
-  }
-  if (A.ticket == nullptr)
-    ENFLOW_TIMED("reduce_ldj_kernel", S(stream),
-                 hipLaunchKernelGGL(reduce_ldj_kernel, dim3(1), dim3(BLOCK), 0, S(stream), ldj_mol, num_mols, cst, ldj_total));
-  return hipGetLastError() == hipSuccess ? 0 : -2;
+  return enflow_lf_forward_io2_f32(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, h_in, g_in, pos_in,
+                                   vel_in, h, g, pos, vel, layers, n_layers, dequant_kind, dequant, noise, noise_seed,
+                                   noise_offset, dequant_scale, dt, cw, ldj_mol, ldj_total, ticket, err_flag,
+                                   pair_stats, tape, pair_counts, gemm_precision, nullptr, nullptr, 0, stream);
 }
 
 int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
@@ -624,14 +647,14 @@ int enflow_lf_forward_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf
                                   pair_counts, gemm_precision, stream);
 }
 
-int enflow_lf_reverse_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+int enflow_lf_reverse_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
                              const int32_t* mol_ptr, const float* r_cut, const float* box,
                              const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
                              float* h, float* g, float* pos, float* vel,
                              const float* layers, int n_layers,
                              int dequant_kind, float dt, float cw,
                              int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
-                             void* stream) {
+                             int32_t* mol_err, const int32_t* mol_list, int num_listed, void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
   if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
       (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
@@ -642,12 +665,31 @@ int enflow_lf_reverse_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int
   FlowArgs A{mol_ptr, r_cut, box, h, g, pos, vel, layers, n_layers, nf, dequant_kind, nullptr, nullptr,
              0.f, dt, cw, nullptr, argmax_idx, max_idx, err_flag, nullptr};
   A.h_in = h_in; A.g_in = g_in; A.pos_in = pos_in; A.vel_in = vel_in;
-  if (num_mols > 0) {
-#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, true>(gemm_precision, num_mols, S(stream), A)
+  if (mol_list != nullptr && (num_listed < 0 || num_listed > num_mols)) return -1;
+  if ((mol_list != nullptr || mol_err != nullptr) && max_mol_atoms > MAX_ATOMS) return -3;
+  A.num_mols = num_mols;
+  A.mol_err = mol_err;
+  A.mol_list = mol_list;
+  const int grid = mol_list != nullptr ? num_listed : num_mols;
+  if (grid > 0) {
+#define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, true>(gemm_precision, grid, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);
 #undef CALL
   }
   return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_lf_reverse_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,
+                             const int32_t* mol_ptr, const float* r_cut, const float* box,
+                             const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                             float* h, float* g, float* pos, float* vel,
+                             const float* layers, int n_layers,
+                             int dequant_kind, float dt, float cw,
+                             int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
+                             void* stream) {
+  return enflow_lf_reverse_io2_f32(num_mols, num_atoms, max_mol_atoms, nf, H, mol_ptr, r_cut, box, h_in, g_in, pos_in,
+                                   vel_in, h, g, pos, vel, layers, n_layers, dequant_kind, dt, cw, argmax_idx,
+                                   max_idx, err_flag, gemm_precision, nullptr, nullptr, 0, stream);
 }
 
 int enflow_lf_reverse_f32(int num_mols, int num_atoms, int max_mol_atoms, int nf, int H,

@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lg_layer_kernel(LgArgs B, int mode) 
   if constexpr (PREC != PREC_F32) node_phase_x3<H, 32, 32, VAR>(sm, B.layer, L, rb, nf, tid, 0, rb);
   else node_phase<H, 32, 32, VAR>(sm, B.layer, L, rb, nf, tid, 0, rb);
   if constexpr (PREC == PREC_F16X3) {   // small-operand guard of the row block (BIGK_*)
-    if (tid == 0 && small_operands(sm.big)) sm.err |= ENFLOW_ERR_RANGE;
+    if (tid == 0 && small_operands(sm.big)) sm.err |= ENFLOW_ERR_SMALL;
   }
   if (tid == 0 && sm.err) atomicOr(B.err, sm.err);   // edge tiles' range check (split precision)
 

@@ -42,7 +42,9 @@
 #include "enflow_timing.h"
 #include "enflow_split.h"
 
-#define WAVES 4
+#define WAVES 8
+// the message MFMAs read the group's operand image: no per-wave message image in Smem
+#define ENFLOW_MSG_MFMA 0
 namespace enflow_fs {
 #include "flow_device.h"
 
@@ -55,14 +57,17 @@ template <int H>
 struct FsSmem {
   static constexpr int NT = H / 32, KS = 2 * NT;
   Smem<H, NMX, NMX> s;
-  // GEMM operand exchange: [x0 | e][k-slice][hi | lo][lane] x 16 B
-  alignas(16) uint32_t xb[2][KS][2][64][4];
-  float phip[2][NT][32];               // coord_nn.2 partial dots [tile parity][wave][pair]
-  uint32_t tb[NT][32];                 // per wave: the tile's selection words (f16 multiplicity << 16 | segment)
-  int rt[NT][96];                      // per wave: segment rows (slots 32.. absorb the non-start lanes)
-  int nseg[NT];
-  uint8_t vld[NT][2][64];              // per wave and tile parity: lane holds a pair
-  alignas(16) float dummy[NT][H];      // message rows of lanes without a segment
+  // GEMM operands, [k-slice][hi | lo][lane] x 16 B: edge_nn.2's (x0) and, per
+  // tile parity, coord_nn.0's (e, also the messages)
+  alignas(16) uint32_t xa[KS][2][64][4];
+  alignas(16) uint32_t xe[2][KS][2][64][4];
+  float phip[2][NT][32];               // coord_nn.2 partial dots [tile parity][block][pair]
+  uint32_t tb[3][32];                  // per tile mod 3: selection words (f16 multiplicity << 16 | segment)
+  int rt[3][96];                       // per tile mod 3: segment rows (slots 32.. absorb the non-start lanes)
+  int nseg[3];
+  int dat[2][32];                      // per tile parity: pair's row atom | column atom << 8
+  float rad[2][32];                    // per tile parity: pair's radial
+  alignas(16) float dummy[NT][32];     // message row of lanes without a segment (per stage-B wave)
   int timeout;
 };
 
@@ -74,29 +79,29 @@ struct FsArgs {
   int blocks;
 };
 
-// wave w's output block of the three edge GEMMs (F16X3 fragments, registers)
+// the wave's weight blocks (F16X3 fragments, registers): stage A (waves
+// 0 .. NT - 1) block b of edge_nn.0 and edge_nn.2, stage B block b of coord_nn.0
 template <int H>
 struct FsW {
   static constexpr int NT = H / 32, KS = 2 * NT;
-  f32x4 g0h[KS0MAX], g0l[KS0MAX], g1h[KS], g1l[KS], g2h[KS], g2l[KS];
+  f32x4 g0h[KS0MAX], g0l[KS0MAX], wh[KS], wl[KS];
   __device__ __forceinline__ void load(rsrc_t W, const EgclLayout& L, int lane, int w, int ks0) {
-    const int vo = lane * 32;
+    const int vo = lane * 32, b = w % NT;
+    const bool A = w < NT;
+    if (A) {
 #pragma unroll
-    for (int ks = 0; ks < KS0MAX; ++ks) {
-      if (ks < ks0) {
-        g0h[ks] = bload4(W, vo, (L.we1x + (w * KS0MAX + ks) * 512) * 4);
-        g0l[ks] = bload4(W, vo + 16, (L.we1x + (w * KS0MAX + ks) * 512) * 4);
+      for (int ks = 0; ks < KS0MAX; ++ks) {
+        if (ks < ks0) {
+          g0h[ks] = bload4(W, vo, (L.we1x + (b * KS0MAX + ks) * 512) * 4);
+          g0l[ks] = bload4(W, vo + 16, (L.we1x + (b * KS0MAX + ks) * 512) * 4);
+        }
       }
     }
+    const int off = A ? L.we2x : L.wc1x;
 #pragma unroll
     for (int ts = 0; ts < KS; ++ts) {
-      g1h[ts] = bload4(W, vo, (L.we2x + (w * KS + ts) * 512) * 4);
-      g1l[ts] = bload4(W, vo + 16, (L.we2x + (w * KS + ts) * 512) * 4);
-    }
-#pragma unroll
-    for (int ts = 0; ts < KS; ++ts) {
-      g2h[ts] = bload4(W, vo, (L.wc1x + (w * KS + ts) * 512) * 4);
-      g2l[ts] = bload4(W, vo + 16, (L.wc1x + (w * KS + ts) * 512) * 4);
+      wh[ts] = bload4(W, vo, (off + (b * KS + ts) * 512) * 4);
+      wl[ts] = bload4(W, vo + 16, (off + (b * KS + ts) * 512) * 4);
     }
   }
 };
@@ -154,8 +159,8 @@ __device__ __forceinline__ PairLane decode_pair(FsSmem<H>& F, const MolRef& M, i
 }
 
 // forces of one tile (egcl.py:68-74: trans = clamp(coord_diff * phi), segment
-// sums for the mean), phi = the four waves' partial dots in wave order; run by
-// one wave, tiles in order (rows continuing into the next tile accumulate)
+// sums for the mean), phi = the four partial dots in block order; run by one
+// stage-B wave, tiles in order (rows continuing into the next tile accumulate)
 template <int H>
 __device__ __forceinline__ void tile_forces(FsSmem<H>& F, const MolRef& M, int r0, int P, int tile, int lane,
                                            bool& range_bad) {
@@ -166,7 +171,7 @@ __device__ __forceinline__ void tile_forces(FsSmem<H>& F, const MolRef& M, int r
   const PairLane q = decode_pair(F, M, r0, P, tile, j);
   float phi = 0.f;
 #pragma unroll
-  for (int w = 0; w < NT; ++w) phi += F.phip[tile & 1][w][j];
+  for (int b = 0; b < NT; ++b) phi += F.phip[tile & 1][b][j];
   range_bad |= q.valid && !__builtin_isfinite(phi);
   const SegExec SE = seg_exec(q.row);
   const int row_next = __shfl_down(q.row, 1, 32);
@@ -182,25 +187,32 @@ __device__ __forceinline__ void tile_forces(FsSmem<H>& F, const MolRef& M, int r
 }
 
 // EGCL edge part of the workgroup's rows (edge_tiles' contract: agg[row][0..H)
-// message sums, agg[row][H..H+2] force sums, multiplicity-weighted), every tile
-// shared by the four waves, wave w on output block w.  Software-pipelined over
-// tiles, two barriers per tile:
-//   B1(t) | GEMM1(t), its MFMA shadow: act + coord_nn.2 dot of tile t - 1 ->
-//         phi partials | act(e) -> operands, message image | message MFMAs
-//   B2(t) | forces of tile t - 1 (one wave, rotating) | GEMM2(t), its shadow:
-//         pair decode, GEMM0, act and operand split of tile t + 1
+// message sums, agg[row][H..H+2] force sums, multiplicity-weighted) as a
+// two-stage pipeline over the tiles.  Waves 0..3 (stage A) own output block b
+// of edge_nn.0 and edge_nn.2, waves 4..7 (stage B) block b of coord_nn.0 and
+// of the message sums: each keeps one weight block in registers, and the two
+// waves on a SIMD (one per stage) run different phases side by side.  Step s:
+//   A: GEMM0, act, operand split of tile s   | B: GEMM2, act, coord_nn.2 partial
+//                                            |    dot of tile s - 1
+//   -- barrier --
+//   A: GEMM1, act, operand split of tile s   | B: message MFMAs of tile s - 1; forces
+//      (-> e image, double-buffered)         |    of tile s - 1 (one wave); pair decode
+//                                            |    + segment tables of tile s + 1 (another)
+//   -- barrier --
+// Each wave handles every tile in order, so message and force rows that
+// continue into the next tile accumulate in order: deterministic.
 // KS0: edge_nn.0 k-slices compiled (gemm0_ksteps(nf) <= KS0; slices past it
 // multiply zero fragments by zero inputs: exact).
-template <int H, int KS0, class Pre>
+template <int H, int KS0>
 __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restrict__ Lp, const EgclLayout& L,
-                                              const MolRef& M, int nf, int tid, int r0, int rb, const FsW<H>& Wt,
-                                              Pre&& pre STAMP_ARGS) {
+                                              const MolRef& M, int nf, int tid, int r0, int rb, const FsW<H>& Wt
+                                              STAMP_ARGS) {
   constexpr int NT = H / 32, KS = 2 * NT;
-  static_assert(NT == WAVES, "one output block per wave");
   constexpr int AST = Smem<H, NMX, NMX>::AST;
-  constexpr int MIS = Smem<H, NMX, NMX>::MIS;
   auto& sm = F.s;
   const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool stA = w < NT;                   // stage
+  const int b = w % NT;                      // output block
   const int j = lane & 31, hh = lane >> 5;
   const int P = sm.npairs;
   const int T = (P + 31) >> 5;
@@ -212,21 +224,18 @@ __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restr
     sm.bias[2 * H + k] = Lp[L.bc1 + k] * K2;
     sm.bias[3 * H + k] = Lp[L.wc2 + k];
   }
-  __syncthreads();
   constexpr float NLOG2E = -1.4426950408889634f;
   const float c0 = NLOG2E * Lp[L.scl + 5], c1 = NLOG2E * Lp[L.scl + 1], c2 = NLOG2E * Lp[L.scl + 3];
   const int nch = gemm0_nch(nf);
   const bool rad7 = gemm0_radial_slot7(nf);
-  uint32_t* const img = &sm.u.mm.img[w][0];
-  const int ibase = (8 * hh + ((lane >> 2) & 3)) * MIS + 2 * (4 * ((lane >> 4) & 1) + (lane & 3));
+  // the transposed (pairs x features) reads of block b's message operand from
+  // the e image (ds_read_b64_tr_b16: lane 4q + p of each 16-lane group
+  // addresses pair q, features 4p .. 4p + 3 of its 16-feature half)
+  const int tr_off = (8 * hh + ((lane >> 2) & 3) + 32 * (lane & 1)) * 4 + 2 * ((lane >> 1) & 1);
   bool range_bad = false;
   uint32_t bigw = 0u;
-  STAMP(9);
-
-  // front(t): decode, segment tables, GEMM0, act, operand split -> xb[0]
-  // (branch-free: a tile past the last one decodes to invalid lanes, writes
-  // nothing anybody reads)
-  auto front = [&](int tile) {
+  // stage B: a tile's pair decode (atoms, radial) and segment tables -> LDS
+  auto decode = [&](int tile) {
     const int p = tile * 32 + j;
     const bool valid = p < P;
     uint32_t pr = sm.pairs[valid ? p : 0];
@@ -237,198 +246,169 @@ __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restr
     const float dx = pbc1(sm.pos[i * 3 + 0] - sm.pos[jl * 3 + 0], M.bx * 0.5f);
     const float dy = pbc1(sm.pos[i * 3 + 1] - sm.pos[jl * 3 + 1], M.by * 0.5f);
     const float dz = pbc1(sm.pos[i * 3 + 2] - sm.pos[jl * 3 + 2], M.bz * 0.5f);
-    const float radial = dx * dx + dy * dy + dz * dz;   // egcl.py:79
-    // segment tables of the tile (the message MFMAs' selection matrix)
+    const int par = tile & 1, tpar = tile % 3;
     const int row_prev = __shfl_up(row, 1, 32);
     const bool start = j == 0 || row_prev != row;
     const uint32_t Sb = (uint32_t)__ballot(start);
     const int seg = __builtin_popcount(Sb & (uint32_t)((2ull << j) - 1ull)) - 1;
-    F.tb[w][j] = ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)c) << 16) | (uint32_t)seg;
-    F.rt[w][(start && hh == 0) ? seg : 32 + lane] = valid ? il : -1;
-    F.nseg[w] = __builtin_popcount(Sb);
-    const uint32_t vmask = valid ? ENFLOW_BIG_BITS : 0u;
-    // GEMM0: edge_nn.0 . [h_i, h_j, radial] (egcl.py:57-58), output block w
-    f32x16 x0 = bias_block(sm.bias, w, hh);
-    uint32_t o0 = 0u;
-#pragma unroll
-    for (int ks = 0; ks < KS0; ++ks) {
-      f32x16 in;
-      const float* hrow = &sm.h[(hh ? jl : i) * NFP + 8 * (ks < nch ? ks : 0)];   // rows zero-padded past nf
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) in[jj] = ks < nch ? hrow[jj] : 0.f;
-      in[7] = (hh && ks == nch - 1 && rad7) ? radial : in[7];
-      in[0] = (hh == 0 && ks == nch && !rad7) ? radial : in[0];
-      f16x8 bh, bl;
-      split_f16(in, 0, bh, bl);
-      o0 = or_hi(o0, bh);
-      x0 = mfma_f16(Wt.g0h[ks], bh, x0);
-      x0 = mfma_f16(Wt.g0h[ks], bl, x0);
-      x0 = mfma_f16(Wt.g0l[ks], bh, x0);
-    }
-    bigw |= __ballot((o0 & vmask) != 0u) ? (uint32_t)BIGK_X0 : 0u;
-    silu_block(x0, c0, K0);
-    uint32_t o1 = 0u;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      f16x8 bh, bl;
-      split_f16(x0, s, bh, bl);
-      o1 = or_hi(o1, bh);
-      st_u4(&F.xb[0][2 * w + s][0][lane][0], bh);
-      st_u4(&F.xb[0][2 * w + s][1][lane][0], bl);
-    }
-    bigw |= __ballot((o1 & vmask) != 0u) ? (uint32_t)BIGK_Y0 : 0u;
-    F.vld[w][tile & 1][lane] = valid;
+    F.tb[tpar][j] = ((uint32_t)__builtin_bit_cast(uint16_t, (_Float16)c) << 16) | (uint32_t)seg;
+    F.rt[tpar][(start && hh == 0) ? seg : 32 + lane] = valid ? il : -1;
+    F.nseg[tpar] = __builtin_popcount(Sb);
+    F.dat[par][j] = i | (jl << 8);
+    F.rad[par][j] = dx * dx + dy * dy + dz * dz;   // egcl.py:79
   };
-  // coord_nn.2 partial dot of a tile's coord_nn.0 accumulators (block w) -> phi partials
-  auto dot2 = [&](const f32x16& hc, int tile) {
-    float part = 0.f;
+  if (!stA && b == 0 && T > 0) decode(0);
+  __syncthreads();
+  STAMP(9);
+  for (int s = 0; s <= T; ++s) {
+    if (stA) {
+      if (s < T) {   // ---- GEMM0 (egcl.py:57-58) of tile s, block b; act, operand split
+        const int par = s & 1;
+        const bool valid = s * 32 + j < P;
+        const int at = F.dat[par][j];
+        const int i = at & 0xff, jl = at >> 8;
+        const float radial = F.rad[par][j];
+        const uint32_t vmask = valid ? ENFLOW_BIG_BITS : 0u;
+        f32x16 x0 = bias_block(sm.bias, b, hh);
+        uint32_t o0 = 0u;
 #pragma unroll
-    for (int g4 = 0; g4 < 4; ++g4) {
-      const f32x4 w2 = ld4(sm.bias + 3 * H + 32 * w + 8 * g4 + 4 * hh);
-      const f32x4 y = silu4s((f32x4){hc[4 * g4], hc[4 * g4 + 1], hc[4 * g4 + 2], hc[4 * g4 + 3]}, c2, K2);
+        for (int ks = 0; ks < KS0; ++ks) {
+          f32x16 in;
+          const float* hrow = &sm.h[(hh ? jl : i) * NFP + 8 * (ks < nch ? ks : 0)];   // rows zero-padded past nf
 #pragma unroll
-      for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
-    }
-    part += __shfl_xor(part, 32, 64);
-    F.phip[tile & 1][w][j] = part;   // both lane halves: the same value to the same word
-  };
-
-  f32x16 hc = bias_block(sm.bias + 2 * H, w, hh);   // tile t - 1's coord_nn.0 accumulators
-  if (T > 0) front(0);
-  STAMP(10);
-  for (int tile = 0; tile < T; ++tile) {
-    __syncthreads();   // B1: x0 of every block in LDS
-    STAMP(11);
-    // ---- GEMM1: edge_nn.2 (egcl.py:20-24), output block w; shadow: tile - 1's coord_nn.2
-    f32x16 e = bias_block(sm.bias + H, w, hh);
-    {
-      f16x8 bh[KS], bl[KS];
-#pragma unroll
-      for (int ts = 0; ts < KS; ++ts) {
-        bh[ts] = ld_u4(&F.xb[0][ts][0][lane][0]);
-        bl[ts] = ld_u4(&F.xb[0][ts][1][lane][0]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ts = 0; ts < KS; ++ts) {
-        e = mfma_f16(Wt.g1h[ts], bh[ts], e);
-        e = mfma_f16(Wt.g1h[ts], bl[ts], e);
-        e = mfma_f16(Wt.g1l[ts], bh[ts], e);
-      }
-      dot2(hc, tile - 1);   // (tile 0: a dummy write to phi partials nobody reads)
-#pragma unroll
-      for (int k = 0; k < 3 * KS; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, 5, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    STAMP(12);
-    silu_block(e, c1, K1);
-    {
-      uint32_t o2 = 0u;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        f16x8 bh, bl;
-        split_f16(e, s, bh, bl);
-        o2 = or_hi(o2, bh);
-        st_u4(&F.xb[1][2 * w + s][0][lane][0], bh);
-        st_u4(&F.xb[1][2 * w + s][1][lane][0], bl);
-        // the message image of this block: [pair][hi 16 dwords | lo 16 dwords]
-        const u32x4v hv = __builtin_bit_cast(u32x4v, bh), lv = __builtin_bit_cast(u32x4v, bl);
-        uint32_t* const r = img + j * MIS + 2 * hh + 8 * s;
-        *reinterpret_cast<u32x2v*>(r) = (u32x2v){hv[0], hv[1]};
-        *reinterpret_cast<u32x2v*>(r + 4) = (u32x2v){hv[2], hv[3]};
-        *reinterpret_cast<u32x2v*>(r + 16) = (u32x2v){lv[0], lv[1]};
-        *reinterpret_cast<u32x2v*>(r + 20) = (u32x2v){lv[2], lv[3]};
-      }
-      const uint32_t vmask = F.vld[w][tile & 1][lane] ? ENFLOW_BIG_BITS : 0u;
-      bigw |= __ballot((o2 & vmask) != 0u) ? (uint32_t)BIGK_M : 0u;
-    }
-    STAMP(13);
-    {   // message segment sums of block w on the matrix cores (edge_tiles' MMA path):
-        // agg[row(n)][32 w + f] += sum_p E[p][f] S[p][n], S[p][n] = multiplicity of p in segment n
-      u32x4v tq[4];
-#pragma unroll
-      for (int qq = 0; qq < 4; ++qq)
-        tq[qq] = *reinterpret_cast<const u32x4v*>(&F.tb[w][16 * (qq >> 1) + 8 * hh + 4 * (qq & 1)]);
-      const int rn = F.rt[w][j];
-      const int nseg = F.nseg[w];
-      f16x8 sel[2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const u32x4v q0 = tq[2 * ks], q1 = tq[2 * ks + 1];
-        const uint32_t wv[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
-        u32x4v pk;
-#pragma unroll
-        for (int i2 = 0; i2 < 4; ++i2) {
-          const uint32_t a0 = (wv[2 * i2] & 0xffffu) == (uint32_t)j ? wv[2 * i2] >> 16 : 0u;
-          const uint32_t a1 = (wv[2 * i2 + 1] & 0xffffu) == (uint32_t)j ? wv[2 * i2 + 1] & 0xffff0000u : 0u;
-          pk[i2] = a0 | a1;
+          for (int jj = 0; jj < 8; ++jj) in[jj] = ks < nch ? hrow[jj] : 0.f;
+          in[7] = (hh && ks == nch - 1 && rad7) ? radial : in[7];
+          in[0] = (hh == 0 && ks == nch && !rad7) ? radial : in[0];
+          f16x8 bh, bl;
+          split_f16(in, 0, bh, bl);
+          o0 = or_hi(o0, bh);
+          x0 = mfma_f16(Wt.g0h[ks], bh, x0);
+          x0 = mfma_f16(Wt.g0h[ks], bl, x0);
+          x0 = mfma_f16(Wt.g0l[ks], bh, x0);
         }
-        sel[ks] = __builtin_bit_cast(f16x8, pk);
+        bigw |= __ballot((o0 & vmask) != 0u) ? (uint32_t)BIGK_X0 : 0u;
+        silu_block(x0, c0, K0);
+        uint32_t o1 = 0u;
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          f16x8 bh, bl;
+          split_f16(x0, sl, bh, bl);
+          o1 = or_hi(o1, bh);
+          st_u4(&F.xa[2 * b + sl][0][lane][0], bh);
+          st_u4(&F.xa[2 * b + sl][1][lane][0], bl);
+        }
+        bigw |= __ballot((o1 & vmask) != 0u) ? (uint32_t)BIGK_Y0 : 0u;
       }
-      const bool vn = j < nseg && rn >= 0;
-      float* const dstn = vn ? &sm.agg[rn * AST + 32 * w] : &F.dummy[w][0];
-      s16x4 ar[4][2];
+    } else if (s > 0) {   // ---- GEMM2 (egcl.py:35-42) of tile s - 1, block b; coord_nn.2 partial dot
+      const int par = (s - 1) & 1;
+      const auto& xe = F.xe[par];
+      f32x16 hc = bias_block(sm.bias + 2 * H, b, hh);
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int rd = 0; rd < 2; ++rd) ar[k][rd] = lds_tr16(img + ibase + (16 * (k >> 1) + 4 * rd) * MIS + 16 * (k & 1));
-      f32x16 Y;
+      for (int ts = 0; ts < KS; ++ts) {
+        const f16x8 bh = ld_u4(&xe[ts][0][lane][0]), bl = ld_u4(&xe[ts][1][lane][0]);
+        hc = mfma_f16(Wt.wh[ts], bh, hc);
+        hc = mfma_f16(Wt.wh[ts], bl, hc);
+        hc = mfma_f16(Wt.wl[ts], bh, hc);
+      }
+      float part = 0.f;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const f32x4 v = ld4(dstn + 8 * g4 + 4 * hh);
+        const f32x4 w2 = ld4(sm.bias + 3 * H + 32 * b + 8 * g4 + 4 * hh);
+        const f32x4 y = silu4s((f32x4){hc[4 * g4], hc[4 * g4 + 1], hc[4 * g4 + 2], hc[4 * g4 + 3]}, c2, K2);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) Y[4 * g4 + u] = v[u];
+        for (int u = 0; u < 4; ++u) part += w2[u] * y[u];
       }
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(cat_f16x8(ar[k][0], ar[k][1]), sel[k >> 1], Y, 0, 0, 0);
-#pragma unroll
-      for (int g4 = 0; g4 < 4; ++g4)
-        st4(dstn + 8 * g4 + 4 * hh, (f32x4){Y[4 * g4], Y[4 * g4 + 1], Y[4 * g4 + 2], Y[4 * g4 + 3]});
+      part += __shfl_xor(part, 32, 64);
+      F.phip[par][b][j] = part;   // both lane halves: the same value to the same word
     }
+    STAMP(10);
+    __syncthreads();   // x0 of tile s, phi partials of tile s - 1 complete
+    STAMP(11);
+    if (stA) {
+      if (s < T) {   // ---- GEMM1: edge_nn.2 (egcl.py:20-24) of tile s, block b; act, split -> e image
+        const int par = s & 1;
+        f32x16 e = bias_block(sm.bias + H, b, hh);
+#pragma unroll
+        for (int ts = 0; ts < KS; ++ts) {
+          const f16x8 bh = ld_u4(&F.xa[ts][0][lane][0]), bl = ld_u4(&F.xa[ts][1][lane][0]);
+          e = mfma_f16(Wt.wh[ts], bh, e);
+          e = mfma_f16(Wt.wh[ts], bl, e);
+          e = mfma_f16(Wt.wl[ts], bh, e);
+        }
+        STAMP(12);
+        silu_block(e, c1, K1);
+        uint32_t o2 = 0u;
+#pragma unroll
+        for (int sl = 0; sl < 2; ++sl) {
+          f16x8 bh, bl;
+          split_f16(e, sl, bh, bl);
+          o2 = or_hi(o2, bh);
+          st_u4(&F.xe[par][2 * b + sl][0][lane][0], bh);
+          st_u4(&F.xe[par][2 * b + sl][1][lane][0], bl);
+        }
+        const uint32_t vmask = s * 32 + j < P ? ENFLOW_BIG_BITS : 0u;
+        bigw |= __ballot((o2 & vmask) != 0u) ? (uint32_t)BIGK_M : 0u;
+      }
+    } else {
+      if (s > 0) {   // message MFMAs of tile s - 1, block b
+        const int par = (s - 1) & 1, tpar = (s - 1) % 3;
+        const auto& xe = F.xe[par];
+        // message segment sums of block b on the matrix cores (edge_tiles' MMA path):
+        // agg[row(n)][32 b + f] += sum_p E[p][f] S[p][n], S[p][n] = multiplicity of p in segment n
+        u32x4v tq[4];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+          tq[qq] = *reinterpret_cast<const u32x4v*>(&F.tb[tpar][16 * (qq >> 1) + 8 * hh + 4 * (qq & 1)]);
+        const int rn = F.rt[tpar][j];
+        const int nseg = F.nseg[tpar];
+        f16x8 sel[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const u32x4v q0 = tq[2 * ks], q1 = tq[2 * ks + 1];
+          const uint32_t wv[8] = {q0[0], q0[1], q0[2], q0[3], q1[0], q1[1], q1[2], q1[3]};
+          u32x4v pk;
+#pragma unroll
+          for (int i2 = 0; i2 < 4; ++i2) {
+            const uint32_t a0 = (wv[2 * i2] & 0xffffu) == (uint32_t)j ? wv[2 * i2] >> 16 : 0u;
+            const uint32_t a1 = (wv[2 * i2 + 1] & 0xffffu) == (uint32_t)j ? wv[2 * i2 + 1] & 0xffff0000u : 0u;
+            pk[i2] = a0 | a1;
+          }
+          sel[ks] = __builtin_bit_cast(f16x8, pk);
+        }
+        const bool vn = j < nseg && rn >= 0;
+        float* const dstn = vn ? &sm.agg[rn * AST + 32 * b] : &F.dummy[b][0];
+        s16x4 ar[4][2];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int rd = 0; rd < 2; ++rd)
+            ar[k][rd] = lds_tr16(&xe[2 * b + ((lane >> 4) & 1)][k & 1][0][0] + tr_off + (16 * (k >> 1) + 4 * rd) * 4);
+        f32x16 Y;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const f32x4 v = ld4(dstn + 8 * g4 + 4 * hh);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) Y[4 * g4 + u] = v[u];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          Y = __builtin_amdgcn_mfma_f32_32x32x16_f16(cat_f16x8(ar[k][0], ar[k][1]), sel[k >> 1], Y, 0, 0, 0);
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4)
+          st4(dstn + 8 * g4 + 4 * hh, (f32x4){Y[4 * g4], Y[4 * g4 + 1], Y[4 * g4 + 2], Y[4 * g4 + 3]});
+      }
+      if (s > 0 && b == (s - 1) % NT) tile_forces(F, M, r0, P, s - 1, lane, range_bad);
+      if (s + 1 < T && b == s % NT) decode(s + 1);
+    }
+    STAMP(13);
+    __syncthreads();   // e of tile s, forces of tile s - 1, decode of tile s + 1 complete
     STAMP(14);
-    __syncthreads();   // B2: e of every block in LDS; phi partials of tile - 1 complete
-    STAMP(15);
-    if (tile > 0 && w == (tile - 1) % WAVES) tile_forces(F, M, r0, P, tile - 1, lane, range_bad);
-    STAMP(16);
-    // ---- GEMM2: coord_nn.0 (egcl.py:35-42), output block w; shadow: tile + 1's front
-    hc = bias_block(sm.bias + 2 * H, w, hh);
-    {
-      f16x8 bh[KS], bl[KS];
-#pragma unroll
-      for (int ts = 0; ts < KS; ++ts) {
-        bh[ts] = ld_u4(&F.xb[1][ts][0][lane][0]);
-        bl[ts] = ld_u4(&F.xb[1][ts][1][lane][0]);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int ts = 0; ts < KS; ++ts) {
-        hc = mfma_f16(Wt.g2h[ts], bh[ts], hc);
-        hc = mfma_f16(Wt.g2h[ts], bl[ts], hc);
-        hc = mfma_f16(Wt.g2l[ts], bh[ts], hc);
-      }
-      front(tile + 1);
-#pragma unroll
-      for (int k = 0; k < 3 * KS + 3 * KS0; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002 | 0x100 | 0x200, 6, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    STAMP(17);
   }
-  if (T > 0) dot2(hc, T - 1);
-  pre();
-  __syncthreads();
-  if (T > 0 && w == (T - 1) % WAVES) tile_forces(F, M, r0, P, T - 1, lane, range_bad);
   if (__ballot(range_bad))
     if (lane == 0) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
   if (lane == 0 && T > 0) atomicOr(&sm.big, bigw | (uint32_t)BIGK_EDGE);
   __syncthreads();
-  STAMP(18);
+  STAMP(15);
 }
 
 // ArgMax.forward (argmax.py:13-25) on the molecule: argmax_dequant's
@@ -495,7 +475,11 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
     M.a0 = A.mol_ptr[m];
     M.n = A.mol_ptr[m + 1] - M.a0;
     if (M.n > NMX || A.nf > NFMAX) {
-      if (tid == 0) atomicOr(A.err, M.n > NMX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
+      if (tid == 0) {
+        const int e = M.n > NMX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES;
+        atomicOr(A.err, e);
+        if (A.mol_err && half == 0) atomicOr(&A.mol_err[m], e);
+      }
       active = false;
     }
   }
@@ -591,14 +575,14 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
         atomicAdd(&A.stats[1], edges);
       }
       NodeFrags<H> nfr;
-      fs_edge_tiles<H, KS0>(F, Lp, L, Ml, nfl, tid_l, r0, rb, Wt, [&] {
-        if (w < H / 32) nfr.issue(W, L, lane, w);
-      } STAMP_PASS);
+      // (the node phase's fragments are requested after the tiles: issued early
+      // they would share the tiles' registers with the edge weight blocks)
+      fs_edge_tiles<H, KS0>(F, Lp, L, Ml, nfl, tid_l, r0, rb, Wt STAMP_PASS);
       STAMP(5);
-      node_phase_x3_f<H, NMX, NMX, false>(sm, Lp, L, nl, nfl, tid_l, r0, rb, nfr, true);
+      node_phase_x3_f<H, NMX, NMX, false>(sm, Lp, L, nl, nfl, tid_l, r0, rb, nfr, false);
       STAMP(6);
       if (tid == 0) {
-        if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_RANGE;
+        if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_SMALL;
         sm.big = 0u;
       }
       constexpr int AST = Smem<H, NMX, NMX>::AST;
@@ -670,12 +654,15 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
       A.g[(size_t)(M.a0 + a) * nf + q] = gv;
       bad |= (!REV && !__builtin_isfinite(hv)) || !__builtin_isfinite(gv);
     }
-    if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
+    if (bad) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
     __syncthreads();
     if (tid == 0) {
       int err = sm.err;
       if (F.timeout) err |= ENFLOW_ERR_HANDOFF;
-      if (err) atomicOr(A.err, err);
+      if (err) {
+        atomicOr(A.err, err);
+        if (A.mol_err) atomicOr(&A.mol_err[m], err);
+      }
     }
   }
   STAMP(19);
@@ -691,7 +678,10 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
   __shared__ int last;
   if (tid == 0) {
     if (s != s || !__builtin_isfinite(s)) {
-      if (active) atomicOr(A.err, ENFLOW_ERR_RANGE);
+      if (active) {
+        atomicOr(A.err, ENFLOW_ERR_RANGE);
+        if (A.mol_err) atomicOr(&A.mol_err[m], ENFLOW_ERR_RANGE);
+      }
     }
     __hip_atomic_store(&X.part[b], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -813,7 +803,7 @@ int enflow_fs_split_for(int num_mols) {
 
 bool enflow_fs_launch(int H, bool rev, int prec, int num_mols, hipStream_t st, const void* flow_args) {
   const auto& A = *static_cast<const enflow_fs::FlowArgs*>(flow_args);
-  if (H != 128 || prec != ENFLOW_PREC_F16X3 || A.tape != nullptr || A.nf > NFMAX) return false;
+  if (H != 128 || prec != ENFLOW_PREC_F16X3 || A.tape != nullptr || A.nf > NFMAX || A.mol_list != nullptr) return false;
   const int split = enflow_fs_split_for(num_mols);
   if (split == 0) return false;
   int dev = 0;
@@ -830,7 +820,7 @@ bool enflow_fs_launch(int H, bool rev, int prec, int num_mols, hipStream_t st, c
   Ak.ticket = nullptr;   // the instance reduces through its own ticket (FsArgs::ctl)
   Ak.num_mols = num_mols;   // (the reverse entry leaves it unset: whole-tile kernels index by block)
   const char* name = rev ? "lf_fs_kernel<rev>" : "lf_fs_kernel<fwd>";
-  const dim3 grid(X.blocks), blk(256);
+  const dim3 grid(X.blocks), blk(BLOCK);
 #define FS_GO(RV, SP, K0) ENFLOW_TIMED(name, st, hipLaunchKernelGGL((enflow_fs::lf_fs_kernel<128, RV, SP, K0>), grid, blk, 0, st, Ak, X))
   const bool k1 = enflow_fs::gemm0_ksteps(A.nf) == 1;   // nf <= 7 (radial in slot 7): one edge_nn.0 k-slice
   if (split == 2) {

@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 11
+#define ENFLOW_ABI 12
 #ifndef WAVES
 #define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
 #endif
@@ -1288,6 +1288,7 @@ struct MolRef {
   int a0, n;
   float rc;
   float bx, by, bz;   // the molecule's edge box = box of its first atom (base.py:130)
+  int m = 0;          // molecule index in the batch (FlowArgs::mol_list may map blocks to molecules)
 };
 
 // ---------------------------------------------------------------------------
@@ -2463,6 +2464,10 @@ struct FlowArgs {
   uint32_t* ticket = nullptr;
   float* ldj_total = nullptr;
   double ldj_cst = 0.0;
+  // ABI 12: per-molecule error words (OR of the molecule's ENFLOW_ERR_* bits; the
+  // caller zeroes them), and a molecule list (block b runs molecule mol_list[b])
+  int32_t* mol_err = nullptr;
+  const int32_t* mol_list = nullptr;
   __device__ __forceinline__ NoiseSrc noise_src() const { return NoiseSrc{noise, seed, offset}; }
 };
 
@@ -2470,14 +2475,19 @@ enum { LOAD_POS = 1, LOAD_H = 2, LOAD_VELG = 4 };
 
 template <int H, int NMAX, int RB>
 __device__ __forceinline__ bool load_molecule(Smem<H, NMAX, RB>& sm, const FlowArgs& A, MolRef& M, int what) {
-  const int m = blockIdx.x;
+  const int m = A.mol_list ? A.mol_list[blockIdx.x] : (int)blockIdx.x;
   const int tid = threadIdx.x;
+  M.m = m;
   M.a0 = A.mol_ptr[m];
   M.n = A.mol_ptr[m + 1] - M.a0;
   M.rc = 0.f;
   M.bx = M.by = M.bz = 0.f;
   if (M.n > NMAX || A.nf > NFMAX) {
-    if (tid == 0) atomicOr(A.err, M.n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES);
+    if (tid == 0) {
+      const int e = M.n > NMAX ? ENFLOW_ERR_TOO_MANY_ATOMS : ENFLOW_ERR_TOO_MANY_FEATURES;
+      atomicOr(A.err, e);
+      if (A.mol_err) atomicOr(&A.mol_err[m], e);
+    }
     return false;
   }
   const int n = M.n, nf = A.nf;

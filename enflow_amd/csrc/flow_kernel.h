@@ -64,7 +64,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
 #endif
   if (!load_molecule(sm, A, M, LOAD_POS | LOAD_H | LOAD_VELG)) {   // error raised; keep the ticket count
     if (!REV && A.ticket) {
-      if (threadIdx.x == 0) A.ldj_mol[blockIdx.x] = 0.f;
+      if (threadIdx.x == 0) A.ldj_mol[M.m] = 0.f;
       ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
     }
     return;
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       STAMP(5);
       if constexpr (PREC == PREC_F16X3) {   // every F16X3 operand kind saw a value >= 2^-7 (BIGK_*)?
         if (tid == 0) {
-          if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_RANGE;
+          if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_SMALL;
           sm.big = 0u;   // next written after this layer's / block's barriers
         }
       }
@@ -205,7 +205,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
       block_pass(0, n);   // the whole molecule in one pass
     }
     if (!REV && A.tape != nullptr && tid == 0 && A.pair_counts != nullptr)
-      A.pair_counts[(size_t)l * A.num_mols + blockIdx.x] = npairs_layer;
+      A.pair_counts[(size_t)l * A.num_mols + M.m] = npairs_layer;
     for (int a = tid; a < n; a += BLOCK) {
       const float q = sm.Q[a];
       const float eq = expf(q);
@@ -272,15 +272,24 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
     A.g[(size_t)M.a0 * nf + e] = gv;
     bad |= (!REV && !__builtin_isfinite(hv)) || !__builtin_isfinite(gv);
   }
-  if (!REV) {
-    const float s = block_sum(sm, ldj);
-    if (tid == 0) A.ldj_mol[blockIdx.x] = s;
-    bad |= tid == 0 && !__builtin_isfinite(s);
-  }
   if constexpr (PREC != PREC_F32) {
-    if (bad) atomicOr(A.err, ENFLOW_ERR_RANGE);
+    if (bad) atomicOr(&sm.err, ENFLOW_ERR_RANGE);
   }
-  if (tid == 0 && sm.err) atomicOr(A.err, sm.err);
+  bad = false;
+  if (!REV) {
+    const float s = block_sum(sm, ldj);   // (its barriers also order the err bits above)
+    if (tid == 0) A.ldj_mol[M.m] = s;
+    bad = tid == 0 && !__builtin_isfinite(s);
+  } else {
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int e = sm.err | ((PREC != PREC_F32 && bad) ? ENFLOW_ERR_RANGE : 0);
+    if (e) {
+      atomicOr(A.err, e);
+      if (A.mol_err) atomicOr(&A.mol_err[M.m], e);
+    }
+  }
   if (!REV && A.ticket) ticket_reduce_ldj(A, reinterpret_cast<double*>(sm.agg), &sm.npairs);
   STAMP(7);
   STAMP_FLUSH

@@ -74,12 +74,14 @@ class _FlowFunction(torch.autograd.Function):
                 # no host sync: the word is read at the start of this graph's
                 # backward (before anything consumes the outputs' gradients) or
                 # at the next check; an ENFLOW_ERR_RANGE then raises (the outputs
-                # were consumed already, so the step cannot be re-run)
-                _lib.defer_err(err)
+                # were consumed already, so the step cannot be re-run); an
+                # ENFLOW_ERR_SMALL alone (an operand entirely below 2^-7: ~1e-5
+                # relative, not an overflow) warns
+                _lib.defer_err(err, small_warns=True)
             else:
                 _lib.check_pending()        # an older deferred word is not this launch's
                 e = _lib.take_err(err)
-                if e == _lib.ERR_RANGE and (prec & 0xff) != _lib.PREC_F32:
+                if e and not e & ~_lib.ERR_RERUN and (prec & 0xff) != _lib.PREC_F32:
                     # a split-precision operand left its range (an fp16 overflow, or an
                     # operand entirely below 2^-7): the step's forward again with fp32
                     # GEMMs, same inputs and draws, and the fp32 backward on its tape
@@ -342,7 +344,7 @@ class _EGCLFunction(torch.autograd.Function):
                 _lib.ptr(err), None, _lib.ptr(tape), _lib.ptr(counts), prec, st), "enflow_lf_forward_f32 (EGCL tape)")
         bwd_flags = net.variant_flags()
         e = _lib.take_err(err)
-        if e == _lib.ERR_RANGE:
+        if e and not e & ~_lib.ERR_RERUN:
             # the f16x3 tape lost its range (overflow, or an operand entirely below
             # 2^-7): the tape again with fp32 GEMMs, and the fp32 backward on it
             prec = (prec & ~0xff) | _lib.PREC_F32

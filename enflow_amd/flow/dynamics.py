@@ -159,17 +159,20 @@ class LFIntegrator(BaseFlow):
     # ------------------------------------------------------------------
     def forward_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, noise,
                         ldj_mol, ldj_total, err, pair_stats=None, tape=None, pair_counts=None, prec=None,
-                        src=None, noise_key=(0, 0), ticket=None):
+                        src=None, noise_key=(0, 0), ticket=None, mol_err=None, mol_list=None):
         """Fused forward on preallocated fp32 device buffers (no host sync, no
         allocation): the entry point the benchmark times.  ``src`` = (h, g,
         pos, vel) inputs read by the kernel (None: h, g, pos, vel are updated
         in place); ``noise`` None draws the dequantiser's noise in the kernel
         (Philox keyed by ``noise_key`` = (seed, offset)); ``ticket`` (uint32
         device word, zero) reduces log|detJ| in the same launch
-        (enflow_lf_forward_io_f32).  Molecules past the fused kernel's LDS
-        image (> enflow_max_atoms()) go through the layer-by-layer
-        large-system kernels (enflow_lf_forward_large_f32; needs a workspace,
-        allocated once per shape)."""
+        (enflow_lf_forward_io_f32).  ``mol_err`` (int32 [M], zeroed) receives
+        each molecule's error bits and ``mol_list`` (int32 device tensor) runs
+        only those molecules, in place (enflow_lf_forward_io2_f32, ABI 12).
+        Molecules past the fused kernel's LDS image (> enflow_max_atoms()) go
+        through the layer-by-layer large-system kernels
+        (enflow_lf_forward_large_f32; needs a workspace, allocated once per
+        shape; no per-molecule words there)."""
         hid, nf, cw = self._geometry()
         kind = self._dequant_kind()
         dev = h.device
@@ -197,17 +200,21 @@ class LFIntegrator(BaseFlow):
                 "enflow_lf_forward_large_f32")
             return
         si = (None,) * 4 if src is None else tuple(_lib.ptr(t) for t in src)
-        _lib.check(L.enflow_lf_forward_io_f32(
-            mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
-            _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
-            _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
-            _lib.ptr(noise), int(noise_key[0]) & 0xFFFFFFFFFFFFFFFF, int(noise_key[1]) & 0xFFFFFFFFFFFFFFFF,
-            scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total), _lib.ptr(ticket),
-            _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), prec,
-            _lib.stream_ptr(dev)), "enflow_lf_forward_io_f32")
+        args = (mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid,
+                _lib.ptr(mol_ptr), _lib.ptr(r_cut), _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos),
+                _lib.ptr(vel), _lib.ptr(self.packed_layers(dev)), len(self.networks), kind, _lib.ptr(dq),
+                _lib.ptr(noise), int(noise_key[0]) & 0xFFFFFFFFFFFFFFFF, int(noise_key[1]) & 0xFFFFFFFFFFFFFFFF,
+                scale, float(self.dt), cw, _lib.ptr(ldj_mol), _lib.ptr(ldj_total), _lib.ptr(ticket),
+                _lib.ptr(err), _lib.ptr(pair_stats), _lib.ptr(tape), _lib.ptr(pair_counts), prec)
+        if mol_err is None and mol_list is None:
+            _lib.check(L.enflow_lf_forward_io_f32(*args, _lib.stream_ptr(dev)), "enflow_lf_forward_io_f32")
+        else:
+            _lib.check(L.enflow_lf_forward_io2_f32(
+                *args, _lib.ptr(mol_err), _lib.ptr(mol_list), 0 if mol_list is None else mol_list.numel(),
+                _lib.stream_ptr(dev)), "enflow_lf_forward_io2_f32")
 
     def reverse_buffers(self, h, g, pos, vel, box, r_cut, mol_ptr, max_mol_atoms, argmax_idx, max_idx, err,
-                        src=None, prec=None):
+                        src=None, prec=None, mol_err=None, mol_list=None):
         """Fused reverse on preallocated fp32 device buffers (no host sync, no
         allocation); ``src`` = (h, g, pos, vel) inputs (None: in place); with
         ArgMax, argmax_idx / max_idx receive the dequantiser's indices
@@ -230,12 +237,16 @@ class LFIntegrator(BaseFlow):
                 _lib.stream_ptr(h.device)), "enflow_lf_reverse_large_f32")
             return
         si = (None,) * 4 if src is None else tuple(_lib.ptr(t) for t in src)
-        _lib.check(L.enflow_lf_reverse_io_f32(
-            mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
-            _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
-            _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
-            _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), prec, _lib.stream_ptr(h.device)),
-            "enflow_lf_reverse_io_f32")
+        args = (mol_ptr.numel() - 1, h.shape[0], max_mol_atoms, nf, hid, _lib.ptr(mol_ptr), _lib.ptr(r_cut),
+                _lib.ptr(box), *si, _lib.ptr(h), _lib.ptr(g), _lib.ptr(pos), _lib.ptr(vel),
+                _lib.ptr(self.packed_layers(h.device)), len(self.networks), kind, float(self.dt), cw,
+                _lib.ptr(argmax_idx), _lib.ptr(max_idx), _lib.ptr(err), prec)
+        if mol_err is None and mol_list is None:
+            _lib.check(L.enflow_lf_reverse_io_f32(*args, _lib.stream_ptr(h.device)), "enflow_lf_reverse_io_f32")
+        else:
+            _lib.check(L.enflow_lf_reverse_io2_f32(
+                *args, _lib.ptr(mol_err), _lib.ptr(mol_list), 0 if mol_list is None else mol_list.numel(),
+                _lib.stream_ptr(h.device)), "enflow_lf_reverse_io2_f32")
 
     def _state(self, data):
         """Kernel inputs (fp32, contiguous, on the device: views of the data's
@@ -283,18 +294,39 @@ class LFIntegrator(BaseFlow):
         prec = self._prec()
         if check_errors:
             _lib.check_pending()     # an older deferred error is not this launch's
+        # per-molecule error words (fused path): a split-precision flag names its molecules
+        mol_err = (torch.zeros(max(M, 1), dtype=torch.int32, device=dev)
+                   if check_errors and not _lib.is_large(s["max_n"]) else None)
+        mol_list = None
         while True:
             self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
                                  s["max_n"], noise, ldj_mol, ldj, st[:1], src=s["src"], noise_key=key,
-                                 ticket=st[1:], prec=prec)
+                                 ticket=st[1:] if mol_list is None else None, prec=prec, mol_err=mol_err,
+                                 mol_list=mol_list)
             if not check_errors:
                 break
             e = _lib.take_err(st[:1])
+            if e & _lib.ERR_HANDOFF and not e & ~(_lib.ERR_HANDOFF | _lib.ERR_RERUN):
+                with _split_off():   # the two-workgroup instance lost a partner: the whole launch without it
+                    if mol_err is not None:
+                        mol_err.zero_()
+                    self.forward_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
+                                         s["max_n"], noise, ldj_mol, ldj, st[:1], src=s["src"], noise_key=key,
+                                         ticket=st[1:], prec=prec, mol_err=mol_err)
+                e = _lib.take_err(st[:1])
             if _retry_fp32(e, prec):
-                # a split-precision operand left its range: the same launch with fp32
-                # GEMMs (same noise key, same inputs) returns the reference's result
+                # a split-precision operand left its range (or was entirely small): the
+                # same molecules with fp32 GEMMs (same noise elements, same inputs) give
+                # the reference's result -- only the flagged molecules when the words
+                # name few of them, else the whole launch
                 prec = _fp32_prec(prec)
                 _lib.FP32_RERUNS[0] += 1
+                if mol_err is not None:
+                    flagged = torch.nonzero(mol_err[:M] & _lib.ERR_RERUN).flatten().to(torch.int32)
+                    if 0 < flagged.numel() <= max(1, M // 4):
+                        mol_list = flagged.contiguous()
+                        _lib.FP32_MOL_RERUNS[0] += mol_list.numel()
+                    mol_err.zero_()
                 continue
             _lib.raise_code(e)
             break
@@ -318,19 +350,42 @@ class LFIntegrator(BaseFlow):
         prec = self._prec()
         if check_errors:
             _lib.check_pending()
+        M = s["mol_ptr"].numel() - 1
+        mol_err = (torch.zeros(max(M, 1), dtype=torch.int32, device=dev)
+                   if check_errors and not _lib.is_large(s["max_n"]) else None)
+        mol_list = None
         while True:
             self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
-                                 s["max_n"], idx, mx, err, src=s["src"], prec=prec)
+                                 s["max_n"], idx, mx, err, src=s["src"], prec=prec, mol_err=mol_err,
+                                 mol_list=mol_list)
             if not check_errors:
                 break
             e = _lib.take_err(err)
-            if _retry_fp32(e, prec):     # as in forward: re-run with fp32 GEMMs
+            if e & _lib.ERR_HANDOFF and not e & ~(_lib.ERR_HANDOFF | _lib.ERR_RERUN):
+                with _split_off():
+                    if mol_err is not None:
+                        mol_err.zero_()
+                    mx.zero_()
+                    self.reverse_buffers(s["h"], s["g"], s["pos"], s["vel"], s["box"], s["r_cut"], s["mol_ptr"],
+                                         s["max_n"], idx, mx, err, src=s["src"], prec=prec, mol_err=mol_err)
+                e = _lib.take_err(err)
+            if _retry_fp32(e, prec):     # as in forward: re-run the flagged molecules (or all) with fp32 GEMMs
                 prec = _fp32_prec(prec)
-                mx.zero_()
                 _lib.FP32_RERUNS[0] += 1
+                if mol_err is not None:
+                    flagged = torch.nonzero(mol_err[:M] & _lib.ERR_RERUN).flatten().to(torch.int32)
+                    if 0 < flagged.numel() <= max(1, M // 4):
+                        mol_list = flagged.contiguous()
+                        _lib.FP32_MOL_RERUNS[0] += mol_list.numel()
+                    mol_err.zero_()
+                if mol_list is None:
+                    mx.zero_()
                 continue
             _lib.raise_code(e)
             break
+        if mol_list is not None and kind == _lib.DEQUANT_ARGMAX:
+            # the first launch's batch maximum saw the flagged molecules' f16x3 argmax
+            mx.copy_(idx[:n].max().reshape(1) if n > 0 else mx)
         dt = data.h.dtype
         if kind == _lib.DEQUANT_ARGMAX:
             width = int(mx.item()) + 1
@@ -346,9 +401,21 @@ class LFIntegrator(BaseFlow):
 
 
 def _retry_fp32(e, prec):
-    """The launch's own word says only ENFLOW_ERR_RANGE and the GEMMs were not
-    fp32 yet: re-run with fp32 GEMMs (any other bit is raised as is)."""
-    return e == _lib.ERR_RANGE and (prec & 0xff) != _lib.PREC_F32
+    """The launch's own word says only ENFLOW_ERR_RANGE / ENFLOW_ERR_SMALL and
+    the GEMMs were not fp32 yet: re-run with fp32 GEMMs (any other bit is raised
+    as is)."""
+    return e != 0 and not e & ~_lib.ERR_RERUN and (prec & 0xff) != _lib.PREC_F32
+
+
+class _split_off:
+    """Every loaded library without the two-workgroup latency instance for one
+    launch (ENFLOW_ERR_HANDOFF: a partner workgroup was not co-resident)."""
+
+    def __enter__(self):
+        self.prev = _lib.set_split_threshold(0)
+
+    def __exit__(self, *exc):
+        _lib.set_split_threshold(-1 if self.prev is None else self.prev)
 
 
 def _fp32_prec(prec):

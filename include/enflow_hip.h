@@ -37,10 +37,13 @@ extern "C" {
 #define ENFLOW_ERR_FEW_IMAGES       2  /* reference would IndexError (base.py:137) */
 #define ENFLOW_ERR_TOO_MANY_FEATURES 4
 #define ENFLOW_ERR_RANGE            8  /* f16x3 / bf16 GEMM path produced a non-finite output
-                                          (an operand past the fp16 / bf16 range), or (ABI 11,
-                                          f16x3) a GEMM operand of a molecule / row block was
-                                          entirely below 2^-7 in magnitude (its fp16 lo parts
-                                          subnormal): rerun with ENFLOW_PREC_F32 */
+                                          (an operand past the fp16 / bf16 range): rerun with
+                                          ENFLOW_PREC_F32 */
+#define ENFLOW_ERR_SMALL           16  /* ABI 12 (ABI 11 reported it as ENFLOW_ERR_RANGE): an f16x3 GEMM
+                                          operand of a molecule / row block was entirely below 2^-7
+                                          in magnitude (its fp16 lo parts subnormal, ~1e-5 relative
+                                          error): a precision warning, not an overflow; rerun with
+                                          ENFLOW_PREC_F32 for the fp32-accurate result */
 #define ENFLOW_ERR_HANDOFF         32  /* ABI 12: a two-workgroup latency launch (enflow_set_split_threshold)
                                           timed out waiting for its partner workgroup (not co-resident):
                                           outputs invalid, rerun with the split instance off */
@@ -66,7 +69,9 @@ extern "C" {
  * kinds (enflow_pack_egcl_act_f32, the ArgMax activation trailer), node_nf up to 16 in
  * libenflow_hip_nf16.so; 11: ENFLOW_ERR_RANGE also flags an f16x3 GEMM operand that is entirely
  * small, ENFLOW_BWD_F32 -- the fp32-GEMM backward for a tape recorded by an ENFLOW_PREC_F32
- * forward). */
+ * forward); 12: ENFLOW_ERR_SMALL split from ENFLOW_ERR_RANGE, ENFLOW_ERR_HANDOFF, the feature-split
+ * latency instance (enflow_set_split_threshold / enflow_set_fs_threshold), per-molecule error words
+ * and molecule lists (enflow_lf_forward_io2_f32 / enflow_lf_reverse_io2_f32). */
 int enflow_abi_version(void);
 
 /* Batches of <= 32-atom molecules with at most this many molecules run the
@@ -271,6 +276,40 @@ int enflow_lf_reverse_io_f32(int num_mols, int num_atoms, int max_mol_atoms, int
                              int dequant_kind, float dt, float coords_weight,
                              int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
                              int gemm_precision, void* stream);
+
+/* ABI 12: enflow_lf_forward_io_f32 / enflow_lf_reverse_io_f32 with
+ *   mol_err   (optional, [num_mols], zeroed by the caller): each molecule's own
+ *             ENFLOW_ERR_* bits (err_flag keeps the OR over the batch), so a
+ *             split-precision range / small-operand flag names its molecules;
+ *   mol_list  (optional, [num_listed]): run only these molecules of the batch,
+ *             reading and writing their atoms in place of a full launch (the
+ *             same noise elements: Philox counters are keyed by the batch's
+ *             atom index); the forward then reduces ldj_total over all
+ *             num_mols entries of ldj_mol (ticket must be NULL).
+ * The host mirror re-runs only the flagged molecules with ENFLOW_PREC_F32
+ * (the reference's result) instead of the whole batch.  Molecules past
+ * enflow_max_atoms() are not accepted here (-3). */
+int enflow_lf_forward_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                              const int32_t* mol_ptr, const float* r_cut, const float* box,
+                              const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                              float* h, float* g, float* pos, float* vel,
+                              const float* layers, int n_layers,
+                              int dequant_kind, const float* dequant, const float* noise,
+                              uint64_t noise_seed, uint64_t noise_offset,
+                              float dequant_scale, float dt, float coords_weight,
+                              float* ldj_mol, float* ldj_total, uint32_t* ticket, int32_t* err_flag,
+                              uint64_t* pair_stats, float* tape, int32_t* pair_counts,
+                              int gemm_precision, int32_t* mol_err, const int32_t* mol_list, int num_listed,
+                              void* stream);
+int enflow_lf_reverse_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, int node_nf, int hidden_nf,
+                              const int32_t* mol_ptr, const float* r_cut, const float* box,
+                              const float* h_in, const float* g_in, const float* pos_in, const float* vel_in,
+                              float* h, float* g, float* pos, float* vel,
+                              const float* layers, int n_layers,
+                              int dequant_kind, float dt, float coords_weight,
+                              int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag,
+                              int gemm_precision, int32_t* mol_err, const int32_t* mol_list, int num_listed,
+                              void* stream);
 
 /* ------------------------------------------------------------------------
  * Large systems: molecules / periodic boxes with more than enflow_max_atoms()

@@ -404,17 +404,19 @@ def test_bench_config_f32_gemms_sampled_vs_oracle(bench_run, kernel_instance):
 
 @pytest.mark.parametrize("mols", [6, 1024])
 def test_kernel_instance_selected(mols, kernel_instance):
+    # (split: 6 molecules take two workgroups per molecule, 1024 one)
     """The latency threshold routes a <= 32-atom batch to the instance under
     test (kernel names from the per-launch HIP-event timing)."""
     from enflow_amd import _lib
     from enflow_amd.data import Data
     from enflow_amd.data.synthetic import make_molecules, default_dt
     b = _f32(make_molecules(mols, 22, nf=5, seed=5))
-    model = _make_model(32, 5, 2, 3, default_dt())
+    model = _make_model(128 if kernel_instance == "split" else 32, 5, 2, 3, default_dt())
     with _lib.KernelTimer() as t, torch.no_grad():
         model(Data.from_arrays(b, device=DEV))
     names = set(t.stats)
-    want = "lf_flow_kernel<fwd,lat>" if kernel_instance == "8-wave" else "lf_flow_kernel<fwd>"
+    want = {"8-wave": "lf_flow_kernel<fwd,lat>", "split": "lf_fs_kernel<fwd>"}.get(kernel_instance,
+                                                                                   "lf_flow_kernel<fwd>")
     print(f"[{kernel_instance}] {mols} molecules ran {sorted(names)}")
     assert want in names, names
 
@@ -630,3 +632,61 @@ def test_clamp_propagates_nan_like_torch():
         assert not np.isnan(ref[k][fin]).any(), k
         assert rel_err(got[fin], ref[k][fin]) < TOL, k               # finite outputs are the reference's
     assert np.isnan(ref["vel"]).any(axis=1).sum() > 1                # F of the NaN atom's partners too
+
+
+@pytest.mark.parametrize("mols", [128, 7])
+def test_split_instance_strong_scaling_batch_vs_oracle(mols):
+    """The strong-scaling shard of BASELINE configs[1] (1024 x 22 split over 8
+    GPUs: 128 molecules per GPU, H = 128, 8 layers, f16x3) runs the
+    two-workgroups-per-molecule instance by default (enflow_split.hip: rows
+    split over the pair, one position / feature hand-off per layer): forward,
+    log|detJ| and reverse of sampled molecules against the oracle, bitwise
+    reproducible, and within round-off of the whole-tile 4-wave instance."""
+    from enflow_amd import _lib
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    b = _f32(make_molecules(mols, 22, nf=5, seed=77))
+    model = _make_model(128, 5, 8, 7, default_dt())
+    d = Data.from_arrays(b, device=DEV)
+    noise = torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(3))
+    prev = (_lib.set_latency_threshold(-1), _lib.set_split_threshold(-1), _lib.set_fs_threshold(-1))
+    try:
+        with _lib.KernelTimer() as t, torch.no_grad():
+            o1, l1 = model(d.clone(), noise=noise)
+            o2, l2 = model(d.clone(), noise=noise)
+            back = model.reverse(o1.clone())
+        assert "lf_fs_kernel<fwd>" in t.stats and "lf_fs_kernel<rev>" in t.stats, sorted(t.stats)
+        _lib.set_split_threshold(0)
+        _lib.set_latency_threshold(0)
+        with torch.no_grad():
+            o4, l4 = model(d.clone(), noise=noise)
+    finally:
+        _lib.set_latency_threshold(-1 if prev[0] is None else prev[0])
+        _lib.set_split_threshold(-1 if prev[1] is None else prev[1])
+        _lib.set_fs_threshold(-1 if prev[2] is None else prev[2])
+    for k in ("h", "g", "pos", "vel"):
+        assert torch.equal(getattr(o1, k), getattr(o2, k)), k
+    assert torch.equal(l1, l2)
+    worst = {k: 0.0 for k in ("h", "g", "pos", "vel")}
+    worst_r = {k: 0.0 for k in ("g", "pos", "vel")}
+    layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+    for m in sorted(set(list(range(0, mols, 16)) + [mols - 1])):
+        sub, a0, a1 = _sub(b, m)
+        ref, _ = _oracle_flow(model, sub, noise[a0:a1])
+        for k in worst:
+            worst[k] = worst_of([worst[k], rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k])])
+        st = {k: getattr(o1, k)[a0:a1].cpu().double().numpy() for k in ("h", "g", "pos", "vel")}
+        st.update(box=sub["box"], r_cut=sub["r_cut"], mol_ptr=sub["mol_ptr"])
+        rref = O.lf_reverse(layers, st, model.dt)
+        np.testing.assert_array_equal(np.argmax(back.h[a0:a1].cpu().numpy(), 1), np.argmax(rref["h"], 1))
+        for k in worst_r:
+            worst_r[k] = worst_of([worst_r[k], rel_err(getattr(back, k)[a0:a1].cpu().numpy(), rref[k])])
+    _, ref_ldj = _oracle_flow(model, b, noise)
+    ldj_err = abs(float(l1) - ref_ldj) / abs(ref_ldj)
+    vs4 = {k: rel_err(getattr(o1, k).cpu().numpy(), getattr(o4, k).cpu().numpy()) for k in ("h", "g", "pos", "vel")}
+    print(f"split instance, {mols} molecules: forward vs oracle", fmt(worst), "reverse", fmt(worst_r),
+          f"ldj {ldj_err:.2e}", "vs 4-wave", fmt(vs4))
+    assert_all_within(worst, TOL)
+    assert_all_within(worst_r, TOL)
+    assert ldj_err < TOL
+    assert_all_within(vs4, 1e-6)

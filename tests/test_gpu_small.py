@@ -1,11 +1,13 @@
-"""f16x3 at small operand magnitudes and the fp32 re-run on ENFLOW_ERR_RANGE.
+"""f16x3 at small operand magnitudes and the fp32 re-run on ENFLOW_ERR_SMALL.
 
 The f16x3 split x = hi + lo keeps fp32 accuracy only while lo = x - hi is a
 normal fp16 (|x| >~ 2^-3); the weights carry a power-of-two scale, the
 activation operands do not.  The kernels record per molecule and layer
 whether every GEMM operand kind (edge_nn.0 / edge_nn.2 / coord_nn.0 / node
 inputs) reached 2^-7 somewhere (flow_device.h, BIGK_*); one that never did
-flags ENFLOW_ERR_RANGE, and the host re-runs the launch with fp32 GEMMs --
+flags ENFLOW_ERR_SMALL (ABI 12; ENFLOW_ERR_RANGE before), and the host re-runs
+with fp32 GEMMs -- only the flagged molecules when they are few (per-molecule
+error words, enflow_lf_forward_io2_f32),
 inference (dynamics.py) and, since ABI 11, training: the step's forward
 again in fp32 and the fp32-GEMM backward (ENFLOW_BWD_F32) on its tape.
 
@@ -102,7 +104,7 @@ def _raw_launch_flagged(model, b, u):
 def test_f16x3_small_operands_forward_reverse(scale, where, kernel_instance):
     """Forward and reverse at the default f16x3 precision vs the float64 oracle
     (1e-5).  At 1e-3 / 1e-4 every value of one operand kind is below 2^-7: the
-    raw launch must flag ENFLOW_ERR_RANGE and the module call re-runs in fp32.
+    raw launch must flag ENFLOW_ERR_SMALL and the module call re-runs in fp32.
     Near the threshold (1e-2 .. 1e-1 scales the largest values sit around
     2^-7 .. 2^-3) a launch may or may not flag; one that does not must itself
     meet the bar (the raw f16x3 outputs vs the oracle)."""
@@ -131,7 +133,7 @@ def test_f16x3_small_operands_forward_reverse(scale, where, kernel_instance):
     print(f"[{kernel_instance}] small operands {where} x{scale:g}: raw f16x3 flag={code} "
           f"(raw outputs {fmt(raw_errs)}), forward re-run={reran}, reverse re-run={rev_reran}:", fmt({**errs, **rerr}))
     if scale <= 1e-3:
-        assert code == _lib.ERR_RANGE, "an operand entirely below 2^-7 was not flagged"
+        assert code == _lib.ERR_SMALL, "an operand entirely below 2^-7 was not flagged (ENFLOW_ERR_SMALL)"
         assert reran == 1 and rev_reran == 1
     if code == 0:
         assert_all_within(raw_errs, TOL, "unflagged raw f16x3 launch")
@@ -249,9 +251,11 @@ def test_fp32_precision_trains_with_the_fp32_backward():
     assert_all_within(worst, GRAD_TOL)
 
 
-def test_deferred_training_check_raises_range_error():
+def test_deferred_training_check_small_warns_overflow_raises():
     """defer_error_check=True (no host sync in the forward) cannot re-run a step
-    whose outputs were already consumed: the RangeError is raised at backward."""
+    whose outputs were already consumed.  ADVICE r4: an operand entirely below
+    2^-7 (ENFLOW_ERR_SMALL, a precision loss of ~1e-5 relative) warns at
+    backward; a real fp16 overflow (ENFLOW_ERR_RANGE) raises RangeError there."""
     from enflow_amd import _lib
     from enflow_amd.flow import Alchemical_NLL
     from enflow_amd.data import Data
@@ -262,7 +266,85 @@ def test_deferred_training_check_raises_range_error():
     u = torch.rand(b["h"].shape, device=DEV)
     out, ldj = model(Data.from_arrays(b, device=DEV), noise=u)
     loss = Alchemical_NLL(kBT=default_kBT(), softening=0.1)(out, ldj)
+    with pytest.warns(RuntimeWarning, match="below 2\\^-7"):
+        loss.backward()
+        _lib.check_pending()
+    assert not _lib._pending
+    model, b = _range_train_model_and_batch()
+    model.defer_error_check = True
+    u = torch.rand(b["h"].shape, device=DEV)
+    out, ldj = model(Data.from_arrays(b, device=DEV), noise=u)
+    loss = Alchemical_NLL(kBT=default_kBT(), softening=0.1)(out, ldj)
     with pytest.raises(_lib.RangeError):
         loss.backward()
     _lib.check_pending()
     assert not _lib._pending
+
+
+def test_one_small_molecule_reruns_only_itself():
+    """a BASELINE configs[1]-shaped batch (1024 x 22 atoms,
+    H = 128, 8 layers, f16x3) in which ONE molecule's GEMM0 operands are all
+    ~1e-4 (features and geometry scaled down: the same neighbour list at 1e-3
+    of the size).  The kernel names that molecule in its per-molecule error
+    word (ENFLOW_ERR_SMALL); the host re-runs only it with fp32 GEMMs (in place,
+    same noise elements) and reduces log|detJ| over the batch.  Sampled
+    molecules including the small one match the float64 oracle at 1e-5, and
+    the module call's time is printed beside the clean batch's."""
+    import time
+    from enflow_amd import _lib
+    from enflow_amd.nn import EGCL, Floor
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules, default_dt
+    k = 517
+    base = _f32(make_molecules(1024, 22, nf=5, seed=61))
+    rng = np.random.default_rng(62)
+    base["h"] = _f32({**base, "h": np.floor(rng.uniform(0, 3, size=base["h"].shape))})["h"]
+    small = {kk: (v.copy() if isinstance(v, np.ndarray) else v) for kk, v in base.items()}
+    a0, a1 = int(base["mol_ptr"][k]), int(base["mol_ptr"][k + 1])
+    for key, f in (("h", 1e-4), ("g", 1e-4), ("pos", 1e-3), ("vel", 1e-3), ("box", 1e-3)):
+        small[key][a0:a1] = small[key][a0:a1] * f
+    small["r_cut"][k] = small["r_cut"][k] * 1e-3
+    small = _f32(small)
+    torch.manual_seed(63)
+    model = LFIntegrator([EGCL(5, 5, 128) for _ in range(8)], Floor(dequant_scale=1e-4), dt=default_dt()).to(DEV)
+    u = torch.rand(base["h"].shape, device=DEV, generator=torch.Generator(DEV).manual_seed(64))
+
+    def run(b, reps=1):
+        d = Data.from_arrays(b, device=DEV)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            with torch.no_grad():
+                o, ldj = model(d.clone(), noise=u)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return o, ldj, float(np.median(ts)) * 1e3
+
+    run(base, 3)
+    n0, m0 = _lib.FP32_RERUNS[0], _lib.FP32_MOL_RERUNS[0]
+    o, ldj, _ = run(small)
+    reruns, mol_reruns = _lib.FP32_RERUNS[0] - n0, _lib.FP32_MOL_RERUNS[0] - m0
+    _, _, t_clean = run(base, 9)
+    _, _, t_small = run(small, 9)
+    model.gemm_precision = "f32"     # what the whole-batch fp32 re-run (ABI <= 11) cost on top of the clean call
+    _, _, t_f32 = run(base, 5)
+    model.gemm_precision = "f16x3"
+    ref, ref_ldj = _oracle_fwd(model, small, u)
+    worst = {kk: 0.0 for kk in ("h", "g", "pos", "vel")}
+    for m in sorted(set(list(range(0, 1024, 64)) + [k, 1023])):
+        b0, b1 = int(small["mol_ptr"][m]), int(small["mol_ptr"][m + 1])
+        for kk in worst:
+            worst[kk] = worst_of([worst[kk], rel_err(getattr(o, kk)[b0:b1].cpu().numpy(), ref[kk][b0:b1])])
+    err_k = {kk: rel_err(getattr(o, kk)[a0:a1].cpu().numpy(), ref[kk][a0:a1]) for kk in worst}
+    ldj_err = scalar_rel(ldj, ref_ldj)
+    print(f"one small molecule in 1024: re-runs {reruns} ({mol_reruns} molecule), sampled vs oracle {fmt(worst)}, "
+          f"the small molecule {fmt(err_k)}, ldj {ldj_err:.2e}; module call {t_small:.3f} ms vs clean batch "
+          f"{t_clean:.3f} ms ({t_small / t_clean:.2f}x; a whole-batch fp32 re-run would add {t_f32:.3f} ms: "
+          f"{(t_clean + t_f32) / t_clean:.2f}x)")
+    assert reruns == 1 and mol_reruns == 1
+    assert t_small < t_clean + t_f32
+    assert_all_within(worst, TOL, "sampled molecules")
+    assert_all_within(err_k, TOL, "the small molecule")
+    assert ldj_err < TOL

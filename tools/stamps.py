@@ -14,8 +14,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "enflow_amd", "libenflow_hip_stamps.so")
 FS_PHASES = ["load", "dequant", "layer:weights+rev", "pairs:images+idmap", "pairs:counts+compact", "(after tiles)",
-             "node", "update", "exchange", "  tiles:setup", "  decode+gemm0+act+xw", "  B1 wait", "  forces",
-             "  gemm1", "  act1+split+ew", "  msg mma", "  B2 wait", "  gemm2+dot", "  tail", "writeback"]
+             "node", "update", "exchange", "  tiles:setup+decode0", "  A gemm0+act+split", "  barrier X",
+             "  A gemm1", "  A act+split", "  barrier Y", "  tail", "-", "-", "-", "writeback"]
 PHASES = ["load", "dequant", "pairs:counts+compact", "pairs:images+idmap", "edge_tiles(all)", "node", "update", "writeback",
           "  tiles:setup", "  gemm0", "  silu0", "  gemm1", "  silu1", "  segsum", "  gemm2+phi+force", "  tail-barrier"]
 
