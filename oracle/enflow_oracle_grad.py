@@ -108,15 +108,19 @@ def _nll(h, g, pos, vel, ldj, mol_ptr, kBT, softening, partition_func):
 
 
 def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partition_func=10.0,
-                         coords_weight=1.0, dequant_kind="argmax"):
+                         coords_weight=1.0, dequant_kind="argmax", dtype=torch.float64):
     """Loss of one training step and d loss / d parameter for every EGCL layer
     (list of dicts, EGCL_PARAM_NAMES) and the ArgMax dequantiser (dict).
     dequant_kind "floor" (enflow/nn/floor.py:15-16): h + dequant_scale * eps with
     eps the U[0, 1) draw, log|detJ| starts at 0; ``dequant`` is then the scale
     and the dequantiser gradient dict is empty.
 
+    dtype: the arithmetic (default float64, the reference's; float32 measures
+    what rounding alone does to the gradients -- the neighbour lists are then
+    still built from float64 positions, so both runs see the same edges).
+
     Returns (loss, ldj, [layer grad dicts], dequant grad dict, output state)."""
-    t = lambda a: torch.tensor(np.asarray(a, dtype=np.float64))  # noqa: E731
+    t = lambda a: torch.tensor(np.asarray(a, dtype=np.float64)).to(dtype)  # noqa: E731
     P = [{k: t(v).requires_grad_(True) for k, v in p.items() if k not in ("flags", "act")} for p in layers]
     floor = dequant_kind == "floor"
     D = {} if floor else {k: t(v).requires_grad_(True) for k, v in dequant.items() if k != "act"}
@@ -129,7 +133,7 @@ def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partit
         h, ldj = _argmax(D, t(state["h"]), t(eps), dequant.get("act"))
     g, pos, vel = t(state["g"]), t(state["pos"]), t(state["vel"])
     for p, lp in zip(P, layers):
-        row, col, eb = O.batch_edges(pos.detach().numpy(), state["box"], r_cut, mol_ptr)
+        row, col, eb = O.batch_edges(pos.detach().double().numpy(), state["box"], r_cut, mol_ptr)
         row_t, col_t = torch.as_tensor(row, dtype=torch.long), torch.as_tensor(col, dtype=torch.long)
         q, f, gg = _egcl(p, h, pos, row_t, col_t, t(eb), n, coords_weight, lp.get("flags", (0, 0, 0)), lp.get("act"))
         vel = torch.exp(q) * vel + f * dt
@@ -139,8 +143,8 @@ def train_loss_and_grads(layers, dequant, state, eps, dt, kBT, softening, partit
         ldj = ldj + q.sum()
     loss = _nll(h, g, pos, vel, ldj, mol_ptr, kBT, softening, partition_func)
     loss.backward()
-    gl = [{k: v.grad.numpy() for k, v in p.items()} for p in P]
-    gd = {k: v.grad.numpy() for k, v in D.items()}
-    out = {"h": h.detach().numpy(), "g": g.detach().numpy(), "pos": pos.detach().numpy(),
-           "vel": vel.detach().numpy()}
+    gl = [{k: v.grad.double().numpy() for k, v in p.items()} for p in P]
+    gd = {k: v.grad.double().numpy() for k, v in D.items()}
+    out = {"h": h.detach().double().numpy(), "g": g.detach().double().numpy(), "pos": pos.detach().double().numpy(),
+           "vel": vel.detach().double().numpy()}
     return float(loss), float(ldj), gl, gd, out

@@ -20,7 +20,7 @@ from _fixtures import (load, flow_from_fixture, data_from_fixture, egcl_from_fix
 # 4-wave throughput build and the 8-wave latency build)
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
 TOL = 1e-5
-GRAD_TOL = 1e-4
+GRAD_TOL = 5e-5   # <= 2x the fp32 floor measured on these batches (tools/grad_precision.py, profiles/r05)
 DEV = "cuda:0"
 ACTS = ["relu", "leaky", "elu", "celu", "selu", "gelu", "gelutanh", "tanh", "sigmoid", "softplus", "mish",
         "relu6", "identity"]

@@ -94,7 +94,7 @@ def test_large_flow_forward_and_roundtrip(prec):
 def test_training_past_64_atoms_vs_oracle():
     """Molecules of 65..256 atoms (the row-blocked kernels' range at inference)
     train through the large-system tape and backward: gradients of a ragged
-    [100, 22] batch vs the float64 gradient oracle, 1e-4 normwise."""
+    [100, 22] batch vs the float64 gradient oracle, 5e-5 normwise."""
     from oracle import enflow_oracle_grad as OG
     from enflow_amd.data import Data
     from enflow_amd.flow import Alchemical_NLL
@@ -114,7 +114,7 @@ def test_training_past_64_atoms_vs_oracle():
             for i, n in enumerate(model.networks) for k, p in n.named_parameters()}
     errs.update({f"dq.{k}": nw(p.grad.cpu().double().numpy(), gd[k]) for k, p in model.dequantize.named_parameters()})
     print("100+22-atom training: max normwise grad err", f"{worst_of(errs):.2e}")
-    assert_all_within(errs, 1e-4)
+    assert_all_within(errs, 5e-5)
 
 
 # ---------------------------------------------------------------------------

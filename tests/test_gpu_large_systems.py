@@ -239,7 +239,7 @@ def test_large_training_gradients_vs_oracle(sizes, hid, nl, variants):
     enflow/main.py:212-223): loss.backward() through the large-system forward
     (tape) and backward (enflow_lf_backward_large_f32) vs the float64 gradient
     oracle (oracle/enflow_oracle_grad.py, pinned to the reference's
-    loss.backward() goldens), 1e-4 normwise per parameter tensor."""
+    loss.backward() goldens), 5e-5 normwise per parameter tensor."""
     from oracle import enflow_oracle_grad as OG
     b = _boxes(sizes, 41)
     model = _model(hid, 5, nl, 42, **variants)
@@ -258,7 +258,7 @@ def test_large_training_gradients_vs_oracle(sizes, hid, nl, variants):
         errs[f"dq.{k}"] = normwise(p.grad.cpu().numpy(), gd[k])
     worst = max(errs, key=lambda k: (not np.isfinite(errs[k]), errs[k]))
     print(f"large training {sizes} H={hid} L={nl}: max normwise grad err {errs[worst]:.2e} ({worst})")
-    bad = {k: v for k, v in errs.items() if not v <= 1e-4}
+    bad = {k: v for k, v in errs.items() if not v <= 5e-5}
     assert not bad, bad
 
 

@@ -14,7 +14,7 @@ from _fixtures import load, egcl_from_fixture, data_from_fixture, ARGMAX_KEYS, n
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-GRAD_TOL = 1e-4
+GRAD_TOL = 5e-5   # <= 2x the fp32 floor measured on these batches (tools/grad_precision.py, profiles/r05)
 LOSS_TOL = 1e-5
 
 

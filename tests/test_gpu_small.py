@@ -27,7 +27,7 @@ from _fixtures import rel_err, scalar_rel, normwise, assert_all_within, worst_of
 pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
 DEV = "cuda:0"
 TOL = 1e-5
-GRAD_TOL = 1e-4
+GRAD_TOL = 5e-5   # <= 2x the fp32 floor measured on these batches (tools/grad_precision.py, profiles/r05)
 
 
 @pytest.fixture(scope="module", autouse=True)

@@ -23,7 +23,7 @@ from _fixtures import (load, flow_from_fixture, layer_params, dequant_params, st
 
 pytestmark = pytest.mark.gpu
 
-GRAD_TOL = 1e-4
+GRAD_TOL = 5e-5   # <= 2x the fp32 floor measured on these batches (tools/grad_precision.py, profiles/r05)
 LOSS_TOL = 1e-5
 
 
@@ -317,3 +317,30 @@ def test_configs3_training_step_1024x64_8_layers():
     oerr = {n: normwise(g, r) for n, g, r in zip(names, g4, ref)}
     print(f"configs[3] 4-molecule sub-batch vs gradient oracle worst {worst_of(oerr):.2e}")
     assert_all_within(oerr, GRAD_TOL, "sub-batch vs oracle")
+
+
+@pytest.mark.parametrize("name", ["train_h128_L2", "train_h64_L2", "train_h32_L3"])
+def test_f16x3_gradients_sit_at_the_fp32_floor(name):
+    """the gradients' error vs the reference's
+    float64 loss.backward() splits into what fp32 arithmetic alone gives (the
+    HIP path with gemm_precision='f32': exact fp32 MFMA chains and the fp32
+    backward) and what the f16x3 split adds on top.  Measured (profiles/r05,
+    tools/grad_precision.py): train_h128_L2 f32 3.3e-5, f16x3 3.5e-5, and the
+    float64 oracle re-run in float32 on the CPU 2.7-2.8e-5 -- the error is fp32
+    conditioning (worst tensor coord_nn.0.bias behind the gain-0.001
+    coord_nn.2), not the split.  Bar: f16x3 within 1.25x of f32 (+1e-6)."""
+    inp, ref = load(name)
+    errs = {}
+    for prec in ("f32", "f16x3"):
+        model, data = flow_from_fixture(inp, "cuda")
+        model.gemm_precision = prec
+        eps = torch.tensor(inp["eps"], device="cuda")
+        _train_step(model, data, eps, float(inp["kBT"]), float(inp["softening"]))
+        w = {}
+        for i, net in enumerate(model.networks):
+            for k, p in net.named_parameters():
+                w[f"p{i}.{k}"] = normwise(p.grad.cpu().numpy(), ref[f"grad_p{i}.{k}"])
+        errs[prec] = worst_of(w)
+    print(f"{name}: worst normwise grad err f32 {errs['f32']:.2e}, f16x3 {errs['f16x3']:.2e}")
+    assert errs["f16x3"] <= 1.25 * errs["f32"] + 1e-6
+    assert errs["f32"] <= GRAD_TOL
