@@ -11,7 +11,7 @@ import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ENFLOW_LIB") or os.path.join(_HERE, "libenflow_hip.so")
-# the same sources built with -DENFLOW_NFMAX=16: node_nf 9..16 (training 9..15)
+# the same sources built with -DENFLOW_NFMAX=16: node_nf 9..16 (inference and training)
 LIB_NF16_PATH = os.environ.get("ENFLOW_LIB_NF16") or os.path.join(_HERE, "libenflow_hip_nf16.so")
 BASE_NFMAX = 8
 MAX_NODE_NF = 16

@@ -100,9 +100,10 @@ int enflow_set_fs_threshold(int max_mols);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept.  The ABI
  * ships as two builds of the same sources: libenflow_hip.so (node_nf <= 8) and
- * libenflow_hip_nf16.so (-DENFLOW_NFMAX=16: node_nf <= 16 for inference, <= 15
- * for the training / EGCL backward entry points, whose transposed edge_nn.0
- * GEMM holds 2 node_nf + 1 <= 32 inputs); the host picks by node_nf.  The
+ * libenflow_hip_nf16.so (-DENFLOW_NFMAX=16: node_nf <= 16 for inference and
+ * for the training / EGCL backward entry points -- since ABI 11 the radial row
+ * of the backward's transposed edge_nn.0 GEMM, past its 32-row tile at node_nf
+ * 16, is a separate dot); the host picks by node_nf.  The
  * reference sizes EGCL / ArgMax by the dataset's node_nf
  * (enflow/main.py:148-151). */
 int enflow_max_atoms(void);
