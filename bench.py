@@ -493,9 +493,11 @@ def run_flow(args, world, rank, device, dist, cpu):
             s_el = timed(srun.step, args.steps, args.warmup, dist, device)
             s_kt = kernel_times(srun.step, max(args.steps, 5))
             srun.check()
+            # the instance the library picked for this shard (4-wave, 8-wave or split)
+            sname = next((k for k in ("lf_fs_kernel<fwd>", "lf_flow_kernel<fwd,lat>", kname) if k in s_kt), None)
             strong = {"global_batch": mols, "molecules_per_gpu": m1 - m0, "value": mols * args.steps / s_el,
-                      "ms_per_step": s_el / args.steps * 1e3,
-                      "flow_kernel_ms": s_kt.get(kname, {}).get("ms_per_launch")}
+                      "ms_per_step": s_el / args.steps * 1e3, "flow_kernel": sname,
+                      "flow_kernel_ms": s_kt[sname]["ms_per_launch"] if sname else None}
         else:
             strong = {"global_batch": mols, "molecules_per_gpu": mols, "value": mols * args.steps / elapsed,
                       "ms_per_step": elapsed / args.steps * 1e3, "note": "N=1: identical to the weak-scaling run"}

@@ -14,4 +14,12 @@ timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$OUT/bench_forward_tra
 rm -rf profiles/_box
 timeout -k 10 300 python -u tools/strong_scaling_probe.py > "$OUT/strong_probe.json" 2> "$OUT/strong.err"
 timeout -k 10 900 python -u profiles/collect_pmc.py "${TAG}_train" train lf_layer_bwd_kernel,outer_x3_kernel > "$OUT/pmc_train.log" 2>&1
+
+# last: the strong-scaling probe (split instance included) under the profiler,
+# with its exit status recorded (the round-4 exit-time SIGSEGV check)
+cd /tmp && export TMPDIR=/tmp
+rc=0
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_strong" -o run -- \
+  python3 "$ROOT/tools/strong_scaling_probe.py" > "$OUT/strong_probe_under_profiler.json" 2> "$OUT/prof_strong.err" || rc=$?
+echo "prof_strong exit status $rc" | tee "$OUT/prof_strong.status"
 echo done
