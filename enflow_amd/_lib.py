@@ -197,7 +197,8 @@ def set_split_threshold(max_mols):
 def set_fs_threshold(max_mols):
     """Route such launches of at most `max_mols` molecules that do not take
     the two-workgroup split to the feature-split instance with one workgroup
-    per molecule (-1: never, the default).  Returns the previous setting."""
+    per molecule (-1: the device's CU count, the default; 0: never).  Returns
+    the previous setting."""
     prev = _fs_threshold[0]
     _fs_threshold[0] = int(max_mols)
     for h in _libs.values():

@@ -67,7 +67,14 @@ struct FsSmem {
   int nseg[3];
   int dat[2][32];                      // per tile parity: pair's row atom | column atom << 8
   float rad[2][32];                    // per tile parity: pair's radial
+  alignas(16) float fx[3][32][4];      // per tile mod 3: pair's coord_diff (x, y, z), multiplicity
+  int frow[3][32];                     // per tile mod 3: pair's row, -1 - lane past the pairs
   alignas(16) float dummy[NT][32];     // message row of lanes without a segment (per stage-B wave)
+  // node biases per layer parity, the packed layer's contiguous run from bn1:
+  // node_nn.0 bias, vel_scaling_nn.0 bias, vel_scaling_nn.2 weight (H each),
+  // node_nn.2 bias (NFMAX), vel_scaling_nn.2 bias
+  static constexpr int NB = 3 * H + NFMAX + 1;
+  alignas(16) float nb[2][(NB + 3) & ~3];
   int timeout;
 };
 
@@ -85,10 +92,20 @@ template <int H>
 struct FsW {
   static constexpr int NT = H / 32, KS = 2 * NT;
   f32x4 g0h[KS0MAX], g0l[KS0MAX], wh[KS], wl[KS];
-  __device__ __forceinline__ void load(rsrc_t W, const EgclLayout& L, int lane, int w, int ks0) {
+  f32x4 qh, ql;   // stage B: vel_scaling_nn.0 block b (its item runs in the tiles' first step)
+  // in three parts (part 0: edge_nn.0 and k-slices 0 .. 2, part 1: 3 .. 5, part
+  // 2: the rest), requested between the steps of the pair build: the CU's load
+  // path (~144 KB per layer) drains beside the build's LDS work instead of
+  // stalling the issuing waves at one point
+  __device__ __forceinline__ void load(rsrc_t W, const EgclLayout& L, int lane, int w, int ks0, int part) {
     const int vo = lane * 32, b = w % NT;
     const bool A = w < NT;
-    if (A) {
+    const int t0 = part == 0 ? 0 : (part == 1 ? 3 : 6), t1 = part == 0 ? 3 : (part == 1 ? 6 : KS);
+    if (!A && part == 0) {
+      qh = bload4(W, vo, (L.wv1x + b * 512) * 4);
+      ql = bload4(W, vo + 16, (L.wv1x + b * 512) * 4);
+    }
+    if (A && part == 0) {
 #pragma unroll
       for (int ks = 0; ks < KS0MAX; ++ks) {
         if (ks < ks0) {
@@ -100,8 +117,10 @@ struct FsW {
     const int off = A ? L.we2x : L.wc1x;
 #pragma unroll
     for (int ts = 0; ts < KS; ++ts) {
-      wh[ts] = bload4(W, vo, (off + (b * KS + ts) * 512) * 4);
-      wl[ts] = bload4(W, vo + 16, (off + (b * KS + ts) * 512) * 4);
+      if (ts >= t0 && ts < t1) {
+        wh[ts] = bload4(W, vo, (off + (b * KS + ts) * 512) * 4);
+        wl[ts] = bload4(W, vo + 16, (off + (b * KS + ts) * 512) * 4);
+      }
     }
   }
 };
@@ -132,55 +151,151 @@ __device__ __forceinline__ f16x8 ld_u4(const uint32_t* p) {
   return __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4v*>(p));
 }
 
-// The pair word decode shared by a tile's GEMM pass and its force pass.
-struct PairLane {
-  bool valid;
-  int il, jl, i, row;
-  float c, dx, dy, dz, radial;
+// A layer's bias images, one element of each per thread (BLOCK = 4 H): the
+// tile biases in edge_tiles' order and scale (be1 K0, be2 K1, bc1 K2, wc2) and
+// the node biases (FsSmem::nb).  Requested in registers during the previous
+// layer's node items, stored to LDS after them: no L2 round trip on a phase.
+struct FsBias {
+  float t, n;
 };
+// (Both images are contiguous runs of the packed layer, egcl_layout: be1 be2 bc1
+// wc2, and bn1 bv1 wv2 bn2 bv2 -- no per-thread choice between layout fields,
+// which the compiler would turn into a dynamically indexed copy of the layout
+// in scratch.)
 template <int H>
-__device__ __forceinline__ PairLane decode_pair(FsSmem<H>& F, const MolRef& M, int r0, int P, int tile, int j) {
+__device__ __forceinline__ FsBias fs_bias_load(const float* __restrict__ Lp, const EgclLayout& L, int tid) {
+  static_assert(BLOCK == 4 * H, "one tile-bias element per thread");
+  FsBias r;
+  r.t = Lp[L.be1 + tid];
+  r.n = tid < FsSmem<H>::NB ? Lp[L.bn1 + tid] : 0.f;
+  return r;
+}
+template <int H>
+__device__ __forceinline__ void fs_bias_store(FsSmem<H>& F, const float* __restrict__ Lp, const EgclLayout& L, int tid,
+                                              const FsBias& r, int par) {
+  const int g = tid / H;
+  const float K = g == 0 ? Lp[L.scl + 4] : (g == 1 ? Lp[L.scl + 0] : (g == 2 ? Lp[L.scl + 2] : 1.f));
+  F.s.bias[tid] = r.t * K;
+  if (tid < FsSmem<H>::NB) F.nb[par][tid] = r.n;
+}
+
+// node_nn (egcl.py:51-54, 65-67) on the workgroup's rows with node_phase_x3_f's
+// arithmetic: wave tp < NT the item of features 32 tp .. (G partials:
+// node_nn.0 over [h, agg], act, node_nn.2).  (The vel_scaling_nn items run in
+// the edge tiles' first step, fs_edge_tiles.)  nb: the layer's node biases
+// (FsSmem::nb).
+template <int H>
+__device__ __forceinline__ void fs_node_g(FsSmem<H>& F, const float* __restrict__ Lp, const EgclLayout& L,
+                                              int tid, int r0, int rb, int nf, const float* __restrict__ nb
+                                              STAMP_ARGS) {
+  constexpr int NT = H / 32, KS = H / 16;
+  constexpr int AST = Smem<H, NMX, NMX>::AST;
   auto& sm = F.s;
-  PairLane q;
-  const int p = tile * 32 + j;
-  q.valid = p < P;
-  const uint32_t pr = q.valid ? sm.pairs[p] : 0u;
-  q.il = (int)(pr & 0xffu);
-  q.jl = (int)((pr >> 8) & 0xffu);
-  q.i = r0 + q.il;
-  q.c = (float)(pr >> 16);
-  q.row = q.valid ? q.il : -1 - j;
-  // Edges.coord_diff with the reference's half-box image (base.py:15-19)
-  q.dx = pbc1(sm.pos[q.i * 3 + 0] - sm.pos[q.jl * 3 + 0], M.bx * 0.5f);
-  q.dy = pbc1(sm.pos[q.i * 3 + 1] - sm.pos[q.jl * 3 + 1], M.by * 0.5f);
-  q.dz = pbc1(sm.pos[q.i * 3 + 2] - sm.pos[q.jl * 3 + 2], M.bz * 0.5f);
-  q.radial = q.dx * q.dx + q.dy * q.dy + q.dz * q.dz;   // egcl.py:79
-  return q;
+  const int lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int j = lane & 31, hh = lane >> 5, tp = w % NT, vo = lane * 32;
+  const rsrc_t W = weights_rsrc(Lp, L.total);
+  const int a = j;                        // row within the workgroup's block
+  const bool va = a < rb;
+  const int ag = r0 + (va ? a : 0);
+  const uint32_t vm = va ? ENFLOW_BIG_BITS : 0u;
+  uint32_t bigw = 0u;
+  {   // ---- node_nn item tp
+    const f32x4 nh = bload4(W, vo, (L.wn1hx + tp * 512) * 4), nl = bload4(W, vo + 16, (L.wn1hx + tp * 512) * 4);
+    f32x4 gfh[2], gfl[2], ah[KS], al[KS];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      gfh[s2] = bload4(W, vo, (L.wn2x + (tp * 2 + s2) * 512) * 4);
+      gfl[s2] = bload4(W, vo + 16, (L.wn2x + (tp * 2 + s2) * 512) * 4);
+    }
+#pragma unroll
+    for (int d = 0; d < KS; ++d) {
+      ah[d] = bload4(W, vo, (L.wn1ax + (tp * KS + d) * 512) * 4);
+      al[d] = bload4(W, vo + 16, (L.wn1ax + (tp * KS + d) * 512) * 4);
+    }
+    const float inv_n1 = Lp[L.scl + 9], inv_n2 = Lp[L.scl + 11];
+    f32x16 hin;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && 8 * hh + jj < nf) ? sm.h[ag * NFP + 8 * hh + jj] : 0.f;
+    f16x8 hh16, hl16;
+    split_f16(hin, 0, hh16, hl16);
+    uint32_t oa = or_hi(0u, hh16), on = 0u;
+    STAMP(16);
+    f32x16 acc = (f32x16)0.f;
+    acc = mfma_f16(nh, hh16, acc);
+    acc = mfma_f16(nh, hl16, acc);
+    acc = mfma_f16(nl, hh16, acc);
+    const float* arow = &sm.agg[(va ? a : 0) * AST];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      f32x16 av;
+      const f32x4 a0 = ld4(arow + 16 * ks + 8 * hh), a1 = ld4(arow + 16 * ks + 8 * hh + 4);
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        av[jj] = va ? a0[jj] : 0.f;
+        av[4 + jj] = va ? a1[jj] : 0.f;
+      }
+      f16x8 bh, bl;
+      split_f16(av, 0, bh, bl);
+      oa = or_hi(oa, bh);
+      acc = mfma_f16(ah[ks], bh, acc);
+      acc = mfma_f16(ah[ks], bl, acc);
+      acc = mfma_f16(al[ks], bh, acc);
+    }
+    STAMP(17);
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 b1 = ld4(nb + 32 * tp + 8 * g4 + 4 * hh);   // node_nn.0 bias
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[4 * g4 + u] = silu_f(fmaf(acc[4 * g4 + u], inv_n1, b1[u]));
+    }
+    f32x16 gacc = (f32x16)0.f;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      f16x8 bh, bl;
+      split_f16(acc, s2, bh, bl);
+      on = or_hi(on, bh);
+      gacc = mfma_f16(gfh[s2], bh, gacc);
+      gacc = mfma_f16(gfh[s2], bl, gacc);
+      gacc = mfma_f16(gfl[s2], bh, gacc);
+    }
+    bigw = (__ballot((oa & vm) != 0u) ? (uint32_t)BIGK_HA : 0u) | (__ballot((on & vm) != 0u) ? (uint32_t)BIGK_NH : 0u);
+    if (va) {
+#pragma unroll
+      for (int r = 0; r < NFMAX / 2; ++r) {
+        const int q = rho(r, hh);
+        if (q < nf) sm.u.nd.gp[tp][q][a] = gacc[r] * inv_n2;
+      }
+    }
+    STAMP(18);
+  }
+  if (lane == 0) atomicOr(&sm.big, bigw | (uint32_t)BIGK_NODE);
 }
 
 // forces of one tile (egcl.py:68-74: trans = clamp(coord_diff * phi), segment
-// sums for the mean), phi = the four partial dots in block order; run by one
+// sums for the mean), phi = the four partial dots in block order, the pair's
+// coord_diff / multiplicity / row from its decode (FsSmem::fx, frow); run by one
 // stage-B wave, tiles in order (rows continuing into the next tile accumulate)
 template <int H>
-__device__ __forceinline__ void tile_forces(FsSmem<H>& F, const MolRef& M, int r0, int P, int tile, int lane,
-                                           bool& range_bad) {
+__device__ __forceinline__ void tile_forces(FsSmem<H>& F, int P, int tile, int lane, bool& range_bad) {
   constexpr int NT = H / 32;
   constexpr int AST = Smem<H, NMX, NMX>::AST;
   auto& sm = F.s;
-  const int j = lane & 31, hh = lane >> 5;
-  const PairLane q = decode_pair(F, M, r0, P, tile, j);
+  const int j = lane & 31, hh = lane >> 5, t3 = tile % 3;
+  const bool valid = tile * 32 + j < P;
+  const f32x4 d = ld4(&F.fx[t3][j][0]);
+  const int row = F.frow[t3][j];
   float phi = 0.f;
 #pragma unroll
   for (int b = 0; b < NT; ++b) phi += F.phip[tile & 1][b][j];
-  range_bad |= q.valid && !__builtin_isfinite(phi);
-  const SegExec SE = seg_exec(q.row);
-  const int row_next = __shfl_down(q.row, 1, 32);
-  const bool seg_end = q.valid && (j == 31 || row_next != q.row);
-  f32x4* const fslot = reinterpret_cast<f32x4*>(&sm.agg[(q.valid ? q.il : 0) * AST + H]);   // H + 3: padding
+  range_bad |= valid && !__builtin_isfinite(phi);
+  const SegExec SE = seg_exec(row);
+  const int row_next = __shfl_down(row, 1, 32);
+  const bool seg_end = valid && (j == 31 || row_next != row);
+  f32x4* const fslot = reinterpret_cast<f32x4*>(&sm.agg[(valid ? row : 0) * AST + H]);   // H + 3: padding
   const f32x4 fold = *fslot;
-  float tx = q.c * clamp100(q.dx * phi);
-  float ty = q.c * clamp100(q.dy * phi);
-  float tz = q.c * clamp100(q.dz * phi);
+  float tx = d[3] * clamp100(d[0] * phi);
+  float ty = d[3] * clamp100(d[1] * phi);
+  float tz = d[3] * clamp100(d[2] * phi);
   float tw = 0.f;
   seg_scan4x(tx, ty, tz, tw, SE);
   if (seg_end && hh == 0) *fslot = fold + (f32x4){tx, ty, tz, tw};
@@ -205,8 +320,8 @@ __device__ __forceinline__ void tile_forces(FsSmem<H>& F, const MolRef& M, int r
 // multiply zero fragments by zero inputs: exact).
 template <int H, int KS0>
 __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restrict__ Lp, const EgclLayout& L,
-                                              const MolRef& M, int nf, int tid, int r0, int rb, const FsW<H>& Wt
-                                              STAMP_ARGS) {
+                                              const MolRef& M, int nf, int tid, int r0, int rb, const FsW<H>& Wt,
+                                              const float* __restrict__ nb STAMP_ARGS) {
   constexpr int NT = H / 32, KS = 2 * NT;
   constexpr int AST = Smem<H, NMX, NMX>::AST;
   auto& sm = F.s;
@@ -216,14 +331,8 @@ __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restr
   const int j = lane & 31, hh = lane >> 5;
   const int P = sm.npairs;
   const int T = (P + 31) >> 5;
-  for (int e = tid; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
+  // (the caller zeroed agg and staged the layer's bias image before the pair build)
   const float K0 = Lp[L.scl + 4], K1 = Lp[L.scl + 0], K2 = Lp[L.scl + 2];
-  for (int k = tid; k < H; k += BLOCK) {
-    sm.bias[k] = Lp[L.be1 + k] * K0;
-    sm.bias[H + k] = Lp[L.be2 + k] * K1;
-    sm.bias[2 * H + k] = Lp[L.bc1 + k] * K2;
-    sm.bias[3 * H + k] = Lp[L.wc2 + k];
-  }
   constexpr float NLOG2E = -1.4426950408889634f;
   const float c0 = NLOG2E * Lp[L.scl + 5], c1 = NLOG2E * Lp[L.scl + 1], c2 = NLOG2E * Lp[L.scl + 3];
   const int nch = gemm0_nch(nf);
@@ -256,6 +365,9 @@ __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restr
     F.nseg[tpar] = __builtin_popcount(Sb);
     F.dat[par][j] = i | (jl << 8);
     F.rad[par][j] = dx * dx + dy * dy + dz * dz;   // egcl.py:79
+    const int t3 = tile % 3;
+    st4(&F.fx[t3][j][0], (f32x4){dx, dy, dz, c});
+    F.frow[t3][j] = row;
   };
   if (!stA && b == 0 && T > 0) decode(0);
   __syncthreads();
@@ -320,6 +432,35 @@ __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restr
       }
       part += __shfl_xor(part, 32, 64);
       F.phip[par][b][j] = part;   // both lane halves: the same value to the same word
+    } else {   // ---- step 0: vel_scaling_nn item b (egcl.py:26-30, 62-64; depends on h only)
+      // node_phase_x3_f's arithmetic: Q partial over features 32 b .. of the rows
+      // (lane j = row j), summed with the other items in the tail
+      const bool va = j < rb;
+      const int ag = r0 + (va ? j : 0);
+      f32x16 hin;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) hin[jj] = (va && 8 * hh + jj < nf) ? sm.h[ag * NFP + 8 * hh + jj] : 0.f;
+      f16x8 hh16, hl16;
+      split_f16(hin, 0, hh16, hl16);
+      const uint32_t oh = or_hi(0u, hh16);
+      f32x16 acc = (f32x16)0.f;
+      acc = mfma_f16(Wt.qh, hh16, acc);
+      acc = mfma_f16(Wt.qh, hl16, acc);
+      acc = mfma_f16(Wt.ql, hh16, acc);
+      const float inv_v1 = Lp[L.scl + 7];
+      float part = 0.f;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int f0 = 32 * b + 8 * g4 + 4 * hh;
+        const f32x4 b1 = ld4(nb + H + f0), w2 = ld4(nb + 2 * H + f0);   // vel_scaling_nn.0 bias, .2 weight
+#pragma unroll
+        for (int u = 0; u < 4; ++u) part += w2[u] * silu_f(fmaf(acc[4 * g4 + u], inv_v1, b1[u]));
+      }
+      part += __shfl_xor(part, 32, 64);
+      if (hh == 0 && va) sm.u.nd.qp[b][j] = part;
+      const uint32_t vm = va ? ENFLOW_BIG_BITS : 0u;
+      const uint32_t qb = __ballot((oh & vm) != 0u) ? (uint32_t)BIGK_HV : 0u;
+      if (lane == 0) atomicOr(&sm.big, qb | (uint32_t)BIGK_NODE);
     }
     STAMP(10);
     __syncthreads();   // x0 of tile s, phi partials of tile s - 1 complete
@@ -397,7 +538,7 @@ __device__ __forceinline__ void fs_edge_tiles(FsSmem<H>& F, const float* __restr
         for (int g4 = 0; g4 < 4; ++g4)
           st4(dstn + 8 * g4 + 4 * hh, (f32x4){Y[4 * g4], Y[4 * g4 + 1], Y[4 * g4 + 2], Y[4 * g4 + 3]});
       }
-      if (s > 0 && b == (s - 1) % NT) tile_forces(F, M, r0, P, s - 1, lane, range_bad);
+      if (s > 0 && b == (s - 1) % NT) tile_forces(F, P, s - 1, lane, range_bad);
       if (s + 1 < T && b == s % NT) decode(s + 1);
     }
     STAMP(13);
@@ -535,6 +676,35 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
     }
 
     STAMP(1);
+    // Layer l: pair build (the layer's weight blocks requested beside it), edge
+    // tiles (vel_scaling_nn in their first step), then the tail: T1 the node_nn
+    // items beside the position update, the positions published as they are
+    // updated and the partner's read, the next layer's bias images requested;
+    // T2 the features' update, published.  The partner's
+    // features are read just before the next layer's tiles, a pair build after
+    // they were published: the hand-off latencies sit behind the node items and
+    // the pair build (SPLIT = 2).  Reverse folds the next layer's half-step
+    // (dynamics.py:28-30) into the tail.  Layer 0's biases and reverse half-step
+    // are set up here.
+    {
+      const EgclLayout L0 = egcl_layout(H, nf);
+      const float* Lp0 = A.layers + (size_t)(REV ? A.n_layers - 1 : 0) * L0.total;
+      fs_bias_store(F, Lp0, L0, tid, fs_bias_load<H>(Lp0, L0, tid), 0);
+      if (REV) {   // dynamics.py:28-30 on the workgroup's atoms, first layer
+        for (int a = r0 + tid; a < r0 + rb; a += BLOCK) {
+          for (int q = 0; q < nf; ++q) sm.h[a * NFP + q] -= sm.g[a * NFP + q] * A.dt;
+          for (int d = 0; d < 3; ++d)
+            sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, pbox(a, d));
+        }
+        __syncthreads();
+        if constexpr (SPLIT == 2) {
+          const uint32_t tag = xtag(epoch, 0x7f);
+          fs_publish(F, xmine + XSLOT, r0, rb, nf, tag);
+          fs_consume(F, xpart + XSLOT, pr0, prb, nf, tag);
+        }
+      }
+    }
+    constexpr int AST = Smem<H, NMX, NMX>::AST;
     for (int it = 0; it < A.n_layers; ++it) {
       int nfl = __builtin_amdgcn_readfirstlane(A.nf), nl = __builtin_amdgcn_readfirstlane(M.n), tid_l = tid;
       asm volatile("" : "+s"(nfl), "+s"(nl), "+v"(tid_l));
@@ -542,30 +712,32 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
       Ml.n = nl;
       const EgclLayout L = egcl_layout(H, nfl);
       const int l = REV ? A.n_layers - 1 - it : it;
+      const bool more = it + 1 < A.n_layers;
       const float* Lp = A.layers + (size_t)l * L.total;
-      const rsrc_t W = weights_rsrc(Lp, L.total);
+      const float* Lpn = A.layers + (size_t)(REV ? l - 1 : l + 1) * L.total;   // next layer (valid when more)
       const int lane = tid_l & 63, w = __builtin_amdgcn_readfirstlane(tid_l >> 6);
-      // this wave's weight block, requested before the neighbour list (its L2
-      // round trips overlap the pair build)
-      FsW<H> Wt;
-      Wt.load(W, L, lane, w, KS0);
-      if (REV) {   // dynamics.py:28-30 on the workgroup's atoms
-        for (int a = r0 + tid; a < r0 + rb; a += BLOCK) {
-          for (int q = 0; q < nfl; ++q) sm.h[a * NFP + q] -= sm.g[a * NFP + q] * A.dt;
-          for (int d = 0; d < 3; ++d)
-            sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] - sm.vel[a * 3 + d] * A.dt, pbox(a, d));
-        }
-        __syncthreads();
-        if constexpr (SPLIT == 2) {
-          const uint32_t tag = xtag(epoch, it);
-          fs_publish(F, xmine + (it & 1) * XSLOT, r0, rb, nfl, tag);
-          fs_consume(F, xpart + (it & 1) * XSLOT, pr0, prb, nfl, tag);
-        }
+      for (int e = tid_l; e < rb * AST; e += BLOCK) sm.agg[e] = 0.f;
+      // the partner's features from the previous layer's tail: granule loads issued
+      // here, their tags checked before the tiles (the load latency behind the pair
+      // build; a granule not yet published is polled then)
+      uint64_t hg = 0;
+      const int he = tid_l;                 // one granule per thread: prb * nf <= 16 * NFMAX <= BLOCK
+      const bool hget = SPLIT == 2 && it > 0 && he < prb * nfl;
+      if (hget) {
+        const int a = he / nfl, q = he - a * nfl;
+        hg = __hip_atomic_load(xpart + ((it - 1) & 1) * XSLOT + a * XG + 3 + q, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
       }
       STAMP(2);
+      // this wave's weight blocks of the layer, requested in parts during the pair build
+      FsW<H> Wt;
+      const rsrc_t Wr = weights_rsrc(Lp, L.total);
+      Wt.load(Wr, L, lane, w, KS0, 0);
       build_images(sm, Ml, tid_l);
       STAMP(3);
+      Wt.load(Wr, L, lane, w, KS0, 1);
       block_counts(sm, Ml, tid_l, r0, rb, true);   // build_images zeroed the whole count matrix
+      Wt.load(Wr, L, lane, w, KS0, 2);
       block_compact(sm, nl, tid_l, rb, 0);
       STAMP(4);
       if (A.stats != nullptr && tid == 0) {
@@ -574,54 +746,109 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
         atomicAdd(&A.stats[0], (unsigned long long)sm.npairs);
         atomicAdd(&A.stats[1], edges);
       }
-      NodeFrags<H> nfr;
-      // (the node phase's fragments are requested after the tiles: issued early
-      // they would share the tiles' registers with the edge weight blocks)
-      fs_edge_tiles<H, KS0>(F, Lp, L, Ml, nfl, tid_l, r0, rb, Wt STAMP_PASS);
+      constexpr int NT = H / 32;
+      // the hand-off granules of layer k's tail: {value, tag(k)} in parity k & 1
+      auto put = [&](int k, int a, int c, float v) {   // a: row within the block, c: 0..2 pos, 3.. h
+        const uint64_t g = ((uint64_t)xtag(epoch, k) << 32) | (uint64_t)__float_as_uint(v);
+        __hip_atomic_store(xmine + (k & 1) * XSLOT + a * XG + c, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      };
+      auto get = [&](int k, int a, int c) {            // a: row within the partner's block
+        const uint32_t tag = xtag(epoch, k);
+        const uint64_t* const slot = xpart + (k & 1) * XSLOT + a * XG + c;
+        uint64_t g = 0;
+        int spins = 0;
+        for (;;) {
+          g = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(g >> 32) == tag) break;
+          if (++spins > (1 << 20)) {
+            F.timeout = 1;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        return __uint_as_float((uint32_t)g);
+      };
+      const float* nb = F.nb[it & 1];
+      // the partner's features from the previous layer's tail, published there a
+      // pair build ago (needed from the first GEMM0 on: fs_edge_tiles' first barrier
+      // orders these writes before it)
+      static_assert(HALF * NFMAX <= BLOCK, "one partner feature granule per thread");
+      if (hget) {
+        const int a = he / nfl, q = he - a * nfl;
+        sm.h[(pr0 + a) * NFP + q] = (uint32_t)(hg >> 32) == xtag(epoch, it - 1) ? __uint_as_float((uint32_t)hg)
+                                                                              : get(it - 1, a, 3 + q);
+      }
+      fs_edge_tiles<H, KS0>(F, Lp, L, Ml, nfl, tid_l, r0, rb, Wt, nb STAMP_PASS);
       STAMP(5);
-      node_phase_x3_f<H, NMX, NMX, false>(sm, Lp, L, nl, nfl, tid_l, r0, rb, nfr, false);
+      // ---- tail T1: node_nn items on waves 0 .. NT - 1; on the others the
+      // velocity / position update of the workgroup's rows (dynamics.py:15-20
+      // forward, 33-35 + the next half-step 29 in reverse: Q from the tiles' first
+      // step, the forces from the tiles), the positions published at once; the
+      // next layer's bias images requested
+      FsBias nbias{0.f, 0.f};
+      if (more) nbias = fs_bias_load<H>(Lpn, L, tid_l);
+      constexpr int GT = NT * 64;   // threads per wave group
+      if (w < NT) {
+        fs_node_g(F, Lp, L, tid_l, r0, rb, nfl, nb STAMP_PASS);
+      } else {
+        for (int a = tid_l - GT; a < rb; a += BLOCK - GT) {
+          const int ag = r0 + a;
+          float q = 0.f;
+#pragma unroll
+          for (int tp = 0; tp < NT; ++tp) q += sm.u.nd.qp[tp][a];
+          q += nb[3 * H + NFMAX];
+          const float eq = expf(q);
+          const float inv = 1.f / fmaxf((float)sm.cntrow[ag], 1.f);   // helpers.py:63-70
+          for (int d = 0; d < 3; ++d) {
+            const float Fd = sm.agg[a * AST + H + d] * inv * A.cw;
+            float v, p = sm.pos[ag * 3 + d];
+            if (!REV) {
+              v = eq * sm.vel[ag * 3 + d] + Fd * A.dt;
+              p = pbc1(p + v * A.dt, pbox(ag, d));
+            } else {
+              v = (sm.vel[ag * 3 + d] - Fd * A.dt) / eq;
+              if (more) p = pbc1(p - v * A.dt, pbox(ag, d));
+            }
+            sm.vel[ag * 3 + d] = v;
+            sm.pos[ag * 3 + d] = p;
+            if (SPLIT == 2 && more) put(it, a, d, p);
+          }
+          if (!REV) ldj += q;
+        }
+        // the partner's positions, published in its own T1: polled here, behind
+        // the node_nn items of this T1
+        if (SPLIT == 2 && more)
+          for (int e = tid_l - GT; e < prb * 3; e += BLOCK - GT) {
+            const int a = e / 3, d = e - a * 3;
+            sm.pos[(pr0 + a) * 3 + d] = get(it, a, d);
+          }
+      }
+      __syncthreads();
       STAMP(6);
+      // ---- tail T2: the features' update (G), published
       if (tid == 0) {
         if (small_operands(sm.big)) sm.err |= ENFLOW_ERR_SMALL;
         sm.big = 0u;
       }
-      constexpr int AST = Smem<H, NMX, NMX>::AST;
-      for (int a = r0 + tid; a < r0 + rb; a += BLOCK) {
-        const float q = sm.Q[a];
-        const float eq = expf(q);
-        const float inv = 1.f / fmaxf((float)sm.cntrow[a], 1.f);   // helpers.py:63-70
-        auto force = [&](int d) { return sm.agg[(a - r0) * AST + H + d] * inv * A.cw; };
-        if (!REV) {   // dynamics.py:15-22
-          for (int d = 0; d < 3; ++d) {
-            const float Fd = force(d);
-            const float v = eq * sm.vel[a * 3 + d] + Fd * A.dt;
-            sm.vel[a * 3 + d] = v;
-            sm.pos[a * 3 + d] = pbc1(sm.pos[a * 3 + d] + v * A.dt, pbox(a, d));
-          }
-          for (int qf = 0; qf < nfl; ++qf) {
-            const float gn = sm.g[a * NFP + qf] + sm.G[a * NFP + qf] * A.dt;
-            sm.g[a * NFP + qf] = gn;
-            sm.h[a * NFP + qf] += gn * A.dt;
-          }
-          ldj += q;
-        } else {      // dynamics.py:32-35
-          for (int qf = 0; qf < nfl; ++qf) sm.g[a * NFP + qf] -= sm.G[a * NFP + qf] * A.dt;
-          for (int d = 0; d < 3; ++d) {
-            const float Fd = force(d);
-            sm.vel[a * 3 + d] = (sm.vel[a * 3 + d] - Fd * A.dt) / eq;
-          }
+      if (w < NT) {   // dynamics.py:21-22 (forward) / 32 + the next half-step 28 (reverse)
+        for (int e = tid_l; e < rb * nfl; e += GT) {
+          const int a = e / nfl, q = e - a * nfl, ag = r0 + a;
+          float G = 0.f;
+#pragma unroll
+          for (int tp = 0; tp < NT; ++tp) G += sm.u.nd.gp[tp][q][a];
+          G += nb[3 * H + q];
+          const float gn = REV ? sm.g[ag * NFP + q] - G * A.dt : sm.g[ag * NFP + q] + G * A.dt;
+          sm.g[ag * NFP + q] = gn;
+          float hv = sm.h[ag * NFP + q];
+          if (!REV) hv += gn * A.dt;
+          else if (more) hv -= gn * A.dt;
+          sm.h[ag * NFP + q] = hv;
+          if (SPLIT == 2 && more) put(it, a, 3 + q, hv);
         }
       }
+      if (more) fs_bias_store(F, Lpn, L, tid_l, nbias, (it + 1) & 1);
       __syncthreads();
       STAMP(7);
-      if constexpr (SPLIT == 2) {
-        if (!REV && it + 1 < A.n_layers) {
-          const uint32_t tag = xtag(epoch, it);
-          fs_publish(F, xmine + (it & 1) * XSLOT, r0, rb, nfl, tag);
-          fs_consume(F, xpart + (it & 1) * XSLOT, pr0, prb, nfl, tag);
-        }
-      }
-      STAMP(8);
     }
 
     if (REV) {   // dequantize.reverse (argmax.py:27-28 / floor.py:13), the workgroup's atoms
@@ -743,7 +970,7 @@ std::mutex g_mu;
 XBuf g_buf[64];
 int g_nbuf = 0;
 int g_split_threshold = -1;   // SPLIT = 2 for batches of at most this many molecules (-1: CUs / 2)
-int g_fs_threshold = -1;      // SPLIT = 1 for batches of at most this many molecules (-1: off)
+int g_fs_threshold = -1;      // SPLIT = 1 for batches of at most this many molecules (-1: CUs; 0: off)
 int g_cus[64];
 
 int cus_of(int dev) {
@@ -797,7 +1024,8 @@ int enflow_fs_split_for(int num_mols) {
   const int cus = cus_of(dev);
   const int t2 = g_split_threshold >= 0 ? g_split_threshold : cus / 2;
   if (num_mols > 0 && num_mols <= t2 && 2 * num_mols <= cus) return 2;
-  if (num_mols > 0 && g_fs_threshold >= 0 && num_mols <= g_fs_threshold) return 1;
+  const int t1 = g_fs_threshold >= 0 ? g_fs_threshold : cus;   // one workgroup per molecule and CU
+  if (num_mols > 0 && num_mols <= t1) return 1;
   return 0;
 }
 

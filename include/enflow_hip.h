@@ -92,7 +92,8 @@ int enflow_latency_threshold(void);
  * CUs run it with each molecule's rows split over two workgroups (one position
  * / feature hand-off per layer; -1 (default): CUs / 2; 0: never).
  * enflow_set_fs_threshold: batches of at most `max_mols` molecules that do not
- * take that split run it with one workgroup per molecule (-1 (default): never).
+ * take that split run it with one workgroup per molecule (-1 (default): the
+ * device's CU count, one round of workgroups; 0: never).
  * Same strong-scaling role as enflow_set_latency_threshold (enflow/main.py:
  * 141-145); both return the previous setting. */
 int enflow_set_split_threshold(int max_mols);

@@ -17,20 +17,21 @@ def pytest_configure(config):
 import pytest  # noqa: E402
 
 
-@pytest.fixture(scope="module", params=["4-wave", "8-wave", "split"])
+@pytest.fixture(scope="module", params=["4-wave", "8-wave", "split", "split1"])
 def kernel_instance(request):
     """Run a module's tests on every instance of the fused <= 32-atom flow
     kernel: the 4-wave throughput build (2 workgroups per CU, the one bench.py
     times), the 8-wave whole-tile latency build (enflow_latency.hip) and the
-    feature-split latency build (enflow_split.hip: two workgroups per molecule
-    where they fit, else one; H = 128 f16x3 inference only, other launches of
-    this param run the 4-wave build), selected through the thresholds (0:
-    never; 2^30: every batch).  The previous settings are restored afterwards."""
+    feature-split latency build (enflow_split.hip: "split" two workgroups per
+    molecule where they fit, else one; "split1" one workgroup per molecule; H =
+    128 f16x3 inference only, other launches of these params run the 4-wave
+    build), selected through the thresholds (0: never; 2^30: every batch).  The
+    previous settings are restored afterwards."""
     from enflow_amd import _lib
     p = request.param
     prev = (_lib.set_latency_threshold(1 << 30 if p == "8-wave" else 0),
             _lib.set_split_threshold(1 << 30 if p == "split" else 0),
-            _lib.set_fs_threshold(1 << 30 if p == "split" else -1))
+            _lib.set_fs_threshold(1 << 30 if p in ("split", "split1") else 0))
     yield p
     _lib.set_latency_threshold(-1 if prev[0] is None else prev[0])
     _lib.set_split_threshold(-1 if prev[1] is None else prev[1])

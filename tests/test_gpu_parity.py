@@ -411,11 +411,12 @@ def test_kernel_instance_selected(mols, kernel_instance):
     from enflow_amd.data import Data
     from enflow_amd.data.synthetic import make_molecules, default_dt
     b = _f32(make_molecules(mols, 22, nf=5, seed=5))
-    model = _make_model(128 if kernel_instance == "split" else 32, 5, 2, 3, default_dt())
+    model = _make_model(128 if kernel_instance in ("split", "split1") else 32, 5, 2, 3, default_dt())
     with _lib.KernelTimer() as t, torch.no_grad():
         model(Data.from_arrays(b, device=DEV))
     names = set(t.stats)
-    want = {"8-wave": "lf_flow_kernel<fwd,lat>", "split": "lf_fs_kernel<fwd>"}.get(kernel_instance,
+    want = {"8-wave": "lf_flow_kernel<fwd,lat>", "split": "lf_fs_kernel<fwd>",
+            "split1": "lf_fs_kernel<fwd>"}.get(kernel_instance,
                                                                                    "lf_flow_kernel<fwd>")
     print(f"[{kernel_instance}] {mols} molecules ran {sorted(names)}")
     assert want in names, names
@@ -634,9 +635,10 @@ def test_clamp_propagates_nan_like_torch():
     assert np.isnan(ref["vel"]).any(axis=1).sum() > 1                # F of the NaN atom's partners too
 
 
-@pytest.mark.parametrize("mols", [128, 7])
+@pytest.mark.parametrize("mols", [128, 7, 256])
 def test_split_instance_strong_scaling_batch_vs_oracle(mols):
-    """The strong-scaling shard of BASELINE configs[1] (1024 x 22 split over 8
+    """(256 molecules, the 4-GPU shard: one workgroup per molecule by default.)
+    The strong-scaling shard of BASELINE configs[1] (1024 x 22 split over 8
     GPUs: 128 molecules per GPU, H = 128, 8 layers, f16x3) runs the
     two-workgroups-per-molecule instance by default (enflow_split.hip: rows
     split over the pair, one position / feature hand-off per layer): forward,
@@ -657,6 +659,7 @@ def test_split_instance_strong_scaling_batch_vs_oracle(mols):
             back = model.reverse(o1.clone())
         assert "lf_fs_kernel<fwd>" in t.stats and "lf_fs_kernel<rev>" in t.stats, sorted(t.stats)
         _lib.set_split_threshold(0)
+        _lib.set_fs_threshold(0)
         _lib.set_latency_threshold(0)
         with torch.no_grad():
             o4, l4 = model(d.clone(), noise=noise)

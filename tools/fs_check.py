@@ -11,7 +11,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-INSTANCES = {"4w": (0, 0, -1), "8w": (1 << 30, 0, -1), "fs2": (0, 1 << 30, -1), "fs1": (0, 0, 1 << 30)}
+INSTANCES = {"4w": (0, 0, 0), "8w": (1 << 30, 0, 0), "fs2": (0, 1 << 30, 0), "fs1": (0, 0, 1 << 30)}
 
 
 def set_instance(name):

@@ -13,9 +13,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO = os.path.join(ROOT, "enflow_amd", "libenflow_hip_stamps.so")
-FS_PHASES = ["load", "dequant", "layer:weights+rev", "pairs:images+idmap", "pairs:counts+compact", "(after tiles)",
-             "node", "update", "exchange", "  tiles:setup+decode0", "  A gemm0+act+split", "  barrier X",
-             "  A gemm1", "  A act+split", "  barrier Y", "  tail", "-", "-", "-", "writeback"]
+FS_PHASES = ["load", "dequant", "layer setup", "pairs:images+idmap", "pairs:counts+compact", "(after tiles)",
+             "tail T1: node items + next weights", "tail T2: update + hand-off", "-", "  tiles:setup+decode0", "  A gemm0+act+split", "  barrier X",
+             "  A gemm1", "  A act+split", "  barrier Y", "  tail", "  T1: G frags issued, h split",
+             "  T1: G node_nn.0 chain", "  T1: G act + node_nn.2", "writeback"]
 PHASES = ["load", "dequant", "pairs:counts+compact", "pairs:images+idmap", "edge_tiles(all)", "node", "update", "writeback",
           "  tiles:setup", "  gemm0", "  silu0", "  gemm1", "  silu1", "  segsum", "  gemm2+phi+force", "  tail-barrier"]
 
@@ -44,7 +45,7 @@ def main():
     rd.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.enflow_set_latency_threshold(100000 if lat else 0)   # which instance is stamped
     L.enflow_set_split_threshold(100000 if fs == 2 else 0)
-    L.enflow_set_fs_threshold(100000 if fs == 1 else -1)
+    L.enflow_set_fs_threshold(100000 if fs == 1 else 0)
     phases = FS_PHASES if fs else PHASES
     wgs = mols * (2 if fs == 2 else 1)
     dev = torch.device("cuda", 0)

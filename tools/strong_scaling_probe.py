@@ -3,10 +3,10 @@ the 1024-molecule batch of BASELINE configs[1] split N ways is, on each rank,
 a 1024/N-molecule forward with no data-path collective, so its step time IS
 the N-rank strong-scaling time (max over ranks = the slowest shard).
 
-Rows per rank count: the instance the library picks ("auto": the split
-instance, two workgroups per molecule, for batches of at most CUs/2
-molecules; the 8-wave instance up to enflow_latency_threshold(); else the
-4-wave one) and each instance forced.
+Rows per rank count: the instance the library picks ("auto": the
+feature-split instance with two workgroups per molecule for batches of at
+most CUs/2 molecules, with one up to CUs; the 8-wave instance up to
+enflow_latency_threshold(); else the 4-wave one) and each instance forced.
 
     python tools/strong_scaling_probe.py > profiles/r05/strong_scaling_probe.json
 """
@@ -37,9 +37,10 @@ def main():
     t1 = None
     for n in (1, 2, 4, 8):
         m1 = 1024 // n
-        auto = "fs2" if m1 <= cus // 2 else "8w" if m1 <= L.enflow_latency_threshold() else "4w"
-        for mode in ("auto", "4w", "8w", "fs2"):
-            if mode == "fs2" and m1 > cus // 2:
+        auto = ("fs2" if m1 <= cus // 2 else "fs1" if m1 <= cus else
+                "8w" if m1 <= out["latency_threshold_auto"] else "4w")
+        for mode in ("auto", "4w", "8w", "fs2", "fs1"):
+            if (mode == "fs2" and m1 > cus // 2) or (mode == "fs1" and m1 > cus):
                 continue
             if mode == "auto":
                 _lib.set_latency_threshold(-1)
