@@ -2345,6 +2345,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
   const AmLayout L = argmax_layout(H, nf);
   const int tid = threadIdx.x;
   float* net = sm.u.net;
+  constexpr int NETA_U = RB;                     // atoms per chunk
   float lq = 0.f;
   const Act aact = VAR ? act_of(Dp + L.act) : act_silu();   // network.1 (argmax.py:7)
   // network.2.weight staged in the (still unused) edge_nn.0 fragment buffer: the
@@ -2386,28 +2387,34 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
       net[a * 2 * NFMAX + o] = s;          // chunk-local rows
     }
     __syncthreads();
-    for (int a = tid; a < cn; a += BLOCK) {   // z of the chunk's atoms (each atom's own h only)
-      const int ag = c0 + a;
-      float u[NFMAX], hv[NFMAX];
+    // z of the chunk's atoms (each atom's own h only), one (atom, feature)
+    // element per thread: the draw (Philox + Box-Muller) and exp of every element
+    // in parallel rather than an atom's nf elements in turn on one thread; u
+    // staged in the (consumed) activation rows, T = sum_q h_q u_q in feature order
+    // by each element's thread, z staged before h is overwritten
+    static_assert(S::AST * RB >= 2 * NETA_U * NFMAX, "u / z staging fits the activation rows");
+    float* const us = act;                       // [a][q] u
+    float* const zs = act + NETA_U * NFMAX;      // [a][q] z
+    for (int e = tid; e < cn * nf; e += BLOCK) {
+      const int a = e / nf, q = e - a * nf, ag = c0 + a;
+      const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
+      const float u = tr + noise.normal((size_t)(a0 + ag) * nf + q) * expf(ls);
+      us[a * NFMAX + q] = u;
+      lq += -0.5f * u * u - ls;
+    }
+    __syncthreads();
+    for (int e = tid; e < cn * nf; e += BLOCK) {
+      const int a = e / nf, q = e - a * nf, ag = c0 + a;
       float T = 0.f;
-#pragma unroll
-      for (int q = 0; q < NFMAX; ++q) {
-        if (q < nf) {
-          const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
-          u[q] = tr + noise.normal((size_t)(a0 + ag) * nf + q) * expf(ls);
-          hv[q] = sm.h[ag * NFP + q];
-          T += hv[q] * u[q];
-          lq += -0.5f * u[q] * u[q] - ls;
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NFMAX; ++q) {
-        if (q < nf) {
-          const float z = hv[q] * u[q] + (1.f - hv[q]) * (T - softplus_f(T - u[q]));
-          lq -= (1.f - hv[q]) * logsigmoid_f(T - u[q]);
-          sm.h[ag * NFP + q] = z;
-        }
-      }
+      for (int q2 = 0; q2 < nf; ++q2) T += sm.h[ag * NFP + q2] * us[a * NFMAX + q2];
+      const float hv = sm.h[ag * NFP + q], u = us[a * NFMAX + q];
+      zs[a * NFMAX + q] = hv * u + (1.f - hv) * (T - softplus_f(T - u));
+      lq -= (1.f - hv) * logsigmoid_f(T - u);
+    }
+    __syncthreads();
+    for (int e = tid; e < cn * nf; e += BLOCK) {
+      const int a = e / nf, q = e - a * nf;
+      sm.h[(c0 + a) * NFP + q] = zs[a * NFMAX + q];
     }
     __syncthreads();
   }
