@@ -81,6 +81,7 @@ SIGNATURES = {
     "enflow_alchemical_nll_f32": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _f, _f, _f,
                                        _p, _p, _p]),
     "enflow_lf_tape_size": (_i64, [_i, _i, _i, _i]),
+    "enflow_lf_tape_size_for": (_i64, [_i, _i, _i, _i, _i]),
     "enflow_egcl_bwd_packed_size": (_i64, [_i, _i]),
     "enflow_pack_egcl_bwd_f32": (_i, [_p, _i, _i, _p, _p]),
     "enflow_lf_backward_workspace_size": (_i64, [_i, _i, _i, _i, _i, _i64]),

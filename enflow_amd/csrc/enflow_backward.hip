@@ -2741,6 +2741,16 @@ int64_t enflow_lf_tape_size(int num_atoms, int nf, int H, int n_layers) {
   return (int64_t)tape_layout(num_atoms, nf, H, n_layers).total;
 }
 
+// The neighbour-list section (pair words and row counts, the layout's tail) is
+// written by the 33..64-atom fused forward and read back by its backward only;
+// other batches' tapes end before it.
+int64_t enflow_lf_tape_size_for(int num_atoms, int nf, int H, int n_layers, int max_mol_atoms) {
+  if (num_atoms < 0 || nf < 1 || nf > BWD_NFMAX || !hid_ok_b(H) || n_layers < 0 || max_mol_atoms < 0) return -1;
+  const TapeLayout T = tape_layout(num_atoms, nf, H, n_layers);
+  static_assert(TAPE_PAIR_CAP + 1 == 64, "the pair section belongs to the 64-atom instance");
+  return (int64_t)(max_mol_atoms > 32 && max_mol_atoms <= TAPE_PAIR_CAP + 1 ? T.total : T.pairs);
+}
+
 int64_t enflow_egcl_bwd_packed_size(int H, int nf) {
   if (!hid_ok_b(H) || nf < 1 || nf > BWD_NFMAX) return -1;
   return egcl_bwd_layout(H).total;

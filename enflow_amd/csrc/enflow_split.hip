@@ -664,7 +664,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
     if (!REV) {
       if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
         // every atom in both halves (the same draws); half 0 counts log_q
-        const float lq = argmax_dequant<H, NMX, NMX, false>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+        const float lq = argmax_dequant<H, NMX, NMX, false, true>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
         if (half == 0) ldj += lq;
       } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
         for (int e = tid; e < n * nf; e += BLOCK) {

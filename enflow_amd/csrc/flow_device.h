@@ -2333,7 +2333,11 @@ struct NoiseSrc {
 
 // ArgMax.forward (enflow/nn/argmax.py:13-25) on the molecule in LDS.  h <- z;
 // returns this thread's share of log_q (without the -0.5 log(2 pi) batch term).
-template <int H, int NMAX, int RB, bool VAR = false>
+// PAR: the last step one (atom, feature) element per thread (the split instance:
+// eight waves, one molecule); else one atom per thread, its elements in turn
+// (the whole-tile instances: the parallel form measured no faster there and
+// moved register spills into the layer loop, profiles/r05/r05w_*, r05z2 PMC)
+template <int H, int NMAX, int RB, bool VAR = false, bool PAR = false>
 __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const NoiseSrc noise,
                                 int a0, int n, int nf) {
   using S = Smem<H, NMAX, RB>;
@@ -2387,36 +2391,63 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
       net[a * 2 * NFMAX + o] = s;          // chunk-local rows
     }
     __syncthreads();
-    // z of the chunk's atoms (each atom's own h only), one (atom, feature)
-    // element per thread: the draw (Philox + Box-Muller) and exp of every element
-    // in parallel rather than an atom's nf elements in turn on one thread; u
-    // staged in the (consumed) activation rows, T = sum_q h_q u_q in feature order
-    // by each element's thread, z staged before h is overwritten
-    static_assert(S::AST * RB >= 2 * NETA_U * NFMAX, "u / z staging fits the activation rows");
-    float* const us = act;                       // [a][q] u
-    float* const zs = act + NETA_U * NFMAX;      // [a][q] z
-    for (int e = tid; e < cn * nf; e += BLOCK) {
-      const int a = e / nf, q = e - a * nf, ag = c0 + a;
-      const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
-      const float u = tr + noise.normal((size_t)(a0 + ag) * nf + q) * expf(ls);
-      us[a * NFMAX + q] = u;
-      lq += -0.5f * u * u - ls;
+    if constexpr (!PAR) {
+      for (int a = tid; a < cn; a += BLOCK) {   // z of the chunk's atoms (each atom's own h only)
+        const int ag = c0 + a;
+        float u[NFMAX], hv[NFMAX];
+        float T = 0.f;
+#pragma unroll
+        for (int q = 0; q < NFMAX; ++q) {
+          if (q < nf) {
+            const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
+            u[q] = tr + noise.normal((size_t)(a0 + ag) * nf + q) * expf(ls);
+            hv[q] = sm.h[ag * NFP + q];
+            T += hv[q] * u[q];
+            lq += -0.5f * u[q] * u[q] - ls;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < NFMAX; ++q) {
+          if (q < nf) {
+            const float z = hv[q] * u[q] + (1.f - hv[q]) * (T - softplus_f(T - u[q]));
+            lq -= (1.f - hv[q]) * logsigmoid_f(T - u[q]);
+            sm.h[ag * NFP + q] = z;
+          }
+        }
+      }
+      __syncthreads();
+    } else {
+      // z of the chunk's atoms (each atom's own h only), one (atom, feature)
+      // element per thread: the draw (Philox + Box-Muller) and exp of every element
+      // in parallel rather than an atom's nf elements in turn on one thread; u
+      // staged in the (consumed) activation rows, T = sum_q h_q u_q in feature order
+      // by each element's thread, z staged before h is overwritten
+      static_assert(S::AST * RB >= 2 * NETA_U * NFMAX, "u / z staging fits the activation rows");
+      float* const us = act;                       // [a][q] u
+      float* const zs = act + NETA_U * NFMAX;      // [a][q] z
+      for (int e = tid; e < cn * nf; e += BLOCK) {
+        const int a = e / nf, q = e - a * nf, ag = c0 + a;
+        const float ls = net[a * 2 * NFMAX + q], tr = net[a * 2 * NFMAX + nf + q];
+        const float u = tr + noise.normal((size_t)(a0 + ag) * nf + q) * expf(ls);
+        us[a * NFMAX + q] = u;
+        lq += -0.5f * u * u - ls;
+      }
+      __syncthreads();
+      for (int e = tid; e < cn * nf; e += BLOCK) {
+        const int a = e / nf, q = e - a * nf, ag = c0 + a;
+        float T = 0.f;
+        for (int q2 = 0; q2 < nf; ++q2) T += sm.h[ag * NFP + q2] * us[a * NFMAX + q2];
+        const float hv = sm.h[ag * NFP + q], u = us[a * NFMAX + q];
+        zs[a * NFMAX + q] = hv * u + (1.f - hv) * (T - softplus_f(T - u));
+        lq -= (1.f - hv) * logsigmoid_f(T - u);
+      }
+      __syncthreads();
+      for (int e = tid; e < cn * nf; e += BLOCK) {
+        const int a = e / nf, q = e - a * nf;
+        sm.h[(c0 + a) * NFP + q] = zs[a * NFMAX + q];
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    for (int e = tid; e < cn * nf; e += BLOCK) {
-      const int a = e / nf, q = e - a * nf, ag = c0 + a;
-      float T = 0.f;
-      for (int q2 = 0; q2 < nf; ++q2) T += sm.h[ag * NFP + q2] * us[a * NFMAX + q2];
-      const float hv = sm.h[ag * NFP + q], u = us[a * NFMAX + q];
-      zs[a * NFMAX + q] = hv * u + (1.f - hv) * (T - softplus_f(T - u));
-      lq -= (1.f - hv) * logsigmoid_f(T - u);
-    }
-    __syncthreads();
-    for (int e = tid; e < cn * nf; e += BLOCK) {
-      const int a = e / nf, q = e - a * nf;
-      sm.h[(c0 + a) * NFP + q] = zs[a * NFMAX + q];
-    }
-    __syncthreads();
   }
   return lq;
 }

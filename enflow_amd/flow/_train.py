@@ -38,7 +38,8 @@ class _FlowFunction(torch.autograd.Function):
         src = tuple(t.detach().contiguous() for t in (h, g, pos, vel))
         h_in = src[0]
         hw, gw, pw, vw = (torch.empty_like(t) for t in src)
-        tape = torch.empty(max(L.enflow_lf_tape_size(A, nf, hid, n_layers), 1), dtype=torch.float32, device=dev)
+        tape = torch.empty(max(L.enflow_lf_tape_size_for(A, nf, hid, n_layers, meta["max_n"]), 1),
+                           dtype=torch.float32, device=dev)
         # fused: unique pairs [n_layers][M]; large: the backward's pair rows per layer
         counts = torch.zeros(max(n_layers * (1 if meta["large"] else M), 1), dtype=torch.int32, device=dev)
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
@@ -322,7 +323,8 @@ class _EGCLFunction(torch.autograd.Function):
         hw, pw = h.clone(), pos.clone()
         gw = torch.zeros_like(h)
         vw = torch.zeros_like(pos)
-        tape = torch.empty(max(L.enflow_lf_tape_size(A, nf, hid, 1), 1), dtype=torch.float32, device=dev)
+        tape = torch.empty(max(L.enflow_lf_tape_size_for(A, nf, hid, 1, meta["max_n"]), 1), dtype=torch.float32,
+                           device=dev)
         counts = torch.zeros(max(M, 1), dtype=torch.int32, device=dev)
         ldj_mol = torch.empty(max(M, 1), dtype=torch.float32, device=dev)
         ldj = torch.empty(1, dtype=torch.float32, device=dev)

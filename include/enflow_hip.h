@@ -424,6 +424,11 @@ int enflow_alchemical_nll_f32(int num_mols, int num_atoms, int max_mol_atoms, in
 
 /* Floats of the training tape enflow_lf_forward_f32 writes. */
 int64_t enflow_lf_tape_size(int num_atoms, int node_nf, int hidden_nf, int n_layers);
+/* ABI 12: the same for a batch whose largest molecule has max_mol_atoms atoms:
+ * the tape's neighbour-list section (its tail) exists only for 33..64-atom
+ * molecules, the only instance that writes and reads it; other batches' tapes
+ * are that much smaller (~30-50 % at H = 128 / 32). */
+int64_t enflow_lf_tape_size_for(int num_atoms, int node_nf, int hidden_nf, int n_layers, int max_mol_atoms);
 
 /* Backward-only packed section of one EGCL layer (transposed MFMA fragments,
  * k-contiguous node weights): size in floats, and the packing kernel (same

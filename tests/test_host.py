@@ -92,6 +92,14 @@ def test_backward_sizes_and_argument_errors():
     A, M, nf, H, nl = 22 * 4, 4, 5, 128, 8
     # per layer and atom: h | message sums, g, pos, vel, Q, the pair-word slab (63) and the row's edge count
     assert L.enflow_lf_tape_size(A, nf, H, nl) == nl * A * (nf + H + nf + 3 + 3 + 1 + 63 + 1)
+    # the pair-word section only for the 33..64-atom instance that writes it
+    base = nl * A * (nf + H + nf + 3 + 3 + 1)
+    assert L.enflow_lf_tape_size_for(A, nf, H, nl, 22) == base
+    assert L.enflow_lf_tape_size_for(A, nf, H, nl, 32) == base
+    assert L.enflow_lf_tape_size_for(A, nf, H, nl, 33) == L.enflow_lf_tape_size(A, nf, H, nl)
+    assert L.enflow_lf_tape_size_for(A, nf, H, nl, 64) == L.enflow_lf_tape_size(A, nf, H, nl)
+    assert L.enflow_lf_tape_size_for(A, nf, H, nl, 65) == base
+    assert L.enflow_lf_tape_size_for(A, nf, H, nl, -1) == -1
     assert L.enflow_egcl_bwd_packed_size(H, nf) >= 2 * H * H
     assert L.enflow_egcl_bwd_packed_size(96, nf) == -1
     assert L.enflow_lf_backward_workspace_size(M, A, nf, H, nl, 4 * 480) > 4 * 480 * 5 * H * 4
