@@ -10,16 +10,19 @@
 // its three GEMMs from L2 (64 KB per GEMM per tile), one chain step ahead, so
 // each F16X3 step waits on an L2 round trip; the tile loop is ~60 % of a layer.
 //
-// Here the four waves of a workgroup share every tile and split its OUTPUT
-// features: wave w owns features 32 w .. 32 w + 31 of edge_nn.0, edge_nn.2 and
-// coord_nn.0 (H = 128), so its weight fragments of the three GEMMs (hi / lo
-// fp16, 36 KB) are loaded into registers once per layer (one wave per SIMD:
-// 512 registers).  A GEMM's input (all 128 features of the 32 pairs) is
-// exchanged through LDS as the producers' own fp16 hi / lo split, in the MFMA
-// B-operand lane layout (one ds_write_b128 / ds_read_b128 per lane and k-slice,
-// conflict-free); two barriers per tile.  Each wave segment-sums the messages of
-// its own 32 features (selection-matrix MFMAs as in edge_tiles) and the four
-// coord_nn.2 partial dots are added in wave order (deterministic).
+// Here the eight waves of a workgroup share every tile and split its OUTPUT
+// features over two pipeline stages: stage-A wave b (waves 0-3) owns features
+// 32 b .. 32 b + 31 of edge_nn.0 and edge_nn.2, stage-B wave b (waves 4-7) the
+// same features of coord_nn.0 and of the message sums (H = 128), so each wave's
+// weight blocks (hi / lo fp16, 16-20 KB) are loaded into registers once per
+// layer, during the pair build.  A GEMM's input (all 128 features of the 32
+// pairs) is exchanged through LDS as the producers' own fp16 hi / lo split, in
+// the MFMA B-operand lane layout (one ds_write_b128 / ds_read_b128 per lane and
+// k-slice, conflict-free); two barriers per pipeline step (fs_edge_tiles).  Each
+// stage-B wave segment-sums the messages of its own 32 features (selection-
+// matrix MFMAs as in edge_tiles) and the four coord_nn.2 partial dots are added
+// in block order (deterministic).  The node part is split the same way
+// (fs_node_g, the vel_scaling_nn items in the tiles' first step).
 //
 // SPLIT = 2 (at most half as many molecules as CUs): two workgroups per
 // molecule, on two CUs, each owning half of the molecule's rows.  Message and

@@ -86,8 +86,9 @@ int enflow_set_latency_threshold(int max_mols);
 int enflow_latency_threshold(void);
 
 /* ABI 12: the feature-split latency instance (H = 128, f16x3, inference): the
- * four waves of a workgroup share every 32-pair edge tile, each owning 32 of
- * its output features with those weights in registers.  Batches of at most
+ * eight waves of a workgroup share every 32-pair edge tile in a two-stage
+ * pipeline (four per stage), each owning 32 output features of its stage's
+ * GEMMs with those weights in registers.  Batches of at most
  * `max_mols` molecules that fit two workgroups per molecule on the device's
  * CUs run it with each molecule's rows split over two workgroups (one position
  * / feature hand-off per layer; -1 (default): CUs / 2; 0: never).
