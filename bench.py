@@ -345,6 +345,35 @@ def timed(step, steps, warmup, dist, device):
     return max_over_ranks(time.perf_counter() - t0, device)
 
 
+def module_call_timing(model, b, device, steps, warmup, reverse=False):
+    """The reference's own call surface, timed like timed(): ``model(data)``
+    (``model.reverse(data)`` for the generate mode) on a Data with the
+    reference's fields (enflow_amd.data.Data), under torch.no_grad(), per call:
+    the host's input handling, output allocation, the launch, the error word's
+    synchronous read (raised from the call, as the reference raises inside
+    forward) and the output dtype -- for fp32 inputs and for the reference's
+    own float64 (BaseFlow casts its model, enflow/flow/base.py:12).  Each call
+    gets a shallow copy of the batch (the reference rebinds data's tensors to
+    the outputs), so every call transforms the same inputs."""
+    from enflow_amd.data import Data
+    out = {}
+    for name, dt in (("float32", torch.float32), ("float64", torch.float64)):
+        d = Data.from_arrays(b, device=device, dtype=dt)
+        if reverse:     # generate direction: invert one forward output (main.py:263-278)
+            with torch.no_grad():
+                d, _ = model(d._replace())
+        call = (lambda: model.reverse(d._replace())) if reverse else (lambda: model(d._replace()))
+
+        def step():
+            with torch.no_grad():
+                call()
+        el = timed(step, steps, warmup, None, device)
+        out[name] = {"ms_per_call": el / steps * 1e3, "calls": steps}
+    out["note"] = ("model.reverse(data)" if reverse else "model(data)") + \
+        " under torch.no_grad() on enflow_amd.data.Data, one synchronous error-word read per call"
+    return out
+
+
 def kernel_times(step, steps):
     """Per-kernel average launch duration (ms) over `steps` steps, from the
     library's HIP-event timer (events on each kernel's own launch stream)."""
@@ -483,6 +512,11 @@ def run_flow(args, world, rank, device, dist, cpu):
     kname = "lf_flow_kernel<rev>" if c["reverse"] else "lf_flow_kernel<fwd>"
     run.check()
 
+    module_call = None
+    if args.mode in ("forward", "generate") and world == 1:
+        module_call = module_call_timing(model, b, device, args.steps, args.warmup, reverse=c["reverse"])
+        module_call["bench_entry_ms_per_step"] = elapsed / args.steps * 1e3
+
     strong = None
     if args.mode == "forward":
         if world > 1:
@@ -531,6 +565,8 @@ def run_flow(args, world, rank, device, dist, cpu):
         }
         if strong is not None:
             line["strong_scaling"] = strong
+        if module_call is not None:
+            line["module_call"] = module_call
         print(json.dumps(line), flush=True)
 
 

@@ -29,6 +29,7 @@ ERR_RERUN = ERR_RANGE | ERR_SMALL   # bits an fp32-GEMM re-run of the flagged mo
 DEQUANT_NONE, DEQUANT_ARGMAX, DEQUANT_FLOOR = 0, 1, 2
 PREC_F32, PREC_F16X3, PREC_BF16 = 0, 1, 2
 PRECISIONS = {"f32": PREC_F32, "f16x3": PREC_F16X3, "bf16": PREC_BF16}
+PREC_NO_SPLIT = 0x400   # ABI 13, ENFLOW_PREC_NO_SPLIT: OR into gemm_precision, this launch skips the split instances
 EGCL_ATTENTION, EGCL_NORM_DIFF, EGCL_TANH, EGCL_ACT = 1, 2, 4, 8   # ENFLOW_EGCL_* (include/enflow_hip.h)
 EGCL_VARIANTS = 0x100                                  # OR into gemm_precision
 BWD_F32 = 0x200                                        # ENFLOW_BWD_F32: OR into the backward's dequant_kind
@@ -43,6 +44,7 @@ SIGNATURES = {
     "enflow_latency_threshold": (_i, []),
     "enflow_set_split_threshold": (_i, [_i]),
     "enflow_set_fs_threshold": (_i, [_i]),
+    "enflow_set_handoff_spin_limit": (_i, [_i]),
     "enflow_max_atoms": (_i, []),
     "enflow_max_node_nf": (_i, []),
     "enflow_supports_hidden": (_i, [_i]),
@@ -156,6 +158,8 @@ def lib(nf=None):
             handle.enflow_set_split_threshold(_split_threshold[0])
         if _fs_threshold[0] is not None and hasattr(handle, "enflow_set_fs_threshold"):
             handle.enflow_set_fs_threshold(_fs_threshold[0])
+        if _spin_limit[0] is not None and hasattr(handle, "enflow_set_handoff_spin_limit"):
+            handle.enflow_set_handoff_spin_limit(_spin_limit[0])
         _libs[path] = handle
     return handle
 
@@ -179,6 +183,21 @@ def set_latency_threshold(max_mols):
 
 _split_threshold = [None]
 _fs_threshold = [None]
+_spin_limit = [None]
+
+
+def set_handoff_spin_limit(polls):
+    """Polls a workgroup of the two-workgroup split instance makes for one
+    partner granule before it gives up with ENFLOW_ERR_HANDOFF (-1: the
+    default 2^20; 0: give up without polling -- forces the host's re-run, for
+    tests).  Every loaded library and any loaded later; returns the previous
+    setting (None: never set from Python)."""
+    prev = _spin_limit[0]
+    _spin_limit[0] = int(polls)
+    for h in _libs.values():
+        if hasattr(h, "enflow_set_handoff_spin_limit"):
+            h.enflow_set_handoff_spin_limit(int(polls))
+    return prev
 
 
 def set_split_threshold(max_mols):
@@ -209,8 +228,8 @@ def set_fs_threshold(max_mols):
 
 
 def ptr(t):
-    """Device pointer of a tensor (None -> NULL)."""
-    return None if t is None else ctypes.c_void_p(t.data_ptr())
+    """Device pointer of a tensor (None -> NULL), as the int the c_void_p argtypes take."""
+    return None if t is None else t.data_ptr()
 
 
 def stream_ptr(device):
@@ -297,6 +316,12 @@ _pending = []
 # it); FP32_MOL_RERUNS: molecules of the inference re-runs that ran only the flagged molecules
 FP32_RERUNS = [0]
 FP32_MOL_RERUNS = [0]
+# inference launches re-run without the split instances after an ENFLOW_ERR_HANDOFF (tests read it)
+HANDOFF_RERUNS = [0]
+# deferred-check training steps whose word held ENFLOW_ERR_SMALL alone (warned, not re-run): a caller
+# that needs every step at fp32 accuracy reads it, or sets STRICT_SMALL[0] = True to raise instead
+DEFERRED_SMALL_STEPS = [0]
+STRICT_SMALL = [False]
 
 
 def defer_err(err_flag, small_warns=False):
@@ -319,7 +344,8 @@ def check_pending():
         ev, host, small_warns = _pending.pop(0)
         ev.synchronize()
         e = int(host.item())
-        if small_warns and e == ERR_SMALL:
+        if small_warns and e == ERR_SMALL and not STRICT_SMALL[0]:
+            DEFERRED_SMALL_STEPS[0] += 1
             import warnings
             warnings.warn("enflow_amd: a deferred-check training step ran an f16x3 GEMM whose operand was "
                           "entirely below 2^-7 (gradients ~1e-5 relative instead of fp32 accuracy); set "
@@ -369,6 +395,40 @@ def status_word(device):
         st = torch.zeros(2, dtype=torch.int32, device=device)
         _status[key] = st
     return st
+
+
+class _InferWords:
+    """Per-(device, stream) buffers of the inference module calls, zero
+    between calls (the kernels OR bits into them; a call that finds any set
+    zeroes them before it returns): the status word pair (error word, log|detJ|
+    ticket), the reverse's (error word, ArgMax index maximum), per-molecule
+    error words, and the scratch the caller never sees (per-molecule log|detJ|,
+    the reverse's ArgMax indices).  Grown on demand, never shrunk."""
+    __slots__ = ("status", "rev", "mol_err", "ldj_mol", "idx", "cap_m", "cap_a")
+
+
+def infer_words(device, num_mols, num_atoms=0):
+    key = (str(device), torch.cuda.current_stream(device).cuda_stream)
+    w = _words.get(key)
+    if w is None:
+        w = _InferWords()
+        w.status = status_word(device)
+        w.rev = torch.zeros(2, dtype=torch.int32, device=device)
+        w.cap_m = w.cap_a = -1
+        _words[key] = w
+    if num_mols > w.cap_m:
+        cap = max(num_mols, 1)
+        w.mol_err = torch.zeros(cap, dtype=torch.int32, device=device)
+        w.ldj_mol = torch.empty(cap, dtype=torch.float32, device=device)
+        w.cap_m = cap
+    if num_atoms > w.cap_a:
+        cap = max(num_atoms, 1)
+        w.idx = torch.empty(cap, dtype=torch.int32, device=device)
+        w.cap_a = cap
+    return w
+
+
+_words = {}
 
 
 def _raise_code(e):

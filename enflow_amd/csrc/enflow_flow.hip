@@ -488,7 +488,9 @@ static int lat_threshold_now() {
 
 template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
-  if (NN == 32 && enflow_fs_launch(HH, REV, prec, num_mols, st, &A)) return;
+  // ENFLOW_PREC_NO_SPLIT (ABI 13): this launch skips the feature-split instances
+  if (NN == 32 && !(prec & ENFLOW_PREC_NO_SPLIT) && enflow_fs_launch(HH, REV, prec, num_mols, st, &A)) return;
+  prec &= ~ENFLOW_PREC_NO_SPLIT;
   if (NN == 32 && num_mols <= lat_threshold_now() && enflow_lat_launch(HH, REV, prec, num_mols, st, &A)) return;
   if (prec & ENFLOW_EGCL_VARIANTS) launch_flow_v<HH, NN, RBB, REV, true>(prec & 0xff, num_mols, st, A);
   else launch_flow_v<HH, NN, RBB, REV, false>(prec, num_mols, st, A);
@@ -578,8 +580,8 @@ int enflow_lf_forward_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, in
                              uint64_t* pair_stats, float* tape, int32_t* pair_counts, int gemm_precision,
                              int32_t* mol_err, const int32_t* mol_list, int num_listed, void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
-  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
-      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
+  if ((gemm_precision & ~(ENFLOW_EGCL_VARIANTS | ENFLOW_PREC_NO_SPLIT)) < ENFLOW_PREC_F32 ||
+      (gemm_precision & ~(ENFLOW_EGCL_VARIANTS | ENFLOW_PREC_NO_SPLIT)) > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && !dequant)) return -1;
   if (!h || !g || !pos || !vel || !ldj_mol || !ldj_total || !err_flag) return -1;
@@ -656,8 +658,8 @@ int enflow_lf_reverse_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, in
                              int32_t* argmax_idx, int32_t* max_idx, int32_t* err_flag, int gemm_precision,
                              int32_t* mol_err, const int32_t* mol_list, int num_listed, void* stream) {
   int rc = check_common(num_mols, max_mol_atoms, nf, H);
-  if ((gemm_precision & ~ENFLOW_EGCL_VARIANTS) < ENFLOW_PREC_F32 ||
-      (gemm_precision & ~ENFLOW_EGCL_VARIANTS) > ENFLOW_PREC_BF16) return -1;
+  if ((gemm_precision & ~(ENFLOW_EGCL_VARIANTS | ENFLOW_PREC_NO_SPLIT)) < ENFLOW_PREC_F32 ||
+      (gemm_precision & ~(ENFLOW_EGCL_VARIANTS | ENFLOW_PREC_NO_SPLIT)) > ENFLOW_PREC_BF16) return -1;
   if (rc) return rc;
   if (n_layers < 0 || (dequant_kind == ENFLOW_DEQUANT_ARGMAX && (!argmax_idx || !max_idx))) return -1;
   if (!h || !g || !pos || !vel || !err_flag) return -1;

@@ -87,7 +87,29 @@ struct FsArgs {
   float* part;         // [blocks] log|detJ| partial per workgroup
   int split;           // 1 or 2
   int blocks;
+  int spin_limit;      // polls per hand-off wait before ENFLOW_ERR_HANDOFF (enflow_set_handoff_spin_limit)
 };
+
+// one hand-off wait (SPLIT = 2): poll the partner's granule until it carries
+// `tag`, at most `limit` polls; a wait that gives up sets F.timeout, and once
+// set every later wait of the workgroup gives up after its first poll, so a
+// lost partner costs one bounded wait per workgroup, not one per granule and
+// layer.  limit 0 gives up without polling (the forced ENFLOW_ERR_HANDOFF path).
+template <class FS>
+__device__ __forceinline__ uint64_t fs_poll(FS& F, const uint64_t* slot, uint32_t tag, int limit) {
+  uint64_t g = 0;
+  for (int spins = 0;; ++spins) {
+    if (spins >= limit) {
+      F.timeout = 1;
+      break;
+    }
+    g = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((uint32_t)(g >> 32) == tag) break;
+    if (*reinterpret_cast<volatile int*>(&F.timeout)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return g;
+}
 
 // the wave's weight blocks (F16X3 fragments, registers): stage A (waves
 // 0 .. NT - 1) block b of edge_nn.0 and edge_nn.2, stage B block b of coord_nn.0
@@ -576,24 +598,15 @@ __device__ __forceinline__ void fs_publish(FsSmem<H>& F, uint64_t* slot, int r0,
     __hip_atomic_store(slot + a * XG + k, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
-// wait for the partner's atoms [r0, r0 + rb) of this tag (bounded: ~0.1 s, then ENFLOW_ERR_HANDOFF)
+// wait for the partner's atoms [r0, r0 + rb) of this tag (bounded: fs_poll, then ENFLOW_ERR_HANDOFF)
 template <int H>
-__device__ __forceinline__ void fs_consume(FsSmem<H>& F, const uint64_t* slot, int r0, int rb, int nf, uint32_t tag) {
+__device__ __forceinline__ void fs_consume(FsSmem<H>& F, const uint64_t* slot, int r0, int rb, int nf, uint32_t tag,
+                                           int limit) {
   auto& sm = F.s;
   const int per = 3 + nf;
   for (int e = threadIdx.x; e < rb * per; e += BLOCK) {
     const int a = e / per, k = e - a * per;
-    uint64_t g = 0;
-    int spins = 0;
-    for (;;) {
-      g = __hip_atomic_load(slot + a * XG + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((uint32_t)(g >> 32) == tag) break;
-      if (++spins > (1 << 20)) {
-        F.timeout = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    const uint64_t g = fs_poll(F, slot + a * XG + k, tag, limit);
     const float v = __uint_as_float((uint32_t)g);
     if (k < 3) sm.pos[(r0 + a) * 3 + k] = v;
     else sm.h[(r0 + a) * NFP + (k - 3)] = v;
@@ -703,7 +716,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
         if constexpr (SPLIT == 2) {
           const uint32_t tag = xtag(epoch, 0x7f);
           fs_publish(F, xmine + XSLOT, r0, rb, nf, tag);
-          fs_consume(F, xpart + XSLOT, pr0, prb, nf, tag);
+          fs_consume(F, xpart + XSLOT, pr0, prb, nf, tag, X.spin_limit);
         }
       }
     }
@@ -756,19 +769,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
         __hip_atomic_store(xmine + (k & 1) * XSLOT + a * XG + c, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       };
       auto get = [&](int k, int a, int c) {            // a: row within the partner's block
-        const uint32_t tag = xtag(epoch, k);
-        const uint64_t* const slot = xpart + (k & 1) * XSLOT + a * XG + c;
-        uint64_t g = 0;
-        int spins = 0;
-        for (;;) {
-          g = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint32_t)(g >> 32) == tag) break;
-          if (++spins > (1 << 20)) {
-            F.timeout = 1;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
+        const uint64_t g = fs_poll(F, xpart + (k & 1) * XSLOT + a * XG + c, xtag(epoch, k), X.spin_limit);
         return __uint_as_float((uint32_t)g);
       };
       const float* nb = F.nb[it & 1];
@@ -778,8 +779,8 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
       static_assert(HALF * NFMAX <= BLOCK, "one partner feature granule per thread");
       if (hget) {
         const int a = he / nfl, q = he - a * nfl;
-        sm.h[(pr0 + a) * NFP + q] = (uint32_t)(hg >> 32) == xtag(epoch, it - 1) ? __uint_as_float((uint32_t)hg)
-                                                                              : get(it - 1, a, 3 + q);
+        sm.h[(pr0 + a) * NFP + q] = ((uint32_t)(hg >> 32) == xtag(epoch, it - 1) && X.spin_limit > 0)
+                                        ? __uint_as_float((uint32_t)hg) : get(it - 1, a, 3 + q);
       }
       fs_edge_tiles<H, KS0>(F, Lp, L, Ml, nfl, tid_l, r0, rb, Wt, nb STAMP_PASS);
       STAMP(5);
@@ -974,6 +975,8 @@ XBuf g_buf[64];
 int g_nbuf = 0;
 int g_split_threshold = -1;   // SPLIT = 2 for batches of at most this many molecules (-1: CUs / 2)
 int g_fs_threshold = -1;      // SPLIT = 1 for batches of at most this many molecules (-1: CUs; 0: off)
+constexpr int kSpinDefault = 1 << 20;
+int g_spin_limit = kSpinDefault;   // polls per hand-off wait (enflow_set_handoff_spin_limit)
 int g_cus[64];
 
 int cus_of(int dev) {
@@ -1034,9 +1037,16 @@ int enflow_fs_split_for(int num_mols) {
 
 bool enflow_fs_launch(int H, bool rev, int prec, int num_mols, hipStream_t st, const void* flow_args) {
   const auto& A = *static_cast<const enflow_fs::FlowArgs*>(flow_args);
-  if (H != 128 || prec != ENFLOW_PREC_F16X3 || A.tape != nullptr || A.nf > NFMAX || A.mol_list != nullptr) return false;
-  const int split = enflow_fs_split_for(num_mols);
+  if (H != 128 || prec != ENFLOW_PREC_F16X3 || A.tape != nullptr || A.nf > NFMAX || A.mol_list != nullptr ||
+      A.n_layers < 1)
+    return false;
+  int split = enflow_fs_split_for(num_mols);
   if (split == 0) return false;
+  // in place, a half could overwrite rows its partner has not read yet (a
+  // one-layer flow has no hand-off to order them), and a re-run after
+  // ENFLOW_ERR_HANDOFF would start from overwritten inputs: one workgroup per
+  // molecule instead (it reads its whole molecule before it writes anything)
+  if (split == 2 && !(A.h_in && A.g_in && A.pos_in && A.vel_in)) split = 1;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return false;
   XBuf* B = buffers(dev, st, num_mols);
@@ -1047,6 +1057,7 @@ bool enflow_fs_launch(int H, bool rev, int prec, int num_mols, hipStream_t st, c
   X.part = B->part;
   X.split = split;
   X.blocks = split == 2 ? ((2 * num_mols + 15) / 16) * 16 : num_mols;
+  X.spin_limit = g_spin_limit;
   enflow_fs::FlowArgs Ak = A;
   Ak.ticket = nullptr;   // the instance reduces through its own ticket (FsArgs::ctl)
   Ak.num_mols = num_mols;   // (the reverse entry leaves it unset: whole-tile kernels index by block)
@@ -1088,6 +1099,11 @@ int enflow_set_split_threshold(int max_mols) {
 int enflow_set_fs_threshold(int max_mols) {
   const int prev = g_fs_threshold;
   g_fs_threshold = max_mols < 0 ? -1 : max_mols;
+  return prev;
+}
+int enflow_set_handoff_spin_limit(int polls) {
+  const int prev = g_spin_limit;
+  g_spin_limit = polls < 0 ? kSpinDefault : polls;
   return prev;
 }
 }  // extern "C"

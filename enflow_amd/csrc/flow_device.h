@@ -11,7 +11,7 @@
 #include "enflow_hip.h"
 #include "enflow_timing.h"
 
-#define ENFLOW_ABI 12
+#define ENFLOW_ABI 13
 #ifndef WAVES
 #define WAVES 4    // waves per workgroup (the latency build, enflow_latency.hip, uses 8)
 #endif

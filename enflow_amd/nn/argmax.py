@@ -9,7 +9,7 @@ import torch
 from torch import nn
 
 from .. import _lib
-from ..utils.helpers import one_hot, mol_ptr_from_counts
+from ..utils.helpers import one_hot, mol_ptr_from_counts, params_of
 from ._act import SILU, act_code, act_kind, check_trainable
 from ._pad import ARGMAX_HDIMS, Geom, flat_padded, kernel_hidden
 
@@ -65,8 +65,7 @@ class ArgMax(nn.Module):
 
     def packed(self, device, width=None):
         width = width or self.kernel_hidden
-        params = [p for _, p in self.named_parameters()]
-        key = (str(device), width) + tuple((p.data_ptr(), p._version) for p in params)
+        key = (str(device), width) + tuple((p.data_ptr(), p._version) for p in params_of(self))
         if self._packed is not None and self._packed_key == key:
             return self._packed
         L = _lib.lib(self.node_nf)

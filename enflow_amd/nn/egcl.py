@@ -14,6 +14,7 @@ from .. import _lib
 from ..data.base import Edges
 from ._act import SILU, act_code, act_kind, check_trainable, supported as act_supported
 from ._pad import EGCL_HDIMS, Geom, flat_padded, kernel_hidden
+from ..utils.helpers import params_of
 
 
 class EGCL(nn.Module):
@@ -140,8 +141,7 @@ class EGCL(nn.Module):
     def packed(self, device):
         """MFMA-fragment packed fp32 weights on `device` (cached, re-packed when
         any parameter changes)."""
-        params = [p for _, p in self.named_parameters()]
-        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params)
+        key = (str(device),) + tuple((p.data_ptr(), p._version) for p in params_of(self))
         if self._packed is not None and self._packed_key == key:
             return self._packed
         L = _lib.lib(self.kernel_nf)

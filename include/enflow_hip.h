@@ -53,6 +53,11 @@ extern "C" {
 #define ENFLOW_PREC_F32   0  /* v_mfma_f32_32x32x2_f32: exact fp32 FMA chain          */
 #define ENFLOW_PREC_F16X3 1  /* fp32 operands split hi+lo in fp16, 3 products, fp32 acc */
 #define ENFLOW_PREC_BF16  2  /* bf16 operands, fp32 accumulation                       */
+/* ABI 13: OR into gemm_precision of the forward / reverse io / io2 entries: the
+ * launch does not take the feature-split instances (enflow_set_split_threshold /
+ * enflow_set_fs_threshold) whatever the thresholds say -- the per-call re-run
+ * after ENFLOW_ERR_HANDOFF, without touching the process-wide setting. */
+#define ENFLOW_PREC_NO_SPLIT 0x400
 
 #define ENFLOW_DEQUANT_NONE   0
 #define ENFLOW_DEQUANT_ARGMAX 1  /* enflow/nn/argmax.py */
@@ -71,7 +76,8 @@ extern "C" {
  * small, ENFLOW_BWD_F32 -- the fp32-GEMM backward for a tape recorded by an ENFLOW_PREC_F32
  * forward); 12: ENFLOW_ERR_SMALL split from ENFLOW_ERR_RANGE, ENFLOW_ERR_HANDOFF, the feature-split
  * latency instance (enflow_set_split_threshold / enflow_set_fs_threshold), per-molecule error words
- * and molecule lists (enflow_lf_forward_io2_f32 / enflow_lf_reverse_io2_f32). */
+ * and molecule lists (enflow_lf_forward_io2_f32 / enflow_lf_reverse_io2_f32); 13: ENFLOW_PREC_NO_SPLIT,
+ * enflow_set_handoff_spin_limit, the two-workgroup split only for out-of-place launches). */
 int enflow_abi_version(void);
 
 /* Batches of <= 32-atom molecules with at most this many molecules run the
@@ -96,9 +102,20 @@ int enflow_latency_threshold(void);
  * take that split run it with one workgroup per molecule (-1 (default): the
  * device's CU count, one round of workgroups; 0: never).
  * Same strong-scaling role as enflow_set_latency_threshold (enflow/main.py:
- * 141-145); both return the previous setting. */
+ * 141-145); both return the previous setting.
+ * ABI 13: the two-workgroup split runs only out of place (h_in, g_in, pos_in,
+ * vel_in all non-NULL): in place, the two halves of a molecule would read rows
+ * the partner may already have overwritten (one-layer flows have no hand-off
+ * to order them), so such launches take one workgroup per molecule. */
 int enflow_set_split_threshold(int max_mols);
 int enflow_set_fs_threshold(int max_mols);
+/* ABI 13: polls a waiting workgroup of the two-workgroup split makes for one
+ * partner granule before it gives up (ENFLOW_ERR_HANDOFF; once one wait of a
+ * workgroup has given up, its later waits give up at once).  Default (-1):
+ * 2^20, ~0.1 s.  0: every wait gives up without polling -- forces the
+ * ENFLOW_ERR_HANDOFF path, for testing the host's re-run.  Per library;
+ * returns the previous setting. */
+int enflow_set_handoff_spin_limit(int polls);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept.  The ABI
  * ships as two builds of the same sources: libenflow_hip.so (node_nf <= 8) and

@@ -38,7 +38,7 @@ def test_node_feature_library_selection():
     assert _lib.lib_path(5) == _lib.lib_path(None) == _lib.LIB_PATH
     assert _lib.lib_path(8) == _lib.LIB_PATH and _lib.lib_path(9) == _lib.LIB_NF16_PATH
     L16 = _lib.lib(16)
-    assert L16.enflow_abi_version() == 12 and L16.enflow_max_node_nf() == 16
+    assert L16.enflow_abi_version() == 13 and L16.enflow_max_node_nf() == 16
     assert L16.enflow_egcl_packed_size(128, 16) > 0 and L16.enflow_egcl_packed_size(128, 17) == -1
     # training: every node_nf of the build (nf 16's radial row past the transposed
     # edge_nn.0 GEMM's 32-row tile is a dot product of its own), not past it
@@ -52,7 +52,7 @@ def test_node_feature_library_selection():
 
 def test_abi_queries():
     L = _lib.lib()
-    assert L.enflow_abi_version() == 12
+    assert L.enflow_abi_version() == 13
     assert L.enflow_max_atoms() == 256
     assert L.enflow_max_node_nf() == 8
     for h in (32, 64, 128):
