@@ -359,6 +359,14 @@ class LFIntegrator(BaseFlow):
             cfg = redo
             launch(cfg)
         prec = cfg.prec
+        dt, pdt = data.h.dtype, data.pos.dtype
+
+        def outputs():      # in the data's dtypes, queued behind the launch (no-ops for fp32 data)
+            return (_as_dtype(s["h"], dt), _as_dtype(s["g"], dt), _as_dtype(s["pos"], pdt),
+                    _as_dtype(s["vel"], data.vel.dtype), _as_dtype(ldj.reshape(()), dt))
+
+        outs = outputs()    # a float64 caller's conversions run while the host waits for the word
+        reran = False
         while check_errors:
             e = _lib.take_err(st[:1])
             if e & _lib.ERR_HANDOFF and not e & ~(_lib.ERR_HANDOFF | _lib.ERR_RERUN):
@@ -369,6 +377,7 @@ class LFIntegrator(BaseFlow):
                 if mol_err is not None:
                     mol_err.zero_()
                 launch(cfg, prec)
+                reran = True
                 e = _lib.take_err(st[:1])
             if _retry_fp32(e, prec):
                 # a split-precision operand left its range (or was entirely small): the
@@ -385,15 +394,16 @@ class LFIntegrator(BaseFlow):
                         _lib.FP32_MOL_RERUNS[0] += mol_list.numel()
                     mol_err.zero_()
                 launch(cfg, prec, mol_list)
+                reran = True
                 e = _lib.take_err(st[:1])
             if e and mol_err is not None:
                 mol_err.zero_()      # the cached words stay zero between calls
             _lib.raise_code(e)
             break
-        dt = data.h.dtype
-        data.h, data.g = _as_dtype(s["h"], dt), _as_dtype(s["g"], dt)
-        data.pos, data.vel = _as_dtype(s["pos"], data.pos.dtype), _as_dtype(s["vel"], data.vel.dtype)
-        return data, _as_dtype(ldj.reshape(()), dt)
+        if reran:
+            outs = outputs()
+        data.h, data.g, data.pos, data.vel, ldj_out = outs
+        return data, ldj_out
 
     def reverse(self, data, check_errors=True):
         """dynamics.py:26-37 (ends with dequantize.reverse).  The same

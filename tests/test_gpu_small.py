@@ -264,11 +264,25 @@ def test_deferred_training_check_small_warns_overflow_raises():
     model, b = _small_model_and_batch(1e-4, "edge0")
     model.defer_error_check = True
     u = torch.rand(b["h"].shape, device=DEV)
+    n0 = _lib.DEFERRED_SMALL_STEPS[0]
     out, ldj = model(Data.from_arrays(b, device=DEV), noise=u)
     loss = Alchemical_NLL(kBT=default_kBT(), softening=0.1)(out, ldj)
     with pytest.warns(RuntimeWarning, match="below 2\\^-7"):
         loss.backward()
         _lib.check_pending()
+    assert not _lib._pending
+    assert _lib.DEFERRED_SMALL_STEPS[0] == n0 + 1           # the warned step is counted
+    # STRICT_SMALL: the same step raises instead of warning
+    _lib.STRICT_SMALL[0] = True
+    try:
+        out, ldj = model(Data.from_arrays(b, device=DEV), noise=u)
+        loss = Alchemical_NLL(kBT=default_kBT(), softening=0.1)(out, ldj)
+        with pytest.raises(_lib.RangeError):
+            loss.backward()
+            _lib.check_pending()
+    finally:
+        _lib.STRICT_SMALL[0] = False
+    _lib.check_pending()
     assert not _lib._pending
     model, b = _range_train_model_and_batch()
     model.defer_error_check = True
