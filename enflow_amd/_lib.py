@@ -45,6 +45,7 @@ SIGNATURES = {
     "enflow_set_split_threshold": (_i, [_i]),
     "enflow_set_fs_threshold": (_i, [_i]),
     "enflow_set_handoff_spin_limit": (_i, [_i]),
+    "enflow_set_dequant_ahead": (_i, [_i]),
     "enflow_max_atoms": (_i, []),
     "enflow_max_node_nf": (_i, []),
     "enflow_supports_hidden": (_i, [_i]),
@@ -86,6 +87,8 @@ SIGNATURES = {
     "enflow_lf_tape_size_for": (_i64, [_i, _i, _i, _i, _i]),
     "enflow_egcl_bwd_packed_size": (_i64, [_i, _i]),
     "enflow_pack_egcl_bwd_f32": (_i, [_p, _i, _i, _p, _p]),
+    "enflow_pack_egcl_layers_f32": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
+    "enflow_pack_egcl_bwd_layers_f32": (_i, [_p, _i64, _i, _i, _i, _p, _p]),
     "enflow_lf_backward_workspace_size": (_i64, [_i, _i, _i, _i, _i, _i64]),
     "enflow_lf_backward_workspace_size_min": (_i64, [_i, _i, _i, _i, _i, _i64]),
     "enflow_alchemical_nll_backward_f32": (_i, [_i, _i, _i, _i, _p, _p, _p, _p, _p, _f, _f, _p,
@@ -160,6 +163,8 @@ def lib(nf=None):
             handle.enflow_set_fs_threshold(_fs_threshold[0])
         if _spin_limit[0] is not None and hasattr(handle, "enflow_set_handoff_spin_limit"):
             handle.enflow_set_handoff_spin_limit(_spin_limit[0])
+        if _dq_ahead[0] is not None and hasattr(handle, "enflow_set_dequant_ahead"):
+            handle.enflow_set_dequant_ahead(_dq_ahead[0])
         _libs[path] = handle
     return handle
 
@@ -184,6 +189,19 @@ def set_latency_threshold(max_mols):
 _split_threshold = [None]
 _fs_threshold = [None]
 _spin_limit = [None]
+_dq_ahead = [None]
+
+
+def set_dequant_ahead(on):
+    """ArgMax dequantisation of <= 64-atom forward launches as its own kernel
+    ahead of the flow kernel (True, the default) or fused into it (False, A/B).
+    Every loaded library and any loaded later; returns the previous setting."""
+    prev = _dq_ahead[0]
+    _dq_ahead[0] = 1 if on else 0
+    for h in _libs.values():
+        if hasattr(h, "enflow_set_dequant_ahead"):
+            h.enflow_set_dequant_ahead(_dq_ahead[0])
+    return prev
 
 
 def set_handoff_spin_limit(polls):

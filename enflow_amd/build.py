@@ -30,7 +30,7 @@ OUT_NF16 = os.path.join(HERE, "libenflow_hip_nf16.so")
 VARIANTS = [(OUT, ()), (OUT_NF16, ("ENFLOW_NFMAX=16",))]
 # diagnostic / A-B switches that never go into a product library
 DIAGNOSTIC = ("ENFLOW_STAMPS", "ENFLOW_DEV_ONLY", "ENFLOW_BWD_ABLATE", "ENFLOW_SKEW", "ENFLOW_PRIO",
-              "ENFLOW_CHAIN_PRIO", "ENFLOW_AUX_PRIO")
+              "ENFLOW_CHAIN_PRIO", "ENFLOW_AUX_PRIO", "ENFLOW_ABLATE_DEQUANT")
 
 
 class HazardError(RuntimeError):

@@ -30,7 +30,7 @@
 // ---------------------------------------------------------------------------
 // packing of the backward weight section
 // ---------------------------------------------------------------------------
-__global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
+__device__ __forceinline__ void pack_egcl_bwd_body(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
   const EgclBwdLayout L = egcl_bwd_layout(H);
   const RawEgcl R = raw_egcl(H, nf);
   const int NT = H / 32;
@@ -115,9 +115,23 @@ __global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int n
   }
 }
 
+__global__ void pack_egcl_bwd_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
+  pack_egcl_bwd_body(raw, H, nf, out);
+}
+// every layer at once: layer blockIdx.y at raw + y raw_stride, out + y stride
+__global__ void pack_egcl_bwd_layers_kernel(const float* __restrict__ raw, int64_t raw_stride, int H, int nf,
+                                            float* __restrict__ out, int64_t stride) {
+  pack_egcl_bwd_body(raw + blockIdx.y * raw_stride, H, nf, out + blockIdx.y * stride);
+}
+
 __global__ void __launch_bounds__(256) egcl_bwd_scale_kernel(const float* __restrict__ raw, int H, int nf,
                                                              float* __restrict__ out) {
   egcl_scales_block(raw, H, nf, out + egcl_bwd_layout(H).scl);
+}
+__global__ void __launch_bounds__(256) egcl_bwd_scale_layers_kernel(const float* __restrict__ raw, int64_t raw_stride,
+                                                                    int H, int nf, float* __restrict__ out,
+                                                                    int64_t stride) {
+  egcl_scales_block(raw + blockIdx.y * raw_stride, H, nf, out + blockIdx.y * stride + egcl_bwd_layout(H).scl);
 }
 
 __device__ __forceinline__ float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
@@ -2761,6 +2775,19 @@ int enflow_pack_egcl_bwd_f32(const float* raw, int H, int nf, float* packed, voi
   const int total = egcl_bwd_layout(H).total;
   hipLaunchKernelGGL(egcl_bwd_scale_kernel, dim3(6), dim3(256), 0, SB(stream), raw, H, nf, packed);
   hipLaunchKernelGGL(pack_egcl_bwd_kernel, dim3(cdiv(total, 256)), dim3(256), 0, SB(stream), raw, H, nf, packed);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int enflow_pack_egcl_bwd_layers_f32(const float* raw, int64_t raw_stride, int n_layers, int H, int nf,
+                                    float* packed, void* stream) {
+  if (!hid_ok_b(H) || nf < 1 || nf > BWD_NFMAX || !raw || !packed || n_layers < 0 || n_layers > 65535) return -1;
+  if (raw_stride < raw_egcl(H, nf).total) return -1;
+  if (n_layers == 0) return 0;
+  const int total = egcl_bwd_layout(H).total;
+  hipLaunchKernelGGL(egcl_bwd_scale_layers_kernel, dim3(6, n_layers), dim3(256), 0, SB(stream), raw, raw_stride, H, nf,
+                     packed, (int64_t)total);
+  hipLaunchKernelGGL(pack_egcl_bwd_layers_kernel, dim3(cdiv(total, 256), n_layers), dim3(256), 0, SB(stream), raw,
+                     raw_stride, H, nf, packed, (int64_t)total);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

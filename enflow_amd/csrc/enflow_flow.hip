@@ -25,6 +25,7 @@
 //
 // All arithmetic is float32; MFMA f32 is an exact fmaf chain.
 
+#include <mutex>
 #include "enflow_large.h"
 #include "enflow_latency.h"
 #include "enflow_split.h"
@@ -32,8 +33,9 @@
 // ---------------------------------------------------------------------------
 // packing kernels
 // ---------------------------------------------------------------------------
-__global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out, int flags,
-                                 const float* __restrict__ att, int act_kind, float act_p0, float act_p1) {
+__device__ __forceinline__ void pack_egcl_body(const float* __restrict__ raw, int H, int nf, float* __restrict__ out,
+                                               int flags, const float* __restrict__ att, int act_kind, float act_p0,
+                                               float act_p1) {
   const EgclLayout L = egcl_layout(H, nf);
   const RawEgcl R = raw_egcl(H, nf);
   const int NT = H / 32;
@@ -180,10 +182,26 @@ __global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, f
   }
 }
 
+__global__ void pack_egcl_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out, int flags,
+                                 const float* __restrict__ att, int act_kind, float act_p0, float act_p1) {
+  pack_egcl_body(raw, H, nf, out, flags, att, act_kind, act_p0, act_p1);
+}
+// every layer of a default-flag (SiLU, no variants) flow at once: layer blockIdx.y
+// at raw + y raw_stride, packed + y stride (enflow_pack_egcl_layers_f32)
+__global__ void pack_egcl_layers_kernel(const float* __restrict__ raw, int64_t raw_stride, int H, int nf,
+                                        float* __restrict__ out, int64_t stride) {
+  pack_egcl_body(raw + blockIdx.y * raw_stride, H, nf, out + blockIdx.y * stride, 0, nullptr, ACT_SILU, 0.f, 0.f);
+}
+
 // Power-of-two scales of the F16X3 fragments (egcl_scales_block, flow_device.h), one workgroup per matrix.
 __global__ void __launch_bounds__(256) egcl_scale_kernel(const float* __restrict__ raw, int H, int nf,
                                                          float* __restrict__ out) {
   egcl_scales_block(raw, H, nf, out + egcl_layout(H, nf).scl);
+}
+__global__ void __launch_bounds__(256) egcl_scale_layers_kernel(const float* __restrict__ raw, int64_t raw_stride,
+                                                                int H, int nf, float* __restrict__ out,
+                                                                int64_t stride) {
+  egcl_scales_block(raw + blockIdx.y * raw_stride, H, nf, out + blockIdx.y * stride + egcl_layout(H, nf).scl);
 }
 
 __global__ void pack_argmax_kernel(const float* __restrict__ raw, int H, int nf, float* __restrict__ out) {
@@ -254,6 +272,32 @@ __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float
   }
   const float s = block_sum(sm, lq);
   if (tid == 0) lq_mol[blockIdx.x] = s;
+}
+
+// ArgMax.forward (argmax.py:13-25) of the batch ahead of the flow kernel
+// (round 6): one workgroup per molecule (or per listed molecule), the fused
+// kernels' argmax_dequant in its parallel form (every value bitwise the fused
+// dequantisation's), z [atoms][nf] and each molecule's log_q written out.  The
+// flow kernel then runs without a dequantiser on z and adds log_q to its
+// log|detJ| (FlowArgs::lq_mol).  Inside the fused kernel the dequantisation is
+// a latency chain at the start of every workgroup -- at the first round of
+// workgroups nothing else runs on the CUs -- and removing it saves ~4 % of the
+// bench forward (0.753 -> 0.721 ms, profiles/r06/r06f_*); here it runs once
+// for the whole batch, all molecules in parallel.
+template <int H, int NMAX>
+__global__ void __launch_bounds__(BLOCK) dequant_kernel(FlowArgs A, float* z, float* lq_mol) {
+  __shared__ Smem<H, NMAX, NMAX> sm;
+  MolRef M;
+  if (!load_molecule(sm, A, M, LOAD_H)) return;   // (the flow kernel flags the molecule too)
+  const int tid = threadIdx.x;
+  const int n = M.n, nf = A.nf;
+  const float lq = argmax_dequant<H, NMAX, NMAX, true, true>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+  for (int e = tid; e < n * nf; e += BLOCK) {
+    const int a = e / nf, q = e - a * nf;
+    z[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
+  }
+  const float s = block_sum(sm, lq);
+  if (tid == 0) lq_mol[M.m] = s;
 }
 
 // neighbour pairs only (rows re-labelled molecule-local when row-blocked)
@@ -472,6 +516,48 @@ static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs
 // The threshold is a per-library setting (libenflow_hip.so and _nf16.so each
 // hold one; enflow_amd._lib.set_latency_threshold sets every loaded library).
 static int g_lat_threshold = -1;
+// ArgMax dequantisation ahead of the flow kernel (dequant_kernel) for batches of
+// <= 64-atom molecules: per-(device, stream) z / log_q buffers, grown on demand
+// and never freed (queued launches may still read the old ones)
+static int g_dq_ahead = 1;
+struct DqBuf {
+  int dev;
+  hipStream_t st;
+  size_t cap_z, cap_m;
+  float* z;
+  float* lq;
+};
+static std::mutex g_dq_mu;
+static DqBuf g_dq[64];
+static int g_ndq = 0;
+static DqBuf* dq_buffers(hipStream_t st, size_t nz, size_t nm) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lk(g_dq_mu);
+  DqBuf* b = nullptr;
+  for (int i = 0; i < g_ndq; ++i)
+    if (g_dq[i].dev == dev && g_dq[i].st == st) b = &g_dq[i];
+  if (!b) {
+    if (g_ndq >= 64) return nullptr;
+    b = &g_dq[g_ndq++];
+    *b = DqBuf{dev, st, 0, 0, nullptr, nullptr};
+  }
+  if (b->cap_z < nz) {
+    float* p = nullptr;
+    const size_t c = nz < 65536 ? 65536 : nz;
+    if (hipMalloc(&p, c * sizeof(float)) != hipSuccess) return nullptr;
+    b->z = p;
+    b->cap_z = c;
+  }
+  if (b->cap_m < nm) {
+    float* p = nullptr;
+    const size_t c = nm < 4096 ? 4096 : nm;
+    if (hipMalloc(&p, c * sizeof(float)) != hipSuccess) return nullptr;
+    b->lq = p;
+    b->cap_m = c;
+  }
+  return b;
+}
 static int g_cus[64];   // CU count per device ordinal (0: not queried yet), cached off the launch path
 static int lat_threshold_now() {
   if (g_lat_threshold >= 0) return g_lat_threshold;
@@ -511,6 +597,11 @@ int enflow_read_stamps(unsigned long long* host_out, int reset) {
 #endif
 
 int enflow_abi_version(void) { return ENFLOW_ABI; }
+int enflow_set_dequant_ahead(int on) {
+  const int prev = g_dq_ahead;
+  g_dq_ahead = on ? 1 : 0;
+  return prev;
+}
 int enflow_set_latency_threshold(int max_mols) {
   const int prev = g_lat_threshold;
   g_lat_threshold = max_mols < 0 ? -1 : max_mols;
@@ -551,6 +642,19 @@ int enflow_pack_egcl_ex_f32(const float* raw, int H, int nf, int flags, const fl
 
 int enflow_pack_egcl_f32(const float* raw, int H, int nf, float* packed, void* stream) {
   return enflow_pack_egcl_ex_f32(raw, H, nf, 0, nullptr, packed, stream);
+}
+
+int enflow_pack_egcl_layers_f32(const float* raw, int64_t raw_stride, int n_layers, int H, int nf, float* packed,
+                                void* stream) {
+  if (!hid_ok(H) || nf < 1 || nf > NFMAX || !raw || !packed || n_layers < 0 || n_layers > 65535) return -1;
+  const EgclLayout L = egcl_layout(H, nf);
+  if (raw_stride < raw_egcl(H, nf).total) return -1;
+  if (n_layers == 0) return 0;
+  hipLaunchKernelGGL(egcl_scale_layers_kernel, dim3(6, n_layers), dim3(256), 0, S(stream), raw, raw_stride, H, nf,
+                     packed, (int64_t)L.total);
+  hipLaunchKernelGGL(pack_egcl_layers_kernel, dim3((L.total + 255) / 256, n_layers), dim3(256), 0, S(stream), raw,
+                     raw_stride, H, nf, packed, (int64_t)L.total);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 int enflow_pack_argmax_f32(const float* raw, int H, int nf, float* packed, void* stream) {
@@ -604,6 +708,19 @@ int enflow_lf_forward_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, in
   A.mol_err = mol_err;
   A.mol_list = mol_list;
   const int grid = mol_list != nullptr ? num_listed : num_mols;
+  if (grid > 0 && g_dq_ahead && dequant_kind == ENFLOW_DEQUANT_ARGMAX && max_mol_atoms <= 64) {
+    // the ArgMax dequantisation ahead of the flow (dequant_kernel, same values)
+    DqBuf* Z = dq_buffers(S(stream), (size_t)(num_atoms > 0 ? num_atoms : 1) * nf, (size_t)num_mols);
+    if (Z == nullptr) return -2;
+    const FlowArgs D = A;
+#define DQ(HH, NN) ENFLOW_TIMED("dequant_kernel", S(stream), hipLaunchKernelGGL((dequant_kernel<HH, NN>), dim3(grid), dim3(BLOCK), 0, S(stream), D, Z->z, Z->lq))
+    if (max_mol_atoms <= 32) { if (H == 32) DQ(32, 32); else if (H == 64) DQ(64, 32); else DQ(128, 32); }
+    else { if (H == 32) DQ(32, 64); else if (H == 64) DQ(64, 64); else DQ(128, 64); }
+#undef DQ
+    A.h_in = Z->z;
+    A.dequant_kind = ENFLOW_DEQUANT_NONE;
+    A.lq_mol = Z->lq;
+  }
   if (grid > 0) {
 #define CALL(HH, NN, RBB) launch_flow<HH, NN, RBB, false>(gemm_precision, grid, S(stream), A)
     DISPATCH_HN(H, max_mol_atoms, CALL);

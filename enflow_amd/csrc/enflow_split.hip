@@ -678,6 +678,7 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
 
     STAMP(0);
     if (!REV) {
+      if (A.lq_mol != nullptr && half == 0 && tid == 0) ldj += A.lq_mol[m];   // dequantised ahead (dequant_kernel)
       if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
         // every atom in both halves (the same draws); half 0 counts log_q
         const float lq = argmax_dequant<H, NMX, NMX, false, true>(sm, A.dequant, A.noise_src(), M.a0, n, nf);

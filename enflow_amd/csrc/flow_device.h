@@ -2340,6 +2340,9 @@ struct NoiseSrc {
 template <int H, int NMAX, int RB, bool VAR = false, bool PAR = false>
 __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const NoiseSrc noise,
                                 int a0, int n, int nf) {
+#ifdef ENFLOW_ABLATE_DEQUANT
+  return 0.f;   // timing ablation (tools, never the product: build.py refuses it): h passes through
+#endif
   using S = Smem<H, NMAX, RB>;
   constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
   // hidden activations staged in agg (free before layer 0); 16-B aligned rows
@@ -2363,10 +2366,19 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
     {
       const int k = tid % H, grp = tid / H;
       if (grp < NG) {
+        // network.0's column k in registers, requested once: inside the atom loop
+        // the loads (a runtime-length inner loop) were issued per atom, each
+        // iteration waiting on an L2 round trip (~9 k cycles of a ~30 k-cycle
+        // dequantisation, profiles/r06/r06h_*); the same fma sequence (q ascending)
         const float b = Dp[L.ba1 + k];
+        float w1[NFMAX];
+#pragma unroll
+        for (int q = 0; q < NFMAX; ++q) w1[q] = q < nf ? Dp[L.wa1t + q * H + k] : 0.f;
         for (int a = grp; a < cn; a += NG) {
           float v = b;
-          for (int q = 0; q < nf; ++q) v += Dp[L.wa1t + q * H + k] * sm.h[(c0 + a) * NFP + q];
+#pragma unroll
+          for (int q = 0; q < NFMAX; ++q)
+            if (q < nf) v += w1[q] * sm.h[(c0 + a) * NFP + q];
           act[a * ACT + k] = act_v<VAR>(aact, v);
         }
       }
@@ -2506,6 +2518,10 @@ struct FlowArgs {
   // caller zeroes them), and a molecule list (block b runs molecule mol_list[b])
   int32_t* mol_err = nullptr;
   const int32_t* mol_list = nullptr;
+  // round 6: the ArgMax dequantisation ran ahead of the flow kernel
+  // (dequant_kernel): the flow gets dequant_kind NONE, h_in = z, and adds each
+  // molecule's log_q from here to its log|detJ|
+  const float* lq_mol = nullptr;
   __device__ __forceinline__ NoiseSrc noise_src() const { return NoiseSrc{noise, seed, offset}; }
 };
 

@@ -82,6 +82,7 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   };
 
   if (!REV) {
+    if (A.lq_mol != nullptr && tid == 0) ldj += A.lq_mol[M.m];   // dequantised ahead (dequant_kernel)
     if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
       ldj += argmax_dequant<H, NMAX, RB, VAR>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
     } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {

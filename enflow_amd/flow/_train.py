@@ -55,18 +55,20 @@ class _FlowFunction(torch.autograd.Function):
                 import warnings
                 warnings.warn("enflow_amd: gemm_precision='bf16' is a generate-path setting; the training "
                               "forward runs f16x3", RuntimeWarning, stacklevel=2)
+        # both packed sections of every layer first (training_layers: after an
+        # optimiser step, two launches per section for the whole flow, ABI 13), so
+        # the forward launch reuses the forward section (packed_layers' cache); the
+        # buffers and the parameter versions they were packed from go with this
+        # graph: the backward uses exactly these and refuses in-place changes since
+        ctx.train_bufs = flow.training_layers(dev)
+        ctx.train_key = flow._params_key(dev)
         flow.forward_buffers(hw, gw, pw, vw, meta["box"], meta["r_cut"], meta["mol_ptr"], meta["max_n"],
                              meta["noise"], ldj_mol, ldj, err, tape=tape, pair_counts=counts, prec=prec,
                              src=src, ticket=st[1:])
         # an fp32-GEMM forward's tape gets the fp32-GEMM backward (ENFLOW_BWD_F32)
         ctx.bwd_f32 = (prec & 0xff) == _lib.PREC_F32
-        # queue the backward's weight packing (cached on the parameters' versions,
-        # which cannot change before this graph's backward) and the dequantiser's
-        # flat parameters behind the forward kernel, ahead of the error check's sync
-        # the buffers and the parameter versions they were packed from go with this
-        # graph: the backward uses exactly these and refuses in-place changes since
-        ctx.train_bufs = flow.training_layers(dev)
-        ctx.train_key = flow._params_key(dev)
+        # the dequantiser's flat parameters behind the forward kernel, ahead of the
+        # error check's sync
         ctx.dq_raw = None
         if kind == _lib.DEQUANT_ARGMAX:
             ctx.dq_raw = flow.dequantize.kernel_raw(dev, hid)

@@ -130,12 +130,26 @@ class LFIntegrator(BaseFlow):
             pieces.append(n._att_raw(device) if n.attention else zpad)
         raw = torch.cat(pieces)
         stride = L.enflow_egcl_bwd_packed_size(hid, nf)
-        rstride = raw.numel() // max(len(self.networks), 1)
-        bwd = torch.empty(max(stride * len(self.networks), 1), dtype=torch.float32, device=device)
-        for i in range(len(self.networks)):
-            _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw[i * rstride:]), hid, nf,
-                                                  _lib.ptr(bwd[i * stride:]), _lib.stream_ptr(device)),
-                       "enflow_pack_egcl_bwd_f32")
+        n_l = len(self.networks)
+        rstride = raw.numel() // max(n_l, 1)
+        bwd = torch.empty(max(stride * n_l, 1), dtype=torch.float32, device=device)
+        st = _lib.stream_ptr(device)
+        if n_l and hasattr(L, "enflow_pack_egcl_layers_f32") and not any(n.variant_flags() for n in self.networks):
+            # default-flag SiLU layers (the training loop's repack after every
+            # optimiser step): both sections of every layer in two launches each
+            # (ABI 13) instead of two per layer and section; the forward section is
+            # packed_layers' buffer, from the same raw parameters
+            fstride = L.enflow_egcl_packed_size(hid, nf)
+            fwd = torch.empty(max(fstride * n_l, 1), dtype=torch.float32, device=device)
+            _lib.check(L.enflow_pack_egcl_layers_f32(_lib.ptr(raw), rstride, n_l, hid, nf, _lib.ptr(fwd), st),
+                       "enflow_pack_egcl_layers_f32")
+            _lib.check(L.enflow_pack_egcl_bwd_layers_f32(_lib.ptr(raw), rstride, n_l, hid, nf, _lib.ptr(bwd), st),
+                       "enflow_pack_egcl_bwd_layers_f32")
+            self._layers_buf, self._layers_key = fwd, key
+        else:
+            for i in range(n_l):
+                _lib.check(L.enflow_pack_egcl_bwd_f32(_lib.ptr(raw[i * rstride:]), hid, nf,
+                                                      _lib.ptr(bwd[i * stride:]), st), "enflow_pack_egcl_bwd_f32")
         self._train_bufs = (self.packed_layers(device), bwd, raw)
         self._train_key = key
         return self._train_bufs

@@ -77,7 +77,9 @@ extern "C" {
  * forward); 12: ENFLOW_ERR_SMALL split from ENFLOW_ERR_RANGE, ENFLOW_ERR_HANDOFF, the feature-split
  * latency instance (enflow_set_split_threshold / enflow_set_fs_threshold), per-molecule error words
  * and molecule lists (enflow_lf_forward_io2_f32 / enflow_lf_reverse_io2_f32); 13: ENFLOW_PREC_NO_SPLIT,
- * enflow_set_handoff_spin_limit, the two-workgroup split only for out-of-place launches). */
+ * enflow_set_handoff_spin_limit, the two-workgroup split only for out-of-place launches, the ArgMax
+ * dequantisation ahead of the flow kernel, enflow_set_dequant_ahead, enflow_pack_egcl_layers_f32 /
+ * enflow_pack_egcl_bwd_layers_f32). */
 int enflow_abi_version(void);
 
 /* Batches of <= 32-atom molecules with at most this many molecules run the
@@ -116,6 +118,13 @@ int enflow_set_fs_threshold(int max_mols);
  * ENFLOW_ERR_HANDOFF path, for testing the host's re-run.  Per library;
  * returns the previous setting. */
 int enflow_set_handoff_spin_limit(int polls);
+/* ABI 13: the ArgMax dequantisation (argmax.py:13-25) of forward io / io2
+ * launches on batches of <= 64-atom molecules runs as its own kernel ahead of
+ * the flow kernel (one workgroup per molecule, all molecules in parallel; the
+ * same draws and values as the fused form, log|detJ| within round-off of
+ * it).  1 (default) on, 0 the dequantisation fused into the flow kernel.  Per
+ * library; returns the previous setting. */
+int enflow_set_dequant_ahead(int on);
 
 /* Largest molecule (atoms) / node_nf the compiled kernels accept.  The ABI
  * ships as two builds of the same sources: libenflow_hip.so (node_nf <= 8) and
@@ -453,6 +462,16 @@ int64_t enflow_lf_tape_size_for(int num_atoms, int node_nf, int hidden_nf, int n
  * raw concatenation as enflow_pack_egcl_f32). */
 int64_t enflow_egcl_bwd_packed_size(int hidden_nf, int node_nf);
 int enflow_pack_egcl_bwd_f32(const float* raw, int hidden_nf, int node_nf, float* packed, void* stream);
+/* ABI 13: every layer of a flow at once (default-flag SiLU layers): layer l's
+ * raw concatenation at raw + l * raw_stride, written to packed + l *
+ * enflow_egcl_packed_size (forward section) / enflow_egcl_bwd_packed_size
+ * (backward section).  Two launches per section for the whole flow instead of
+ * two per layer -- the repack after every optimiser step (enflow/main.py:
+ * 217-223). */
+int enflow_pack_egcl_layers_f32(const float* raw, int64_t raw_stride, int n_layers, int hidden_nf, int node_nf,
+                                float* packed, void* stream);
+int enflow_pack_egcl_bwd_layers_f32(const float* raw, int64_t raw_stride, int n_layers, int hidden_nf, int node_nf,
+                                    float* packed, void* stream);
 
 /* Bytes of scratch enflow_lf_backward_f32 needs.  pair_row_bound >= the sum
  * over molecules of n_m (n_m - 1) rounded up to a multiple of 32. */

@@ -1,0 +1,112 @@
+"""The ArgMax dequantisation ahead of the flow kernel (ABI 13, dequant_kernel):
+the same draws and values as the dequantisation fused into the flow kernel
+(enflow_set_dequant_ahead(0)) -- outputs bitwise equal, log|detJ| within
+round-off (its sum order differs), training gradients bitwise equal -- on
+every fused instance, with the caller's noise and with in-kernel draws, and
+against the float64 oracle.  Reference: enflow/nn/argmax.py:13-25,
+enflow/flow/dynamics.py:10-24."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import enflow_oracle as O
+from _fixtures import rel_err, worst_of, assert_all_within
+
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("kernel_instance")]
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _f32(b):
+    out = dict(b)
+    for k in ("h", "g", "pos", "vel", "box", "r_cut"):
+        out[k] = b[k].astype(np.float32).astype(np.float64)
+    return out
+
+
+def _model(hid, n_layers, seed):
+    from enflow_amd.nn import EGCL, ArgMax
+    from enflow_amd.flow import LFIntegrator
+    from enflow_amd.data.synthetic import default_dt
+    torch.manual_seed(seed)
+    return LFIntegrator([EGCL(5, 5, hid) for _ in range(n_layers)], ArgMax(5, hid), dt=default_dt()).to(DEV)
+
+
+def _run(model, d, eps, ahead, key_seed):
+    from enflow_amd import _lib
+    prev = _lib.set_dequant_ahead(ahead)
+    try:
+        torch.manual_seed(key_seed)          # the same in-kernel noise key when eps is None
+        with _lib.KernelTimer() as t, torch.no_grad():
+            o, ldj = model(d.clone(), noise=eps)
+    finally:
+        _lib.set_dequant_ahead(True if prev is None else bool(prev))
+    return o, ldj, set(t.stats)
+
+
+@pytest.mark.parametrize("mols,atoms,hid", [(1024, 22, 128), (48, 60, 64)])
+@pytest.mark.parametrize("draws", ["caller", "kernel"])
+def test_dequant_ahead_equals_fused(mols, atoms, hid, draws, kernel_instance):
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules
+    b = _f32(make_molecules(mols, atoms, nf=5, seed=90 + atoms))
+    model = _model(hid, 3, 91)
+    d = Data.from_arrays(b, device=DEV)
+    eps = (torch.randn(d.h.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(92))
+           if draws == "caller" else None)
+    o1, l1, k1 = _run(model, d, eps, True, 93)
+    o0, l0, k0 = _run(model, d, eps, False, 93)
+    assert "dequant_kernel" in k1 and "dequant_kernel" not in k0, (k1, k0)
+    for k in ("h", "g", "pos", "vel"):
+        assert torch.equal(getattr(o1, k), getattr(o0, k)), k
+    ldj_d = abs(float(l1) - float(l0)) / abs(float(l0))
+    print(f"[{kernel_instance}] dequant ahead vs fused, {mols} x {atoms} H {hid}, {draws} draws: outputs bitwise "
+          f"equal, ldj {ldj_d:.2e}")
+    assert ldj_d < 1e-6
+    if draws == "caller":   # and the oracle on sampled molecules
+        layers = [{k: v.detach().cpu().double().numpy() for k, v in n.state_dict().items()} for n in model.networks]
+        dq = {k: v.detach().cpu().double().numpy() for k, v in model.dequantize.state_dict().items()}
+        worst = {k: 0.0 for k in ("h", "g", "pos", "vel")}
+        for m in sorted(set(list(range(0, mols, max(mols // 8, 1))) + [mols - 1])):
+            a0, a1 = int(b["mol_ptr"][m]), int(b["mol_ptr"][m + 1])
+            sub = {k: b[k][a0:a1] for k in ("h", "g", "pos", "vel", "box")}
+            sub.update(r_cut=b["r_cut"][m:m + 1], mol_ptr=np.array([0, a1 - a0]))
+            ref, _ = O.lf_forward(layers, dq, sub, eps[a0:a1].cpu().double().numpy(), model.dt)
+            for k in worst:
+                worst[k] = worst_of([worst[k], rel_err(getattr(o1, k)[a0:a1].cpu().numpy(), ref[k])])
+        _, ref_ldj = O.lf_forward(layers, dq, b, eps.cpu().double().numpy(), model.dt)
+        worst["ldj"] = abs(float(l1) - ref_ldj) / abs(ref_ldj)
+        assert_all_within(worst, 1e-5, "dequant ahead vs oracle")
+
+
+def test_dequant_ahead_training_gradients_bitwise():
+    """A training step (64-atom instance, the tape) with the dequantisation ahead
+    and fused: loss and every gradient bitwise equal."""
+    from enflow_amd import _lib
+    from enflow_amd.data import Data
+    from enflow_amd.flow import Alchemical_NLL
+    from enflow_amd.data.synthetic import make_molecules, default_kBT
+    b = _f32(make_molecules(6, 40, nf=5, seed=95))
+    eps = torch.randn((b["h"].shape[0], 5), device=DEV, generator=torch.Generator(DEV).manual_seed(96))
+    grads, losses = [], []
+    for ahead in (True, False):
+        model = _model(64, 2, 97)
+        prev = _lib.set_dequant_ahead(ahead)
+        try:
+            out, ldj = model(Data.from_arrays(b, device=DEV), noise=eps)
+            loss = Alchemical_NLL(kBT=default_kBT(), softening=0.1)(out, ldj)
+            loss.backward()
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_dequant_ahead(True if prev is None else bool(prev))
+        losses.append(float(loss.detach()))
+        grads.append([p.grad.clone() for p in model.parameters()])
+    same = all(torch.equal(a, c) for a, c in zip(*grads))
+    print(f"training step, dequant ahead vs fused: loss {losses[0]:.9e} vs {losses[1]:.9e}, gradients bitwise {same}")
+    assert same
+    assert abs(losses[0] - losses[1]) <= 1e-6 * abs(losses[1])

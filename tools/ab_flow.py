@@ -38,8 +38,11 @@ def main():
     times = {(lib, m): [] for lib in libs for m in sizes}
     outs = {}
 
-    def use(path):
+    def use(spec):
+        # "path" or "path:noahead" (the same library with enflow_set_dequant_ahead(0))
+        path, _, opt = spec.partition(":")
         _lib._libs.clear()
+        _lib._dq_ahead[0] = 0 if opt == "noahead" else None
         _lib.LIB_PATH = path
         model._layers_key = None
         model._train_key = None
