@@ -284,20 +284,43 @@ __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float
 // workgroups nothing else runs on the CUs -- and removing it saves ~4 % of the
 // bench forward (0.753 -> 0.721 ms, profiles/r06/r06f_*); here it runs once
 // for the whole batch, all molecules in parallel.
+#ifdef ENFLOW_STAMPS
+// dequant_kernel phases (thread 0's wave): 0 load + network.2 staging, 1 hidden
+// layer, 2 barriers, 3 network outputs, 4 draws + u, 5 z + log_q, 6 copy-back + store
+__device__ unsigned long long enflow_dq_stamp_acc[8];
+#endif
 template <int H, int NMAX>
 __global__ void __launch_bounds__(BLOCK) dequant_kernel(FlowArgs A, float* z, float* lq_mol) {
-  __shared__ Smem<H, NMAX, NMAX> sm;
-  MolRef M;
-  if (!load_molecule(sm, A, M, LOAD_H)) return;   // (the flow kernel flags the molecule too)
+  constexpr int RB = 32;
+  __shared__ DqSmem<H, NMAX, RB> sm;
+  const int m = A.mol_list ? A.mol_list[blockIdx.x] : (int)blockIdx.x;
   const int tid = threadIdx.x;
-  const int n = M.n, nf = A.nf;
-  const float lq = argmax_dequant<H, NMAX, NMAX, true, true>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+  const int a0 = A.mol_ptr[m], n = A.mol_ptr[m + 1] - a0, nf = A.nf;
+  if (n > NMAX || nf > NFMAX) return;   // the flow kernel flags the molecule
+  const float* const hin = A.h_in ? A.h_in : A.h;
+  for (int e = tid; e < n * NFP; e += BLOCK) {   // rows zero-padded past nf
+    const int a = e / NFP, q = e - a * NFP;
+    sm.h[e] = q < nf ? hin[(size_t)(a0 + a) * nf + q] : 0.f;
+  }
+#ifdef ENFLOW_STAMPS
+  unsigned long long dqst[8] = {0, 0, 0, 0, 0, 0, 0, __builtin_amdgcn_s_memtime()};
+#else
+  unsigned long long* const dqst = nullptr;
+#endif
+  __syncthreads();
+  DQS(0);
+  const float lq = argmax_dequant<H, NMAX, RB, true, true>(sm, A.dequant, A.noise_src(), a0, n, nf, dqst);
   for (int e = tid; e < n * nf; e += BLOCK) {
     const int a = e / nf, q = e - a * nf;
-    z[(size_t)M.a0 * nf + e] = sm.h[a * NFP + q];
+    z[(size_t)a0 * nf + e] = sm.h[a * NFP + q];
   }
   const float s = block_sum(sm, lq);
-  if (tid == 0) lq_mol[M.m] = s;
+  if (tid == 0) lq_mol[m] = s;
+#ifdef ENFLOW_STAMPS
+  DQS(6);
+  if (tid == 0)
+    for (int k = 0; k < 7; ++k) atomicAdd(&enflow_dq_stamp_acc[k], dqst[k]);
+#endif
 }
 
 // neighbour pairs only (rows re-labelled molecule-local when row-blocked)
@@ -593,6 +616,18 @@ int enflow_read_stamps(unsigned long long* host_out, int reset) {
     if (hipMemcpyToSymbol(HIP_SYMBOL(enflow_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
   }
   return NSTAMP;
+}
+#endif
+
+#ifdef ENFLOW_STAMPS
+int enflow_read_dq_stamps(unsigned long long* host_out, int reset) {
+  if (hipMemcpyFromSymbol(host_out, HIP_SYMBOL(enflow_dq_stamp_acc), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -2;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(enflow_dq_stamp_acc), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return 8;
 }
 #endif
 

@@ -2297,6 +2297,22 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
   node_partials_reduce(sm, Lp, L, nf, tid, r0, rb);
 }
 
+// dequant_kernel's LDS image (round 6): only what argmax_dequant touches -- the
+// molecule's h rows, network.2.weight, the activation rows of a chunk of RB
+// atoms, the chunk's network outputs -- ~29 KB at H = 128 (the flow image is
+// ~65 KB): five workgroups per CU, the bench batch's 1024 molecules in one
+// round instead of two
+template <int H, int NMAX, int RB>
+struct DqSmem {
+  static constexpr int AST = H + 4;
+  static constexpr bool W1X_LDS = true;
+  float h[NMAX * NFP];
+  alignas(16) float w1x[2 * NFMAX * H];
+  alignas(16) float agg[RB * AST];
+  struct { float net[RB * 2 * NFMAX]; } u;
+  float red[WAVES];
+};
+
 // The dequantiser's draws made in the kernel (noise == NULL): Philox4x32-10
 // (Salmon et al., SC'11) keyed by the caller's 64-bit seed, counter = (element
 // index, 0, 64-bit offset); N(0,1) by Box-Muller (argmax.py:16's torch.randn),
@@ -2337,13 +2353,26 @@ struct NoiseSrc {
 // eight waves, one molecule); else one atom per thread, its elements in turn
 // (the whole-tile instances: the parallel form measured no faster there and
 // moved register spills into the layer loop, profiles/r05/r05w_*, r05z2 PMC)
-template <int H, int NMAX, int RB, bool VAR = false, bool PAR = false>
-__device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const float* __restrict__ Dp, const NoiseSrc noise,
-                                int a0, int n, int nf) {
+// S: the flow kernels' Smem image, or DqSmem (dequant_kernel's own image)
+// dqst (diagnostic stamps builds, dequant_kernel only): per-phase cycles, [7] the last stamp
+#ifdef ENFLOW_STAMPS
+#define DQS(k)                                              \
+  do {                                                      \
+    if (dqst) {                                             \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+      dqst[k] += now_ - dqst[7];                            \
+      dqst[7] = now_;                                       \
+    }                                                       \
+  } while (0)
+#else
+#define DQS(k) do {} while (0)
+#endif
+template <int H, int NMAX, int RB, bool VAR = false, bool PAR = false, class S>
+__device__ __forceinline__ float argmax_dequant(S& sm, const float* __restrict__ Dp, const NoiseSrc noise,
+                                int a0, int n, int nf, unsigned long long* dqst = nullptr) {
 #ifdef ENFLOW_ABLATE_DEQUANT
   return 0.f;   // timing ablation (tools, never the product: build.py refuses it): h passes through
 #endif
-  using S = Smem<H, NMAX, RB>;
   constexpr int NG = BLOCK / H > 0 ? BLOCK / H : 1;
   // hidden activations staged in agg (free before layer 0); 16-B aligned rows
   constexpr int ACT = S::AST % 4 == 0 ? S::AST : H + 1;
@@ -2361,6 +2390,7 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
   if constexpr (WLDS) {
     for (int e = tid; e < 2 * nf * H / 4; e += BLOCK) st4(&sm.w1x[4 * e], ld4(Dp + L.wa2 + 4 * e));
   }
+  DQS(0);
   for (int c0 = 0; c0 < n; c0 += RB) {   // atoms in chunks of RB (the agg image)
     const int cn = min(RB, n - c0);
     {
@@ -2383,7 +2413,9 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
         }
       }
     }
+    DQS(1);
     __syncthreads();
+    DQS(2);
     // net[a][o], o < 2 nf
     for (int e = tid; e < cn * 2 * nf; e += BLOCK) {
       const int a = e / (2 * nf), o = e - a * 2 * nf;
@@ -2402,7 +2434,9 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
       }
       net[a * 2 * NFMAX + o] = s;          // chunk-local rows
     }
+    DQS(3);
     __syncthreads();
+    DQS(2);
     if constexpr (!PAR) {
       for (int a = tid; a < cn; a += BLOCK) {   // z of the chunk's atoms (each atom's own h only)
         const int ag = c0 + a;
@@ -2444,7 +2478,9 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
         us[a * NFMAX + q] = u;
         lq += -0.5f * u * u - ls;
       }
+      DQS(4);
       __syncthreads();
+      DQS(2);
       for (int e = tid; e < cn * nf; e += BLOCK) {
         const int a = e / nf, q = e - a * nf, ag = c0 + a;
         float T = 0.f;
@@ -2453,20 +2489,22 @@ __device__ __forceinline__ float argmax_dequant(Smem<H, NMAX, RB>& sm, const flo
         zs[a * NFMAX + q] = hv * u + (1.f - hv) * (T - softplus_f(T - u));
         lq -= (1.f - hv) * logsigmoid_f(T - u);
       }
+      DQS(5);
       __syncthreads();
       for (int e = tid; e < cn * nf; e += BLOCK) {
         const int a = e / nf, q = e - a * nf;
         sm.h[(c0 + a) * NFP + q] = zs[a * NFMAX + q];
       }
       __syncthreads();
+      DQS(6);
     }
   }
   return lq;
 }
 
 // deterministic block sum (thread values -> one float, fixed order)
-template <int H, int NMAX, int RB>
-__device__ __forceinline__ float block_sum(Smem<H, NMAX, RB>& sm, float v) {
+template <class S>
+__device__ __forceinline__ float block_sum(S& sm, float v) {
   v = wave_sum(v);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   __syncthreads();
