@@ -289,7 +289,7 @@ __global__ void __launch_bounds__(BLOCK) argmax_forward_kernel(FlowArgs A, float
 // layer, 2 barriers, 3 network outputs, 4 draws + u, 5 z + log_q, 6 copy-back + store
 __device__ unsigned long long enflow_dq_stamp_acc[8];
 #endif
-template <int H, int NMAX>
+template <int H, int NMAX, bool VAR>
 __global__ void __launch_bounds__(BLOCK) dequant_kernel(FlowArgs A, float* z, float* lq_mol) {
   constexpr int RB = 32;
   __shared__ DqSmem<H, NMAX, RB> sm;
@@ -309,7 +309,8 @@ __global__ void __launch_bounds__(BLOCK) dequant_kernel(FlowArgs A, float* z, fl
 #endif
   __syncthreads();
   DQS(0);
-  const float lq = argmax_dequant<H, NMAX, RB, true, true>(sm, A.dequant, A.noise_src(), a0, n, nf, dqst);
+  // VAR as the fused kernels take it (a non-SiLU network.1 comes with ENFLOW_EGCL_VARIANTS)
+  const float lq = argmax_dequant<H, NMAX, RB, VAR, true>(sm, A.dequant, A.noise_src(), a0, n, nf, dqst);
   for (int e = tid; e < n * nf; e += BLOCK) {
     const int a = e / nf, q = e - a * nf;
     z[(size_t)a0 * nf + e] = sm.h[a * NFP + q];
@@ -582,8 +583,7 @@ static DqBuf* dq_buffers(hipStream_t st, size_t nz, size_t nm) {
   return b;
 }
 static int g_cus[64];   // CU count per device ordinal (0: not queried yet), cached off the launch path
-static int lat_threshold_now() {
-  if (g_lat_threshold >= 0) return g_lat_threshold;
+static int cus_now() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (dev < 0 || dev >= 64) return 0;
@@ -594,6 +594,7 @@ static int lat_threshold_now() {
   }
   return g_cus[dev];
 }
+static int lat_threshold_now() { return g_lat_threshold >= 0 ? g_lat_threshold : cus_now(); }
 
 template <int HH, int NN, int RBB, bool REV>
 static void launch_flow(int prec, int num_mols, hipStream_t st, const FlowArgs& A) {
@@ -743,12 +744,23 @@ int enflow_lf_forward_io2_f32(int num_mols, int num_atoms, int max_mol_atoms, in
   A.mol_err = mol_err;
   A.mol_list = mol_list;
   const int grid = mol_list != nullptr ? num_listed : num_mols;
-  if (grid > 0 && g_dq_ahead && dequant_kind == ENFLOW_DEQUANT_ARGMAX && max_mol_atoms <= 64) {
-    // the ArgMax dequantisation ahead of the flow (dequant_kernel, same values)
+  if (grid > cus_now() && g_dq_ahead && dequant_kind == ENFLOW_DEQUANT_ARGMAX && max_mol_atoms <= 64) {
+    // the ArgMax dequantisation ahead of the flow (dequant_kernel, same values),
+    // for batches of more molecules than CUs: there the fused form is a latency
+    // chain at the start of every workgroup; at most one workgroup per CU (the
+    // latency / split instances) it is one chain either way, and fused saves a
+    // launch (128 molecules: 0.1751 vs 0.1809 ms, profiles/r06/r06l_*)
     DqBuf* Z = dq_buffers(S(stream), (size_t)(num_atoms > 0 ? num_atoms : 1) * nf, (size_t)num_mols);
     if (Z == nullptr) return -2;
     const FlowArgs D = A;
-#define DQ(HH, NN) ENFLOW_TIMED("dequant_kernel", S(stream), hipLaunchKernelGGL((dequant_kernel<HH, NN>), dim3(grid), dim3(BLOCK), 0, S(stream), D, Z->z, Z->lq))
+    const bool dvar = (gemm_precision & ENFLOW_EGCL_VARIANTS) != 0;
+#define DQ(HH, NN)                                                                                                   \
+  do {                                                                                                               \
+    if (dvar) ENFLOW_TIMED("dequant_kernel", S(stream), hipLaunchKernelGGL((dequant_kernel<HH, NN, true>), dim3(grid), \
+                                                                           dim3(BLOCK), 0, S(stream), D, Z->z, Z->lq)); \
+    else ENFLOW_TIMED("dequant_kernel", S(stream), hipLaunchKernelGGL((dequant_kernel<HH, NN, false>), dim3(grid),     \
+                                                                      dim3(BLOCK), 0, S(stream), D, Z->z, Z->lq));     \
+  } while (0)
     if (max_mol_atoms <= 32) { if (H == 32) DQ(32, 32); else if (H == 64) DQ(64, 32); else DQ(128, 32); }
     else { if (H == 32) DQ(32, 64); else if (H == 64) DQ(64, 64); else DQ(128, 64); }
 #undef DQ

@@ -2301,13 +2301,15 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
 // molecule's h rows, network.2.weight, the activation rows of a chunk of RB
 // atoms, the chunk's network outputs -- ~29 KB at H = 128 (the flow image is
 // ~65 KB): five workgroups per CU, the bench batch's 1024 molecules in one
-// round instead of two
+// round instead of two.  network.2.weight is staged in LDS exactly when the
+// fused image stages it (<= 32 atoms): the output sums then run in the fused
+// form's order, so both forms give bitwise the same z
 template <int H, int NMAX, int RB>
 struct DqSmem {
   static constexpr int AST = H + 4;
-  static constexpr bool W1X_LDS = true;
+  static constexpr bool W1X_LDS = NMAX <= 32;
   float h[NMAX * NFP];
-  alignas(16) float w1x[2 * NFMAX * H];
+  alignas(16) float w1x[W1X_LDS ? 2 * NFMAX * (H + 4) : 4];
   alignas(16) float agg[RB * AST];
   struct { float net[RB * 2 * NFMAX]; } u;
   float red[WAVES];
@@ -2385,10 +2387,17 @@ __device__ __forceinline__ float argmax_dequant(S& sm, const float* __restrict__
   float lq = 0.f;
   const Act aact = VAR ? act_of(Dp + L.act) : act_silu();   // network.1 (argmax.py:7)
   // network.2.weight staged in the (still unused) edge_nn.0 fragment buffer: the
-  // output loop then reads both operands as float4 from LDS
-  constexpr bool WLDS = S::W1X_LDS && ACT % 4 == 0 && sizeof(sm.w1x) >= sizeof(float) * 2 * NFMAX * H;
+  // output loop then reads both operands as float4 from LDS.  Rows padded to
+  // WST = H + 4 floats: the output rows o a wave reads at once then start 4
+  // banks apart (stride H put all of them on one bank group: a 10-way conflict
+  // per ds_read_b128, ~8 k cycles of the dequantisation, profiles/r06/r06l_dq_stamps)
+  constexpr int WST = H + 4;
+  constexpr bool WLDS = S::W1X_LDS && ACT % 4 == 0 && sizeof(sm.w1x) >= sizeof(float) * 2 * NFMAX * WST;
   if constexpr (WLDS) {
-    for (int e = tid; e < 2 * nf * H / 4; e += BLOCK) st4(&sm.w1x[4 * e], ld4(Dp + L.wa2 + 4 * e));
+    for (int e = tid; e < 2 * nf * H / 4; e += BLOCK) {
+      const int o = 4 * e / H, k = 4 * e - o * H;
+      st4(&sm.w1x[o * WST + k], ld4(Dp + L.wa2 + 4 * e));
+    }
   }
   DQS(0);
   for (int c0 = 0; c0 < n; c0 += RB) {   // atoms in chunks of RB (the agg image)
@@ -2404,12 +2413,22 @@ __device__ __forceinline__ float argmax_dequant(S& sm, const float* __restrict__
         float w1[NFMAX];
 #pragma unroll
         for (int q = 0; q < NFMAX; ++q) w1[q] = q < nf ? Dp[L.wa1t + q * H + k] : 0.f;
-        for (int a = grp; a < cn; a += NG) {
-          float v = b;
+        // four atoms per step, their h rows read before any activation is stored
+        // (one LDS round trip per four atoms; the same fma sequence per atom)
+        constexpr int AU = 4;
+        for (int a = grp; a < cn; a += AU * NG) {
+          float v[AU];
 #pragma unroll
-          for (int q = 0; q < NFMAX; ++q)
-            if (q < nf) v += w1[q] * sm.h[(c0 + a) * NFP + q];
-          act[a * ACT + k] = act_v<VAR>(aact, v);
+          for (int j = 0; j < AU; ++j) {
+            const int aj = min(a + j * NG, cn - 1);
+            v[j] = b;
+#pragma unroll
+            for (int q = 0; q < NFMAX; ++q)
+              if (q < nf) v[j] += w1[q] * sm.h[(c0 + aj) * NFP + q];
+          }
+#pragma unroll
+          for (int j = 0; j < AU; ++j)
+            if (a + j * NG < cn) act[(a + j * NG) * ACT + k] = act_v<VAR>(aact, v[j]);
         }
       }
     }
@@ -2424,7 +2443,7 @@ __device__ __forceinline__ float argmax_dequant(S& sm, const float* __restrict__
         f32x4 acc4 = (f32x4)0.f;
 #pragma unroll 8
         for (int k = 0; k < H; k += 4) {
-          const f32x4 w4 = ld4(&sm.w1x[o * H + k]), x4 = ld4(&act[a * ACT + k]);
+          const f32x4 w4 = ld4(&sm.w1x[o * WST + k]), x4 = ld4(&act[a * ACT + k]);
           acc4 += w4 * x4;
         }
         s += (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);

@@ -82,10 +82,12 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   };
 
   if (!REV) {
-    if (A.lq_mol != nullptr && tid == 0) ldj += A.lq_mol[M.m];   // dequantised ahead (dequant_kernel)
+#ifndef ENFLOW_NO_FUSED_ARGMAX
     if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
       ldj += argmax_dequant<H, NMAX, RB, VAR>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
-    } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+    } else
+#endif
+    if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
       for (int e = tid; e < n * nf; e += BLOCK) {
         const int a = e / nf, q = e - a * nf;
         sm.h[a * NFP + q] += A.dequant_scale * A.noise_src().uniform((size_t)M.a0 * nf + e);
@@ -278,7 +280,11 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   }
   bad = false;
   if (!REV) {
-    const float s = block_sum(sm, ldj);   // (its barriers also order the err bits above)
+    float s = block_sum(sm, ldj);   // (its barriers also order the err bits above)
+    // dequantised ahead (dequant_kernel): its log_q, read here rather than at
+    // the start (the read there cost the layer loop ~3 % in register allocation,
+    // profiles/r06/r06l_*)
+    if (A.lq_mol != nullptr) s += A.lq_mol[M.m];
     if (tid == 0) A.ldj_mol[M.m] = s;
     bad = tid == 0 && !__builtin_isfinite(s);
   } else {

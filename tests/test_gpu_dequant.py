@@ -1,9 +1,10 @@
-"""The ArgMax dequantisation ahead of the flow kernel (ABI 13, dequant_kernel):
-the same draws and values as the dequantisation fused into the flow kernel
-(enflow_set_dequant_ahead(0)) -- outputs bitwise equal, log|detJ| within
-round-off (its sum order differs), training gradients bitwise equal -- on
-every fused instance, with the caller's noise and with in-kernel draws, and
-against the float64 oracle.  Reference: enflow/nn/argmax.py:13-25,
+"""The ArgMax dequantisation ahead of the flow kernel (ABI 13, dequant_kernel;
+batches of more molecules than the device has CUs): the same draws and values
+as the dequantisation fused into the flow kernel (enflow_set_dequant_ahead(0))
+-- outputs bitwise equal, log|detJ| within round-off (its sum order differs),
+training gradients bitwise equal -- on every fused instance, with the
+caller's noise and with in-kernel draws, and against the float64 oracle;
+smaller batches keep the fused form.  Reference: enflow/nn/argmax.py:13-25,
 enflow/flow/dynamics.py:10-24."""
 import numpy as np
 import pytest
@@ -49,7 +50,11 @@ def _run(model, d, eps, ahead, key_seed):
     return o, ldj, set(t.stats)
 
 
-@pytest.mark.parametrize("mols,atoms,hid", [(1024, 22, 128), (48, 60, 64)])
+def _cus():
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+@pytest.mark.parametrize("mols,atoms,hid", [(1024, 22, 128), (300, 60, 64)])
 @pytest.mark.parametrize("draws", ["caller", "kernel"])
 def test_dequant_ahead_equals_fused(mols, atoms, hid, draws, kernel_instance):
     from enflow_amd.data import Data
@@ -61,7 +66,7 @@ def test_dequant_ahead_equals_fused(mols, atoms, hid, draws, kernel_instance):
            if draws == "caller" else None)
     o1, l1, k1 = _run(model, d, eps, True, 93)
     o0, l0, k0 = _run(model, d, eps, False, 93)
-    assert "dequant_kernel" in k1 and "dequant_kernel" not in k0, (k1, k0)
+    assert ("dequant_kernel" in k1) == (mols > _cus()) and "dequant_kernel" not in k0, (k1, k0)
     for k in ("h", "g", "pos", "vel"):
         assert torch.equal(getattr(o1, k), getattr(o0, k)), k
     ldj_d = abs(float(l1) - float(l0)) / abs(float(l0))
@@ -86,19 +91,22 @@ def test_dequant_ahead_equals_fused(mols, atoms, hid, draws, kernel_instance):
 
 def test_dequant_ahead_training_gradients_bitwise():
     """A training step (64-atom instance, the tape) with the dequantisation ahead
-    and fused: loss and every gradient bitwise equal."""
+    and fused: loss and every gradient bitwise equal; and a batch of at most
+    CU-count molecules keeps the fused form."""
     from enflow_amd import _lib
     from enflow_amd.data import Data
     from enflow_amd.flow import Alchemical_NLL
     from enflow_amd.data.synthetic import make_molecules, default_kBT
-    b = _f32(make_molecules(6, 40, nf=5, seed=95))
+    b = _f32(make_molecules(_cus() + 8, 40, nf=5, seed=95))
     eps = torch.randn((b["h"].shape[0], 5), device=DEV, generator=torch.Generator(DEV).manual_seed(96))
     grads, losses = [], []
     for ahead in (True, False):
         model = _model(64, 2, 97)
         prev = _lib.set_dequant_ahead(ahead)
         try:
-            out, ldj = model(Data.from_arrays(b, device=DEV), noise=eps)
+            with _lib.KernelTimer() as kt:
+                out, ldj = model(Data.from_arrays(b, device=DEV), noise=eps)
+            assert ("dequant_kernel" in kt.stats) == ahead, set(kt.stats)
             loss = Alchemical_NLL(kBT=default_kBT(), softening=0.1)(out, ldj)
             loss.backward()
             torch.cuda.synchronize()
@@ -110,3 +118,19 @@ def test_dequant_ahead_training_gradients_bitwise():
     print(f"training step, dequant ahead vs fused: loss {losses[0]:.9e} vs {losses[1]:.9e}, gradients bitwise {same}")
     assert same
     assert abs(losses[0] - losses[1]) <= 1e-6 * abs(losses[1])
+
+
+def test_small_batch_keeps_fused_dequant():
+    """At most CU-count molecules (the latency / split instances' batches): no
+    dequant_kernel launch, outputs as with the setting off."""
+    from enflow_amd.data import Data
+    from enflow_amd.data.synthetic import make_molecules
+    b = _f32(make_molecules(128, 22, nf=5, seed=98))
+    model = _model(128, 2, 99)
+    d = Data.from_arrays(b, device=DEV)
+    o1, l1, k1 = _run(model, d, None, True, 100)
+    o0, l0, k0 = _run(model, d, None, False, 100)
+    assert "dequant_kernel" not in k1 and "dequant_kernel" not in k0, (k1, k0)
+    for k in ("h", "g", "pos", "vel"):
+        assert torch.equal(getattr(o1, k), getattr(o0, k)), k
+    assert float(l1) == float(l0)

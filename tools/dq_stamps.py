@@ -3,7 +3,7 @@
 with in-kernel draws and with the caller's noise.  Uses the stamps library
 (tools/stamps.py build; -DENFLOW_STAMPS, never the product).
 
-    python tools/dq_stamps.py [MOLS]
+    python tools/dq_stamps.py [MOLS] [lib.so]
 """
 import ctypes
 import json
@@ -18,7 +18,7 @@ PHASES = ["load + network.2 staging", "hidden layer", "barriers", "network outpu
 
 def main():
     mols = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-    os.environ["ENFLOW_LIB"] = SO
+    os.environ["ENFLOW_LIB"] = os.path.abspath(sys.argv[2]) if len(sys.argv) > 2 else SO
     sys.path.insert(0, ROOT)
     import torch
     import bench
