@@ -514,13 +514,26 @@ static void launch_flow_v(int prec, int num_mols, hipStream_t st, const FlowArgs
     (void)prec; (void)num_mols; (void)st; (void)A;
     return;
   } else {
-    hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    if (A.dequant_kind != ENFLOW_DEQUANT_ARGMAX)
+      hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR, false>), dim3(num_mols), dim3(BLOCK), 0, st, A);
+    else
+      hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A);
     return;
   }
 #endif
 #ifdef ENFLOW_DEV_ONLY
   if constexpr (REV || VAR) return;
 #endif
+  if constexpr (!REV && !VAR && NN <= 64) {
+    // the split-precision forward without the fused ArgMax path when the
+    // dequantisation ran ahead (or is Floor / none)
+    if (prec == ENFLOW_PREC_F16X3 && A.dequant_kind != ENFLOW_DEQUANT_ARGMAX) {
+      ENFLOW_TIMED("lf_flow_kernel<fwd>", st,
+                   hipLaunchKernelGGL((lf_flow_kernel<HH, NN, false, PREC_F16X3, RBB, false, false>), dim3(num_mols),
+                                      dim3(BLOCK), 0, st, A));
+      return;
+    }
+  }
   if (prec == ENFLOW_PREC_F16X3)
     ENFLOW_TIMED(REV ? "lf_flow_kernel<rev>" : "lf_flow_kernel<fwd>", st,
                  hipLaunchKernelGGL((lf_flow_kernel<HH, NN, REV, PREC_F16X3, RBB, VAR>), dim3(num_mols), dim3(BLOCK), 0, st, A));

@@ -679,14 +679,11 @@ __global__ void __launch_bounds__(BLOCK, 1) lf_fs_kernel(FlowArgs A, FsArgs X) {
     STAMP(0);
     if (!REV) {
       if (A.lq_mol != nullptr && half == 0 && tid == 0) ldj += A.lq_mol[m];   // dequantised ahead (dequant_kernel)
-#ifndef ENFLOW_NO_FUSED_ARGMAX
       if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
         // every atom in both halves (the same draws); half 0 counts log_q
         const float lq = argmax_dequant<H, NMX, NMX, false, true>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
         if (half == 0) ldj += lq;
-      } else
-#endif
-      if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+      } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
         for (int e = tid; e < n * nf; e += BLOCK) {
           const int a = e / nf, q = e - a * nf;
           sm.h[a * NFP + q] += A.dequant_scale * A.noise_src().uniform((size_t)M.a0 * nf + e);

@@ -42,7 +42,11 @@ __device__ __forceinline__ void ticket_reduce_ldj(const FlowArgs& A, double* red
   }
 }
 
-template <int H, int NMAX, bool REV, int PREC, int RB, bool VAR>
+// FDQ = false: an instance without the fused ArgMax dequantisation, for launches
+// whose dequantisation ran ahead (dequant_kernel) or is Floor / none -- the
+// unused ArgMax path otherwise costs the layer loop ~1.4 % in code generation
+// (profiles/r06/r06n_*: 0.7099 ms with it, ~0.700 without)
+template <int H, int NMAX, bool REV, int PREC, int RB, bool VAR, bool FDQ = true>
 __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLOW_WAVES_PER_SIMD))
     lf_flow_kernel(FlowArgs A) {
   __shared__ Smem<H, NMAX, RB> sm;
@@ -82,12 +86,9 @@ __global__ void __launch_bounds__(BLOCK, (RB < NMAX ? ENFLOW_BLOCKED_WPS : ENFLO
   };
 
   if (!REV) {
-#ifndef ENFLOW_NO_FUSED_ARGMAX
-    if (A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
-      ldj += argmax_dequant<H, NMAX, RB, VAR>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
-    } else
-#endif
-    if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
+    if (FDQ && A.dequant_kind == ENFLOW_DEQUANT_ARGMAX) {
+      if constexpr (FDQ) ldj += argmax_dequant<H, NMAX, RB, VAR>(sm, A.dequant, A.noise_src(), M.a0, n, nf);
+    } else if (A.dequant_kind == ENFLOW_DEQUANT_FLOOR) {
       for (int e = tid; e < n * nf; e += BLOCK) {
         const int a = e / nf, q = e - a * nf;
         sm.h[a * NFP + q] += A.dequant_scale * A.noise_src().uniform((size_t)M.a0 * nf + e);

@@ -35,12 +35,22 @@ def one_hot(index, num_classes=None, dtype=None):
 
 
 def mol_ptr_from_counts(N, device=None):
-    """CSR atom offsets (int32, [M+1]) from per-molecule atom counts Data.N."""
+    """CSR atom offsets (int32, [M+1]) from per-molecule atom counts Data.N.
+    Host counts (the reference's Data.N) are summed on the host into pinned
+    memory and copied asynchronously: one queued copy instead of a synchronous
+    pageable copy and three small kernels (~25 us of every module call on a
+    fresh batch, profiles/r06/r06n_module_call_cprofile.txt)."""
     N = torch.as_tensor(N)
     if N.ndim == 0:
         N = N.reshape(1)
-    ptr = torch.zeros(N.numel() + 1, dtype=torch.int32, device=device if device is not None else N.device)
-    ptr[1:] = torch.cumsum(N.to(ptr.device), 0).to(torch.int32)
+    dev = torch.device(device) if device is not None else N.device
+    if N.device.type == "cpu":
+        host = torch.empty(N.numel() + 1, dtype=torch.int32, pin_memory=dev.type == "cuda")
+        host[0] = 0
+        torch.cumsum(N, 0, dtype=torch.int32, out=host[1:])
+        return host if dev.type == "cpu" else host.to(dev, non_blocking=True)
+    ptr = torch.zeros(N.numel() + 1, dtype=torch.int32, device=dev)
+    ptr[1:] = torch.cumsum(N.to(dev), 0).to(torch.int32)
     return ptr
 
 
