@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <math.h>
+#include <type_traits>
 
 #include "enflow_hip.h"
 #include "enflow_timing.h"
@@ -2306,6 +2307,7 @@ __device__ __forceinline__ void node_phase_x3_f(Smem<H, NMAX, RB>& sm, const flo
 // form's order, so both forms give bitwise the same z
 template <int H, int NMAX, int RB>
 struct DqSmem {
+  static constexpr int HIDDEN_AU = 4;   // atoms per LDS round trip in the hidden layer
   static constexpr int AST = H + 4;
   static constexpr bool W1X_LDS = NMAX <= 32;
   float h[NMAX * NFP];
@@ -2356,6 +2358,14 @@ struct NoiseSrc {
 // (the whole-tile instances: the parallel form measured no faster there and
 // moved register spills into the layer loop, profiles/r05/r05w_*, r05z2 PMC)
 // S: the flow kernels' Smem image, or DqSmem (dequant_kernel's own image)
+// atoms per step of argmax_dequant's hidden layer: S::HIDDEN_AU where the image
+// names it (dequant_kernel: four, its rows read before any activation is
+// stored), else one (inside the fused kernels the blocked form measured ~1 %
+// slower on the split instance, profiles/r06/r06o_*)
+template <class S, class = void>
+struct HiddenAU { static constexpr int v = 1; };
+template <class S>
+struct HiddenAU<S, std::void_t<decltype(S::HIDDEN_AU)>> { static constexpr int v = S::HIDDEN_AU; };
 // dqst (diagnostic stamps builds, dequant_kernel only): per-phase cycles, [7] the last stamp
 #ifdef ENFLOW_STAMPS
 #define DQS(k)                                              \
@@ -2413,9 +2423,9 @@ __device__ __forceinline__ float argmax_dequant(S& sm, const float* __restrict__
         float w1[NFMAX];
 #pragma unroll
         for (int q = 0; q < NFMAX; ++q) w1[q] = q < nf ? Dp[L.wa1t + q * H + k] : 0.f;
-        // four atoms per step, their h rows read before any activation is stored
-        // (one LDS round trip per four atoms; the same fma sequence per atom)
-        constexpr int AU = 4;
+        // AU atoms per step, their h rows read before any activation is stored
+        // (one LDS round trip per AU atoms; the same fma sequence per atom)
+        constexpr int AU = HiddenAU<S>::v;
         for (int a = grp; a < cn; a += AU * NG) {
           float v[AU];
 #pragma unroll
