@@ -2133,7 +2133,23 @@ __global__ void __launch_bounds__(256) reduce_part_kernel(OuterBatch ob) {
   double s = 0.0;
   const int G = nch >> 2;
   if (live) {
-    for (int g = 0; g < G; ++g) s += (double)src[(size_t)(4 * g + sub) * cs];
+    // eight chunk groups per step into independent sums (eight loads in flight
+    // per lane; the partials are read once: non-temporal), combined in a fixed
+    // order: deterministic
+    constexpr int U = 8;
+    double su[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) su[u] = 0.0;
+    int g = 0;
+    for (; g + U <= G; g += U) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(&src[(size_t)(4 * (g + u) + sub) * cs]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) su[u] += (double)v[u];
+    }
+    for (; g < G; ++g) su[0] += (double)__builtin_nontemporal_load(&src[(size_t)(4 * g + sub) * cs]);
+    s = ((su[0] + su[1]) + (su[2] + su[3])) + ((su[4] + su[5]) + (su[6] + su[7]));
     if (sub == 0)
       for (int ch = 4 * G; ch < nch; ++ch) s += (double)src[(size_t)ch * cs];
   }
