@@ -2418,7 +2418,7 @@ __device__ __forceinline__ float argmax_dequant(S& sm, const float* __restrict__
         // network.0's column k in registers, requested once: inside the atom loop
         // the loads (a runtime-length inner loop) were issued per atom, each
         // iteration waiting on an L2 round trip (~9 k cycles of a ~30 k-cycle
-        // dequantisation, profiles/r06/r06h_*); the same fma sequence (q ascending)
+        // dequantisation, profiles/r06/r06l_dq_stamps.txt); the same fma sequence (q ascending)
         const float b = Dp[L.ba1 + k];
         float w1[NFMAX];
 #pragma unroll
